@@ -1,0 +1,234 @@
+"""Headline benchmark: Golay(24,12) INT4 encode+decode on [B=8, L=4096, H=32, D=128].
+
+Metric (BASELINE.json): "INT4 codewords/sec encode+decode (Golay24, L=4096) +
+achieved HBM GB/s", configuration 3: Golay(24,12) triplet encode+decode on
+[8,4096,32,128] at BER 1e-2 on one MI355X.
+
+One step = golay_encode of the per-head-padded triplets (ecc_shim.py packing:
+D=128 -> 129 -> 43 codewords per head, M = 45,088,768 codewords) followed by
+golay_decode of those codewords corrupted at BER 1e-2 (the corruption is
+injected once, before timing, with the reference's Philox stream; its own
+throughput is measured separately and reported under "inject").  Inputs are
+resident in HBM before the timed region; statistics stay on the device.
+
+Multi-GPU (torchrun, one process per GPU): weak scaling -- every rank owns its
+own [8,4096,32,128] shard (global codeword offset rank*M, so the fault pattern
+equals a single-device run over the concatenated tensor); no collective in the
+data path, one RCCL all_reduce of the decode statistics after timing.
+
+Prints ONE JSON line on rank 0.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+B, L, H, D = 8, 4096, 32, 128
+BER = 1e-2
+SEED = 42
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DECODE_BYTES_PER_CW = 8  # 4 B codeword in, 3 B triplet + 1 B count out
+ENCODE_BYTES_PER_CW = 7  # 3 B triplet in, 4 B codeword out
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="time budget of the CPU baseline sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-inject", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(budget_s):
+    """The C oracle (a single-threaded port of the reference path) timed on the
+    host: Golay encode + decode of a bounded sample of the same workload."""
+    import numpy as np
+    from oracle import oracle
+    oracle.lib()
+    g = np.random.default_rng(0)
+    m = 1 << 18
+    trip = g.integers(0, 16, size=(m, 3), dtype=np.int64).astype(np.uint8)
+    cw = oracle.golay_encode(trip)
+    noisy, _, _ = oracle.inject(cw[: 1 << 12], BER, 24, SEED)  # keep it cheap; decode sees errors
+    cw[: 1 << 12] = noisy
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.golay_encode(trip)
+        oracle.golay_decode(cw)
+        done += m
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
+            "sample": f"{done} codewords ({done // m} x {m}) Golay encode+decode, "
+                      f"{el:.1f} s, oracle/kvecc_oracle.c single thread"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import kvecc
+    from kvecc import ops
+    kvecc.require_hip()
+
+    # ---- synthetic INT4 KV tensor, resident in HBM ---------------------------
+    gen = torch.Generator().manual_seed(rank)
+    x = torch.randint(0, 16, (B, L, H, D), generator=gen, dtype=torch.uint8).to(dev)
+    gsz = (D + 2) // 3                      # 43 codewords per head vector
+    trip = torch.zeros(B, L, H, gsz * 3, dtype=torch.uint8, device=dev)
+    trip[..., :D] = x                        # ecc_shim.py:669-679 per-head padding
+    trip = trip.view(-1, 3)
+    m = trip.shape[0]
+    del x
+    cw = torch.empty(m, dtype=torch.int32, device=dev)
+    ops.golay_encode_into(trip.view(-1), cw, m)
+    noisy = torch.empty_like(cw)
+    inj_stats = ops.new_stats(dev)
+    ops.inject_into(cw, noisy, BER, 24, seed=SEED, stats=inj_stats, global_n=m * world,
+                    offset0=rank * m)
+    out_trip = torch.empty(m * 3, dtype=torch.uint8, device=dev)
+    counts = torch.empty(m, dtype=torch.uint8, device=dev)
+    stats = ops.new_stats(dev)
+    torch.cuda.synchronize()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record()
+        ops.golay_encode_into(trip.view(-1), cw, m)
+        if ev is not None:
+            ev[1].record()
+        ops.golay_decode_into(noisy, out_trip, counts, stats)
+        if ev is not None:
+            ev[2].record()
+
+    for _ in range(args.warmup):
+        step()
+    stats.zero_()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+
+    elapsed = t1 - t0
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    tt = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
+    st = stats.clone()
+    if dist is not None:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)     # the single stats all-reduce
+    elapsed, enc_ms, dec_ms = tt.tolist()
+    bits, unc = st.tolist()
+
+    # ---- correctness spot check (outside timing) -----------------------------
+    ref_trip, ref_stats = None, None
+    if rank == 0:
+        chk = ops.new_stats(dev)
+        ops.golay_decode_into(cw, out_trip, counts, chk)  # clean codewords round-trip
+        torch.cuda.synchronize()
+        assert torch.equal(out_trip.view(-1, 3), trip), "encode->decode round trip failed"
+        assert chk.tolist() == [0, 0]
+
+    # ---- injection throughput (VALU-bound, Philox4x32-10 per bit) ------------
+    inject = None
+    if not args.no_inject:
+        reps = 3
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ops.inject_into(cw, noisy, BER, 24, seed=SEED, global_n=m * world, offset0=rank * m)
+        e0.record()
+        for _ in range(reps):
+            ops.inject_into(cw, noisy, BER, 24, seed=SEED, global_n=m * world, offset0=rank * m)
+        e1.record()
+        torch.cuda.synchronize()
+        inj_ms = e0.elapsed_time(e1) / reps
+        inject = {"ms": round(inj_ms, 4), "codewords_per_s": m / (inj_ms * 1e-3),
+                  "philox_per_s": m * 24 / (inj_ms * 1e-3), "flips": int(inj_stats[0]),
+                  "bound": "valu"}
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    total_cw = m * world * args.steps
+    value = total_cw / elapsed
+    dec_gbs = DECODE_BYTES_PER_CW * m / (dec_ms * 1e-3) / 1e9
+    enc_gbs = ENCODE_BYTES_PER_CW * m / (enc_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("golay_decode_bytes_per_launch")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+    line = {
+        "metric": "INT4 codewords/sec encode+decode (Golay24, L=4096) + achieved HBM GB/s",
+        "value": value,
+        "unit": "codewords/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/int32 (bitwise)",
+        "data": "synthetic: torch.randint(0,16) INT4 nibbles, seed=rank; BER 1e-2 Philox corruption",
+        "config": {"workload": "golay24 per-head encode+decode, [B=8,L=4096,H=32,D=128] per GPU",
+                   "codewords_per_gpu": m, "ber": BER, "seed": SEED, "parallelism": f"dp{world}",
+                   "global_batch": B * world, "seq_len": L},
+        "hbm_gbs": {"decode": dec_gbs, "encode": enc_gbs,
+                    "round_trip": (DECODE_BYTES_PER_CW + ENCODE_BYTES_PER_CW) * m
+                    / ((enc_ms + dec_ms) * 1e-3) / 1e9},
+        "kernel_ms": {"encode": enc_ms, "decode": dec_ms},
+        "roofline": {"bound": "hbm", "achieved": dec_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": dec_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "golay_decode_kernel", "bytes_per_launch": DECODE_BYTES_PER_CW * m},
+        "decode_stats": {"bits_corrected": bits, "uncorrectable": unc, "steps": args.steps},
+        "inject": inject,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

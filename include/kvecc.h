@@ -1,0 +1,153 @@
+/*
+ * kvecc.h -- C ABI of the MI355X-native ECC KV-cache codec (libkvecc.so).
+ *
+ * This is the drop-in boundary for the reference's hot path,
+ * ecc_codecs/triton_kernels/ (Hamming(7,4)/(8,4), Golay(24,12), Bernoulli bit
+ * flip injection, double-error interpolation, fused quantize/encode and
+ * decode/dequantize).  The reference exposes these as Python functions over
+ * torch tensors; each entry point below replaces the Triton kernel + wrapper
+ * cited next to it (paths relative to the reference repository root).  The
+ * Python host package `kvecc` binds them with ctypes.
+ *
+ * Conventions (all entry points):
+ *   - Pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless the
+ *     name ends in _host.  Buffers must not overlap unless stated.
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).  Calls only
+ *     enqueue work: no allocation, no host synchronisation (graph-capturable
+ *     once kvecc_init_device() has run for the device).
+ *   - Statistics accumulate (+=) into a caller-provided device uint64_t array,
+ *     or are skipped when the pointer is NULL.  Zero it to start a count.
+ *   - Return 0 on success, a negative KVECC_E* code on failure; the message is
+ *     available from kvecc_last_error() (thread-local).
+ *   - n / m / rows == 0 is valid and enqueues nothing.
+ */
+#ifndef KVECC_H
+#define KVECC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KVECC_API __attribute__((visibility("default")))
+
+enum {
+  KVECC_OK = 0,
+  KVECC_EINVAL = -1, /* bad argument (null pointer, negative size, bad enum) */
+  KVECC_EHIP = -2,   /* HIP runtime error (launch / memory)                  */
+  KVECC_ENODEV = -3  /* no HIP device                                         */
+};
+
+/* dtype codes for fused kernels */
+enum { KVECC_F32 = 0, KVECC_F16 = 1, KVECC_BF16 = 2 };
+/* codec codes for fused kernels */
+enum { KVECC_CODEC_NONE = 0, KVECC_CODEC_H74 = 1, KVECC_CODEC_H84 = 2 };
+
+/* ---- runtime --------------------------------------------------------------- */
+KVECC_API const char *kvecc_version(void);
+KVECC_API const char *kvecc_last_error(void);
+KVECC_API int kvecc_device_count(void);
+/* Upload the Golay tables to `device` (done lazily otherwise; call before graph
+ * capture).  Replaces golay_triton.py:304-330 (_build_syndrome_table cache). */
+KVECC_API int kvecc_init_device(int device);
+/* Host copies of the code tables the kernels use (for verification):
+ *   syndrome table as the reference builds it, config.py:403-457 -> int32[4096]
+ *   H row masks, config.py:354-379 -> uint32[12]                              */
+KVECC_API int kvecc_golay_syndrome_table_host(int32_t *out4096);
+KVECC_API int kvecc_golay_h_row_masks_host(uint32_t *out12);
+/* Integer form of the reference's `tl.rand(..) < ber` test (random.py:126-143):
+ * the smallest folded 31-bit value x with fp32(x)*0x2FFFFFFF >= fp32(ber). */
+KVECC_API uint32_t kvecc_ber_threshold(float ber);
+
+/* ---- Hamming(7,4) / Hamming(8,4) ------------------------------------------ */
+/* hamming74_triton.py:48-91 + :170-201 */
+KVECC_API int kvecc_hamming74_encode(const uint8_t *in, uint8_t *out, int64_t n, void *stream);
+/* hamming74_triton.py:100-162 + :218-277 ; stats[0] += #syndrome != 0 */
+KVECC_API int kvecc_hamming74_decode(const uint8_t *cw, uint8_t *data, uint8_t *flag,
+                                     int64_t n, uint64_t *stats, void *stream);
+/* hamming84_triton.py:50-108 + :217-254 */
+KVECC_API int kvecc_hamming84_encode(const uint8_t *in, uint8_t *out, int64_t n, void *stream);
+/* hamming84_triton.py:117-209 + :281-351 ; error_type may be NULL;
+ * stats[0] += #SINGLE_CORRECTED, stats[1] += #DOUBLE_DETECTED */
+KVECC_API int kvecc_hamming84_decode(const uint8_t *cw, uint8_t *data, uint8_t *error_type,
+                                     int64_t n, uint64_t *stats, void *stream);
+
+/* ---- Golay(24,12) ------------------------------------------------------------ */
+/* golay_triton.py:99-157 + :382-422 ; triplets uint8[m][3] -> int32[m] */
+KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, int64_t m,
+                                 void *stream);
+/* golay_triton.py:213-295 + :425-498 ; counts may be NULL;
+ * stats[0] += sum of counts < 4 (bits corrected), stats[1] += #count == 4 */
+KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, uint8_t *counts,
+                                 int64_t m, uint64_t *stats, void *stream);
+/* Per-head packing of the shim (ecc_shim.py:623-624,669-682): each row of d
+ * nibbles is zero-padded to 3*ceil(d/3) and encoded to ceil(d/3) codewords. */
+KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords, int64_t rows,
+                                      int64_t d, void *stream);
+/* Inverse of the above (ecc_shim.py:990-1008): decoded rows of d nibbles. */
+KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles,
+                                      int64_t rows, int64_t d, uint64_t *stats, void *stream);
+
+/* ---- Bernoulli bit-flip injection ------------------------------------------- */
+/* fault_injection_triton.py:228-299 (uint8) and :303-334 (int32), wrapper
+ * :337-424.  Element i is global element offset0+i of a global_n-element flat
+ * tensor (pass global_n = n, offset0 = 0 for the unsharded call), so shards
+ * reproduce the single-device flip pattern.  counts (uint8 per element) may be
+ * NULL; stats[0] += flips, stats[1] += elements with >=1 flip.  in == out is
+ * allowed (in-place). */
+KVECC_API int kvecc_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
+                              int n_bits, int64_t seed, float ber, int64_t global_n,
+                              int64_t offset0, uint64_t *stats, void *stream);
+KVECC_API int kvecc_inject_i32(const int32_t *in, int32_t *out, uint8_t *counts, int64_t n,
+                               int n_bits, int64_t seed, float ber, int64_t global_n,
+                               int64_t offset0, uint64_t *stats, void *stream);
+/* rand4x variants, fault_injection_triton.py:57-133 / :137-224 / :434-496 */
+KVECC_API int kvecc_inject_u8_vectorized(const uint8_t *in, uint8_t *out, uint8_t *counts,
+                                         int64_t n, int n_bits, int64_t seed, float ber,
+                                         uint64_t *stats, void *stream);
+KVECC_API int kvecc_inject_i32_vectorized(const int32_t *in, int32_t *out, uint8_t *counts,
+                                          int64_t n, int n_bits, int64_t seed, float ber,
+                                          uint64_t *stats, void *stream);
+/* Per-row scheme of the shim (ecc_shim.py:643-651,684-691,713-721): row r
+ * (row_len elements, contiguous, rows back to back) is injected as its own
+ * call with N = row_len and seed = seed_base + r.  in == out allowed. */
+KVECC_API int kvecc_inject_rows_u8(const uint8_t *in, uint8_t *out, int64_t rows,
+                                   int64_t row_len, int n_bits, int64_t seed_base, float ber,
+                                   uint64_t *stats, void *stream);
+KVECC_API int kvecc_inject_rows_i32(const int32_t *in, int32_t *out, int64_t rows,
+                                    int64_t row_len, int n_bits, int64_t seed_base, float ber,
+                                    uint64_t *stats, void *stream);
+
+/* ---- Interpolation ----------------------------------------------------------- */
+/* interpolation_triton.py:120-159 + :162-265 on a contiguous [outer][len][inner]
+ * uint8 array whose sequence axis is the middle one (no permute copies).
+ * err == 2 elements become round_half_up((q[l-1]+q[l+1])/2) from clamped
+ * neighbours, every element is clamped to [0,15] -- unless `gate` is non-NULL
+ * and *gate == 0 (device int32), in which case out = q (the reference's
+ * no-double fast path, :199-201, decided on the device). */
+KVECC_API int kvecc_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
+                                int64_t outer, int64_t len, int64_t inner, const int32_t *gate,
+                                void *stream);
+/* *flag = (any x[i] == value) ? 1 : 0 (device int32, overwritten). */
+KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int32_t *flag,
+                                 void *stream);
+
+/* ---- Fused quantize / encode and decode / dequantize ----------------------- */
+/* fused_kernels.py:18-160 (H84), :163-269 (H74), and the shim's torch path
+ * ecc_shim.py:572-580: per row of d values (dtype x_dtype), scale = absmax/7
+ * (0 -> 1), q = rint(x/scale) clamped [-8,7] + 8, then encoded with `codec`
+ * (KVECC_CODEC_NONE stores the raw nibble).  scales: fp32 per row. */
+KVECC_API int kvecc_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
+                                         float *scales, int64_t rows, int64_t d, void *stream);
+/* fused_kernels.py:272-437 : H84 decode + (q-8)*scale -> out (out_dtype).
+ * zero_doubles = 1 reproduces :344 (double-error data -> 0).
+ * stats[0] += #SINGLE_CORRECTED, stats[1] += #DOUBLE_DETECTED. */
+KVECC_API int kvecc_decode_dequant_h84_rows(const uint8_t *cw, const float *scales, void *out,
+                                            int out_dtype, int64_t rows, int64_t d,
+                                            int zero_doubles, uint64_t *stats, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KVECC_H */

@@ -1,0 +1,330 @@
+// golay.hip -- extended Golay(24,12) encode/decode of INT4 triplets.
+//
+// Reference: ecc_codecs/triton_kernels/golay_triton.py:99-157 (encode) and
+// :213-295 (decode).  Codeword = data12 | parity12 << 12 with
+// data12 = n0 | n1 << 4 | n2 << 8.
+//
+// gfx950 design (HBM-bound, 7 B/codeword encode, 8 B/codeword decode):
+//  * Two 4096-entry uint16 tables live in LDS (16 KiB per workgroup):
+//      parity[d]  = the 12 parity bits of data word d
+//      correct[s] = data-error(12) | count(3) << 12 for syndrome s
+//    so encode is one LDS gather per codeword, and decode is two: the
+//    syndrome is (cw >> 12) ^ parity[cw & 0xFFF] (H = [B^T | I], B symmetric)
+//    instead of the reference's 12 masked popcounts, and the correction comes
+//    from `correct`, which folds the reference's error-pattern table and its
+//    popcount.  Only the data half of an error pattern matters for the output.
+//  * Each lane owns 16 codewords as 4 groups of 4 consecutive codewords, and
+//    each wave-instruction covers one contiguous span (1 KiB of codewords,
+//    768 B of triplets, 256 B of counts), so every access is fully coalesced:
+//    4 x global_load_dwordx4 (codewords) and 4 x (dwordx3 + dword) stores.
+//  * Workgroups walk a contiguous chunk of tiles (grid-stride) so the 16 KiB
+//    table fill is amortised over many tiles.
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+constexpr int kCwPerLane = 16;
+constexpr int kTile = kBlock * kCwPerLane;  // 4096 codewords per workgroup tile
+
+// copy both 4096-entry tables (16 KiB) into LDS
+__device__ __forceinline__ void load_tables(uint16_t *lds, const uint16_t *__restrict__ par,
+                                            const uint16_t *__restrict__ cor, bool need_cor) {
+  const u32x4 *p = reinterpret_cast<const u32x4 *>(par);
+  u32x4 *l = reinterpret_cast<u32x4 *>(lds);
+  // 8 KiB = 512 x 16 B per table
+  for (int i = threadIdx.x; i < 512; i += kBlock) l[i] = p[i];
+  if (need_cor) {
+    const u32x4 *c = reinterpret_cast<const u32x4 *>(cor);
+    for (int i = threadIdx.x; i < 512; i += kBlock) l[512 + i] = c[i];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t pack_data(uint32_t b0, uint32_t b1, uint32_t b2) {
+  return (b0 & 0xFu) | (b1 & 0xFu) << 4 | (b2 & 0xFu) << 8;
+}
+
+// 12-bit data word -> its three nibbles in three consecutive bytes
+__device__ __forceinline__ uint32_t spread_nibbles(uint32_t d) {
+  return (d & 0xFu) | (d & 0xF0u) << 4 | (d & 0xF00u) << 8;
+}
+
+// ---- encode -------------------------------------------------------------------
+
+// 4 consecutive triplets (12 bytes, little endian in 3 words) -> 4 data words
+__device__ __forceinline__ void unpack_triplets(uint32_t w0, uint32_t w1, uint32_t w2,
+                                                uint32_t d[4]) {
+  d[0] = pack_data(w0, w0 >> 8, w0 >> 16);
+  d[1] = pack_data(w0 >> 24, w1, w1 >> 8);
+  d[2] = pack_data(w1 >> 16, w1 >> 24, w2);
+  d[3] = pack_data(w2 >> 8, w2 >> 16, w2 >> 24);
+}
+
+__global__ __launch_bounds__(kBlock) void golay_encode_kernel(const uint32_t *__restrict__ trip,
+                                                              u32x4 *__restrict__ cw,
+                                                              int64_t ntiles,
+                                                              const uint16_t *__restrict__ par) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[4096];
+  load_tables(lds, par, nullptr, false);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    // codeword index of this lane's group g: tile*4096 + wave*1024 + g*256 + lane*4
+    const int64_t base = t * kTile + wave * (kWave * kCwPerLane) + lane * 4;
+    uint32_t w[4][3];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint32_t *p = trip + (base + g * 256) * 3 / 4;  // 12 B per 4 codewords
+      w[g][0] = ld_stream(p);
+      w[g][1] = ld_stream(p + 1);
+      w[g][2] = ld_stream(p + 2);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint32_t d[4];
+      unpack_triplets(w[g][0], w[g][1], w[g][2], d);
+      u32x4 out;
+      out.x = d[0] | (uint32_t)lds[d[0]] << 12;
+      out.y = d[1] | (uint32_t)lds[d[1]] << 12;
+      out.z = d[2] | (uint32_t)lds[d[2]] << 12;
+      out.w = d[3] | (uint32_t)lds[d[3]] << 12;
+      st_stream(cw + (base + g * 256) / 4, out);
+    }
+  }
+}
+
+// scalar path: codewords [begin, m), any alignment
+__global__ __launch_bounds__(kBlock) void golay_encode_tail_kernel(const uint8_t *__restrict__ trip,
+                                                                   int32_t *__restrict__ cw,
+                                                                   int64_t begin, int64_t m,
+                                                                   const uint16_t *__restrict__ par) {
+  for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * kBlock) {
+    uint32_t d = pack_data(trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]);
+    cw[i] = (int32_t)(d | (uint32_t)par[d] << 12);
+  }
+}
+
+// ---- decode -------------------------------------------------------------------
+
+struct GolayStats {
+  uint32_t bits = 0, unc = 0;
+};
+
+// returns the 12-bit data word, count in `c`
+__device__ __forceinline__ uint32_t decode_one(uint32_t w, const uint16_t *lds, uint32_t &c) {
+  uint32_t lo = w & 0xFFFu;
+  uint32_t syn = ((w >> 12) & 0xFFFu) ^ lds[lo];
+  uint32_t e = lds[4096 + syn];
+  c = e >> 12;  // 0..3 corrected bits, 4 = uncorrectable (data kept)
+  return lo ^ (e & 0xFFFu);
+}
+
+template <bool WITH_COUNTS, bool WITH_STATS>
+__global__ __launch_bounds__(kBlock) void golay_decode_kernel(const u32x4 *__restrict__ cw,
+                                                              uint32_t *__restrict__ trip,
+                                                              uint32_t *__restrict__ counts,
+                                                              int64_t ntiles,
+                                                              const uint16_t *__restrict__ par,
+                                                              const uint16_t *__restrict__ cor,
+                                                              uint64_t *__restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[8192];
+  load_tables(lds, par, cor, true);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  uint32_t bits = 0, unc = 0;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t base = t * kTile + wave * (kWave * kCwPerLane) + lane * 4;
+    u32x4 v[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) v[g] = ld_stream(cw + (base + g * 256) / 4);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      uint32_t c0, c1, c2, c3;
+      uint32_t e0 = spread_nibbles(decode_one(v[g].x, lds, c0));
+      uint32_t e1 = spread_nibbles(decode_one(v[g].y, lds, c1));
+      uint32_t e2 = spread_nibbles(decode_one(v[g].z, lds, c2));
+      uint32_t e3 = spread_nibbles(decode_one(v[g].w, lds, c3));
+      uint32_t *p = trip + (base + g * 256) * 3 / 4;
+      st_stream(p, e0 | e1 << 24);
+      st_stream(p + 1, e1 >> 8 | e2 << 16);
+      st_stream(p + 2, e2 >> 16 | e3 << 8);
+      uint32_t cc = c0 | c1 << 8 | c2 << 16 | c3 << 24;
+      if (WITH_COUNTS) st_stream(counts + (base + g * 256) / 4, cc);
+      if (WITH_STATS) {
+        // bytes are 0..4: low two bits = corrected bits (0 for 4), bit 2 = uncorrectable
+        uint32_t lowbits = cc & 0x03030303u;
+        bits += (lowbits * 0x01010101u) >> 24;  // byte sum (max 12, no carry)
+        unc += __builtin_popcount(cc & 0x04040404u);
+      }
+    }
+  }
+  if (WITH_STATS) flush_stats2(stats, bits, unc);
+}
+
+__global__ __launch_bounds__(kBlock) void golay_decode_tail_kernel(
+    const int32_t *__restrict__ cw, uint8_t *__restrict__ trip, uint8_t *__restrict__ counts,
+    int64_t begin, int64_t m, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
+    uint64_t *__restrict__ stats) {
+  uint32_t bits = 0, unc = 0;
+  for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * kBlock) {
+    uint32_t w = (uint32_t)cw[i];
+    uint32_t lo = w & 0xFFFu;
+    uint32_t e = cor[((w >> 12) & 0xFFFu) ^ par[lo]];
+    uint32_t c = e >> 12;
+    uint32_t d = lo ^ (e & 0xFFFu);
+    trip[3 * i] = (uint8_t)(d & 0xF);
+    trip[3 * i + 1] = (uint8_t)(d >> 4 & 0xF);
+    trip[3 * i + 2] = (uint8_t)(d >> 8);
+    if (counts) counts[i] = (uint8_t)c;
+    bits += c & 3u;
+    unc += c >> 2;
+  }
+  if (stats) flush_stats2(stats, bits, unc);
+}
+
+// ---- per-head row packing (ecc_shim.py:623-682, :990-1008) -----------------------
+
+// one thread per codeword: row r, codeword j covers nibbles 3j..3j+2 (zero padded)
+__global__ __launch_bounds__(kBlock) void golay_encode_rows_kernel(
+    const uint8_t *__restrict__ nib, int32_t *__restrict__ cw, int64_t rows, int64_t d,
+    int64_t g, const uint16_t *__restrict__ par) {
+  const int64_t total = rows * g;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    int64_t r = i / g, j = i - r * g;
+    const uint8_t *row = nib + r * d;
+    int64_t c = 3 * j;
+    uint32_t b0 = row[c];
+    uint32_t b1 = c + 1 < d ? row[c + 1] : 0u;
+    uint32_t b2 = c + 2 < d ? row[c + 2] : 0u;
+    uint32_t dw = pack_data(b0, b1, b2);
+    cw[i] = (int32_t)(dw | (uint32_t)par[dw] << 12);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void golay_decode_rows_kernel(
+    const int32_t *__restrict__ cw, uint8_t *__restrict__ nib, int64_t rows, int64_t d, int64_t g,
+    const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
+    uint64_t *__restrict__ stats) {
+  const int64_t total = rows * g;
+  uint32_t bits = 0, unc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    int64_t r = i / g, j = i - r * g;
+    uint32_t w = (uint32_t)cw[i];
+    uint32_t lo = w & 0xFFFu;
+    uint32_t e = cor[((w >> 12) & 0xFFFu) ^ par[lo]];
+    uint32_t c = e >> 12;
+    uint32_t dd = lo ^ (e & 0xFFFu);
+    uint8_t *row = nib + r * d;
+    int64_t k = 3 * j;
+    row[k] = (uint8_t)(dd & 0xF);
+    if (k + 1 < d) row[k + 1] = (uint8_t)(dd >> 4 & 0xF);
+    if (k + 2 < d) row[k + 2] = (uint8_t)(dd >> 8);
+    bits += c & 3u;
+    unc += c >> 2;
+  }
+  if (stats) flush_stats2(stats, bits, unc);
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, int64_t m,
+                                 void *stream) {
+  if (m < 0) return set_error(KVECC_EINVAL, "golay_encode: negative m");
+  if (m == 0) return KVECC_OK;
+  if (!triplets || !codewords) return set_error(KVECC_EINVAL, "golay_encode: null pointer");
+  const uint16_t *par = golay_parity_table_dev();
+  if (!par) return KVECC_EHIP;
+  hipStream_t st = as_stream(stream);
+  int64_t done = 0;
+  if (aligned(triplets, 4) && aligned(codewords, 16)) {
+    int64_t ntiles = m / kTile;
+    if (ntiles > 0) {
+      unsigned g = grid_for(ntiles, 4, 8);  // >= ~4 tiles per workgroup
+      hipLaunchKernelGGL(golay_encode_kernel, dim3(g), dim3(kBlock), 0, st,
+                         reinterpret_cast<const uint32_t *>(triplets),
+                         reinterpret_cast<u32x4 *>(codewords), ntiles, par);
+    }
+    done = ntiles * kTile;
+  }
+  if (done < m) {
+    unsigned g = grid_for(m - done, kBlock);
+    hipLaunchKernelGGL(golay_encode_tail_kernel, dim3(g), dim3(kBlock), 0, st, triplets, codewords,
+                       done, m, par);
+  }
+  return check_launch("golay_encode");
+}
+
+KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, uint8_t *counts,
+                                 int64_t m, uint64_t *stats, void *stream) {
+  if (m < 0) return set_error(KVECC_EINVAL, "golay_decode: negative m");
+  if (m == 0) return KVECC_OK;
+  if (!triplets || !codewords) return set_error(KVECC_EINVAL, "golay_decode: null pointer");
+  const uint16_t *par = golay_parity_table_dev();
+  const uint16_t *cor = golay_correct_table_dev();
+  if (!par || !cor) return KVECC_EHIP;
+  hipStream_t st = as_stream(stream);
+  int64_t done = 0;
+  if (aligned(codewords, 16) && aligned(triplets, 4) && (!counts || aligned(counts, 4))) {
+    int64_t ntiles = m / kTile;
+    if (ntiles > 0) {
+      unsigned g = grid_for(ntiles, 4, 8);
+      auto c = reinterpret_cast<const u32x4 *>(codewords);
+      auto t = reinterpret_cast<uint32_t *>(triplets);
+      auto n = reinterpret_cast<uint32_t *>(counts);
+      if (counts && stats)
+        hipLaunchKernelGGL((golay_decode_kernel<true, true>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+      else if (counts)
+        hipLaunchKernelGGL((golay_decode_kernel<true, false>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+      else if (stats)
+        hipLaunchKernelGGL((golay_decode_kernel<false, true>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+      else
+        hipLaunchKernelGGL((golay_decode_kernel<false, false>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+    }
+    done = ntiles * kTile;
+  }
+  if (done < m) {
+    unsigned g = grid_for(m - done, kBlock);
+    hipLaunchKernelGGL(golay_decode_tail_kernel, dim3(g), dim3(kBlock), 0, st, codewords, triplets,
+                       counts, done, m, par, cor, stats);
+  }
+  return check_launch("golay_decode");
+}
+
+KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords, int64_t rows,
+                                      int64_t d, void *stream) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "golay_encode_rows: negative size");
+  if (rows == 0 || d == 0) return KVECC_OK;
+  if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "golay_encode_rows: null pointer");
+  const uint16_t *par = golay_parity_table_dev();
+  if (!par) return KVECC_EHIP;
+  int64_t g = (d + 2) / 3;
+  unsigned grid = grid_for(rows * g, kBlock);
+  hipLaunchKernelGGL(golay_encode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
+                     nibbles, codewords, rows, d, g, par);
+  return check_launch("golay_encode_rows");
+}
+
+KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles, int64_t rows,
+                                      int64_t d, uint64_t *stats, void *stream) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "golay_decode_rows: negative size");
+  if (rows == 0 || d == 0) return KVECC_OK;
+  if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "golay_decode_rows: null pointer");
+  const uint16_t *par = golay_parity_table_dev();
+  const uint16_t *cor = golay_correct_table_dev();
+  if (!par || !cor) return KVECC_EHIP;
+  int64_t g = (d + 2) / 3;
+  unsigned grid = grid_for(rows * g, kBlock);
+  hipLaunchKernelGGL(golay_decode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
+                     codewords, nibbles, rows, d, g, par, cor, stats);
+  return check_launch("golay_decode_rows");
+}
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+// interp.hip -- temporal interpolation of SECDED double-error positions.
+//
+// Reference: ecc_codecs/triton_kernels/interpolation_triton.py:120-159 (kernel)
+// and :162-265 (wrapper).  The kernel computes, in fp32,
+//   r   = err == 2 ? (q[l-1] + q[l+1]) * 0.5 : q[l]      (clamped neighbours)
+//   out = uint8(max(0, min(15, r + 0.5)))
+// With 8-bit integer inputs every step is exact in fp32, so this equals the
+// integer form  err == 2 ? min(15, (L + R + 1) >> 1) : min(15, q)  which the
+// kernels evaluate SWAR on four bytes per register.
+//
+// gfx950 design: the tensor is addressed as [outer][len][inner] with the
+// sequence axis in the middle, so any seq_dim is handled in place (the
+// reference permutes + copies to make it the last axis).  When inner is a
+// multiple of 16 each lane owns a 16-byte column chunk and walks kRows
+// consecutive sequence positions, so every q row is loaded once per lane
+// (plus a one-row halo) with 16-byte loads.  A device-side gate implements the
+// reference's no-double fast path (:199-201) without a host sync.
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+constexpr int kRows = 8;
+
+// per byte: min(15, x)
+__device__ __forceinline__ uint32_t sat15(uint32_t x) {
+  uint32_t hi = (x >> 4) & 0x0F0F0F0Fu;                // high nibble per byte
+  uint32_t over = ((hi + 0x0F0F0F0Fu) >> 4) & 0x01010101u;  // 1 where x > 15
+  return (x & ~(over * 0xFFu)) | (over * 0x0Fu);
+}
+
+// per byte: (a + b + 1) >> 1 without overflow
+__device__ __forceinline__ uint32_t avg_up(uint32_t a, uint32_t b) {
+  return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu);
+}
+
+// per byte: 0xFF where err == 2, else 0
+__device__ __forceinline__ uint32_t is_double(uint32_t e) {
+  uint32_t v = e ^ 0x02020202u;
+  uint32_t nonzero = (((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+  return ((~nonzero & 0x80808080u) >> 7) * 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t interp_word(uint32_t q, uint32_t l, uint32_t r, uint32_t e) {
+  uint32_t m = is_double(e);
+  return sat15((avg_up(l, r) & m) | (q & ~m));
+}
+
+__device__ __forceinline__ u32x4 interp_vec(u32x4 q, u32x4 l, u32x4 r, u32x4 e) {
+  u32x4 o;
+  o.x = interp_word(q.x, l.x, r.x, e.x);
+  o.y = interp_word(q.y, l.y, r.y, e.y);
+  o.z = interp_word(q.z, l.z, r.z, e.z);
+  o.w = interp_word(q.w, l.w, r.w, e.w);
+  return o;
+}
+
+// vector path: inner % 16 == 0; work item = (o, row block, column chunk)
+__global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restrict__ q,
+                                                            const u32x4 *__restrict__ err,
+                                                            u32x4 *__restrict__ out, int64_t outer,
+                                                            int64_t len, int64_t chunks,
+                                                            const int32_t *__restrict__ gate) {
+  const bool pass = gate != nullptr && *gate == 0;
+  const int64_t rblocks = (len + kRows - 1) / kRows;
+  const int64_t items = outer * rblocks * chunks;
+  for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < items;
+       it += (int64_t)gridDim.x * kBlock) {
+    const int64_t c = it % chunks;
+    const int64_t t = it / chunks;
+    const int64_t rb = t % rblocks;
+    const int64_t o = t / rblocks;
+    const int64_t l0 = rb * kRows;
+    const int64_t base = o * len * chunks + c;  // vector index of (o, l=0, c)
+    const int nrow = (int)min<int64_t>(kRows, len - l0);
+    if (pass) {
+      for (int k = 0; k < nrow; ++k) out[base + (l0 + k) * chunks] = q[base + (l0 + k) * chunks];
+      continue;
+    }
+    u32x4 prev = q[base + (l0 > 0 ? l0 - 1 : 0) * chunks];
+    u32x4 cur = q[base + l0 * chunks];
+    for (int k = 0; k < nrow; ++k) {
+      const int64_t l = l0 + k;
+      u32x4 next = q[base + (l + 1 < len ? l + 1 : len - 1) * chunks];
+      u32x4 e = err[base + l * chunks];
+      out[base + l * chunks] = interp_vec(cur, prev, next, e);
+      prev = cur;
+      cur = next;
+    }
+  }
+}
+
+// scalar path: one element per lane
+__global__ __launch_bounds__(kBlock) void interp_scalar_kernel(const uint8_t *__restrict__ q,
+                                                               const uint8_t *__restrict__ err,
+                                                               uint8_t *__restrict__ out,
+                                                               int64_t outer, int64_t len,
+                                                               int64_t inner,
+                                                               const int32_t *__restrict__ gate) {
+  const bool pass = gate != nullptr && *gate == 0;
+  const int64_t total = outer * len * inner;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (pass) {
+      out[i] = q[i];
+      continue;
+    }
+    const int64_t c = i % inner;
+    const int64_t l = (i / inner) % len;
+    const int64_t rowbase = i - l * inner;
+    const uint32_t left = q[rowbase + (l > 0 ? l - 1 : 0) * inner];
+    const uint32_t right = q[rowbase + (l + 1 < len ? l + 1 : len - 1) * inner];
+    (void)c;
+    out[i] = (uint8_t)interp_word(q[i], left, right, err[i]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void any_equal_kernel(const uint8_t *__restrict__ x, int64_t n,
+                                                           uint32_t value, int32_t *__restrict__ flag) {
+  bool hit = false;
+  const int64_t nvec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) ? n / 16 : 0;
+  const u32x4 *xv = reinterpret_cast<const u32x4 *>(x);
+  const uint32_t pat = value * 0x01010101u;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * kBlock) {
+    u32x4 v = xv[i];
+    uint32_t w[4] = {v.x ^ pat, v.y ^ pat, v.z ^ pat, v.w ^ pat};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      hit |= ((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) != 0;  // some byte is zero
+  }
+  for (int64_t i = nvec * 16 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock)
+    hit |= x[i] == value;
+  if (__any(hit) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1);
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int kvecc_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
+                                int64_t outer, int64_t len, int64_t inner, const int32_t *gate,
+                                void *stream) {
+  if (outer < 0 || len < 0 || inner < 0) return set_error(KVECC_EINVAL, "interpolate: negative size");
+  const int64_t total = outer * len * inner;
+  if (total == 0) return KVECC_OK;
+  if (!q || !err || !out) return set_error(KVECC_EINVAL, "interpolate: null pointer");
+  hipStream_t st = as_stream(stream);
+  if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
+    const int64_t chunks = inner / 16;
+    const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
+    hipLaunchKernelGGL(interp_vec_kernel, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, st,
+                       reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
+                       reinterpret_cast<u32x4 *>(out), outer, len, chunks, gate);
+  } else {
+    hipLaunchKernelGGL(interp_scalar_kernel, dim3(grid_for(total, kBlock)), dim3(kBlock), 0, st, q,
+                       err, out, outer, len, inner, gate);
+  }
+  return check_launch("interpolate");
+}
+
+KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int32_t *flag,
+                                 void *stream) {
+  if (n < 0) return set_error(KVECC_EINVAL, "any_equal_u8: negative n");
+  if (!flag) return set_error(KVECC_EINVAL, "any_equal_u8: null flag");
+  hipStream_t st = as_stream(stream);
+  hipError_t e = hipMemsetAsync(flag, 0, sizeof(int32_t), st);
+  if (e != hipSuccess) return set_error(KVECC_EHIP, "any_equal_u8: %s", hipGetErrorString(e));
+  if (n == 0) return KVECC_OK;
+  if (!x) return set_error(KVECC_EINVAL, "any_equal_u8: null input");
+  hipLaunchKernelGGL(any_equal_kernel, dim3(grid_for(n, (int64_t)kBlock * 16, 4)), dim3(kBlock), 0,
+                     st, x, n, (uint32_t)value, flag);
+  return check_launch("any_equal_u8");
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// kvecc_internal.h -- shared device/host helpers for the gfx950 codec kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kvecc.h"
+
+namespace kvecc {
+
+// ---- vector types -----------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;  // 4 waves
+
+// ---- error state (runtime.hip) --------------------------------------------
+int set_error(int code, const char *fmt, ...);
+int check_launch(const char *what);
+int cu_count();               // CUs of the current device (cached)
+int current_device();
+// Golay tables on the current device (uploaded on first use):
+//   parity[d]   (uint16) = 12 parity bits of data word d       (encode, syndrome)
+//   correct[s]  (uint16) = data-error(12) | count(3) << 12      (decode)
+const uint16_t *golay_parity_table_dev();
+const uint16_t *golay_correct_table_dev();
+// host-side table builders (product copy, independent of the test oracle)
+void build_golay_parity_table(uint16_t *out4096);
+void build_golay_correct_table(uint16_t *out4096);
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// grid for a grid-stride loop over `work` items of `per_block` each: enough
+// blocks to fill the chip (8 per CU), never more than there is work.
+inline unsigned grid_for(int64_t work, int64_t per_block, int per_cu = 8) {
+  int64_t need = cdiv(work, per_block);
+  int64_t cap = (int64_t)cu_count() * per_cu;
+  if (need > cap) need = cap;
+  if (need < 1) need = 1;
+  return (unsigned)need;
+}
+
+inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+// ---- device helpers ----------------------------------------------------------
+
+// wave-wide sum (all 64 lanes participate)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// accumulate two per-lane counters into stats[0..1] with one atomic per wave
+__device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32_t b) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    if (a) atomicAdd(reinterpret_cast<unsigned long long *>(stats), (unsigned long long)a);
+    if (b) atomicAdd(reinterpret_cast<unsigned long long *>(stats + 1), (unsigned long long)b);
+  }
+}
+
+__device__ __forceinline__ void flush_stats1(uint64_t *stats, uint32_t a) {
+  a = wave_sum(a);
+  if ((threadIdx.x & (kWave - 1)) == 0 && a)
+    atomicAdd(reinterpret_cast<unsigned long long *>(stats), (unsigned long long)a);
+}
+
+// per-byte parity of four packed bytes: bit 0 of each byte = XOR of its 8 bits
+__device__ __forceinline__ uint32_t byte_parity4(uint32_t y) {
+  y ^= y >> 4;
+  y ^= y >> 2;
+  y ^= y >> 1;
+  return y & 0x01010101u;
+}
+
+// nontemporal streaming load/store helpers (data touched exactly once)
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+  return __builtin_nontemporal_load(p);
+}
+template <typename T>
+__device__ __forceinline__ void st_stream(T *p, T v) {
+  __builtin_nontemporal_store(v, p);
+}
+
+}  // namespace kvecc

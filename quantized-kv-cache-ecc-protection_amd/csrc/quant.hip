@@ -1,0 +1,228 @@
+// quant.hip -- fused INT4 quantize+encode and decode+dequantize of KV rows.
+//
+// Reference: ecc_codecs/triton_kernels/fused_kernels.py:18-269 (quantize +
+// Hamming encode) and :272-437 (Hamming(8,4) decode + dequantize), and the
+// shim's torch path ecc_shim.py:572-580 with compute_quantization_scales
+// (kv_cache/paged_cache_ecc.py:302-334), which is the parity target:
+//   scale = absmax(row) / 7  (0 -> 1),  q = round_half_even(x / scale)
+//   clamped to [-8, 7] + 8,  all in IEEE fp32 (correctly rounded division).
+//
+// gfx950 design: a row (one head vector, D values) is owned by LPR lanes of a
+// wave (LPR = the power of two covering D / VEC, VEC elements = 16 B per lane
+// per load), so a wave processes 64 / LPR rows at once and the absmax is a
+// short __shfl_xor butterfly inside the row's lane group.  Loads are 16 B per
+// lane, the 8-bit codewords leave as VEC-byte stores.
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+template <typename T>
+__device__ __forceinline__ float to_f32(T v);
+template <>
+__device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ float to_f32<__half>(__half v) { return __half2float(v); }
+template <>
+__device__ __forceinline__ float to_f32<__hip_bfloat16>(__hip_bfloat16 v) {
+  return __bfloat162float(v);
+}
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float v);
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __half from_f32<__half>(float v) { return __float2half_rn(v); }
+template <>
+__device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) {
+  return __float2bfloat16(v);
+}
+
+// single-value encoders (same algebra as hamming.hip, one byte)
+__device__ __forceinline__ uint32_t enc_nibble(uint32_t v, int codec) {
+  uint32_t d0 = v & 1, d1 = v >> 1 & 1, d2 = v >> 2 & 1, d3 = v >> 3 & 1;
+  uint32_t h = v | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6;
+  if (codec == KVECC_CODEC_H84) return h | (d0 ^ d1 ^ d2) << 7;
+  if (codec == KVECC_CODEC_H74) return h;
+  return v;
+}
+
+__device__ __forceinline__ float row_max(float v, int lpr) {
+  for (int off = lpr >> 1; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
+  return v;
+}
+
+template <typename T, int VEC>
+struct alignas(sizeof(T) * VEC) Vec {
+  T v[VEC];
+};
+
+// Quantize + encode. rows are contiguous of length d; lanes [g*lpr, (g+1)*lpr)
+// of a wave own row (wave_row0 + g).
+template <typename T, int VEC>
+__global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__restrict__ x, int codec,
+                                                                 uint8_t *__restrict__ cw,
+                                                                 float *__restrict__ scales,
+                                                                 int64_t rows, int64_t d, int lpr) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int rows_per_wave = kWave / lpr;
+  const int sub = lane / lpr, li = lane % lpr;
+  const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
+  const int64_t wave_id = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  const int64_t nchunk = d / VEC;  // VEC divides d on this path
+  for (int64_t r0 = wave_id * rows_per_wave; r0 < rows; r0 += waves * rows_per_wave) {
+    const int64_t r = r0 + sub;
+    const bool live = r < rows;
+    const T *xr = x + r * d;
+    float amax = 0.0f;
+    if (live) {
+      for (int64_t c = li; c < nchunk; c += lpr) {
+        Vec<T, VEC> v = *reinterpret_cast<const Vec<T, VEC> *>(xr + c * VEC);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) amax = fmaxf(amax, fabsf(to_f32<T>(v.v[k])));
+      }
+    }
+    amax = row_max(amax, lpr);
+    float scale = __fdiv_rn(amax, 7.0f);
+    if (scale == 0.0f) scale = 1.0f;
+    if (!live) continue;
+    if (li == 0) scales[r] = scale;
+    uint8_t *cr = cw + r * d;
+    for (int64_t c = li; c < nchunk; c += lpr) {
+      Vec<T, VEC> v = *reinterpret_cast<const Vec<T, VEC> *>(xr + c * VEC);
+      Vec<uint8_t, VEC> o;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        float q = rintf(__fdiv_rn(to_f32<T>(v.v[k]), scale));
+        q = fminf(fmaxf(q, -8.0f), 7.0f);
+        o.v[k] = (uint8_t)enc_nibble((uint32_t)(int)(q + 8.0f), codec);
+      }
+      *reinterpret_cast<Vec<uint8_t, VEC> *>(cr + c * VEC) = o;
+    }
+  }
+}
+
+// Hamming(8,4) decode of one codeword byte: data, type (hamming84_triton.py:145-206)
+__device__ __forceinline__ uint32_t dec84(uint32_t c, uint32_t &type) {
+  uint32_t s0 = __builtin_popcount(c & 0x1Bu) & 1, s1 = __builtin_popcount(c & 0x2Du) & 1;
+  uint32_t s2 = __builtin_popcount(c & 0x4Eu) & 1, pe = __builtin_popcount(c) & 1;
+  uint32_t nz = s0 | s1 | s2;
+  uint32_t fix = (s0 & s1 & ~s2 & 1) | (s0 & ~s1 & s2 & 1) << 1 | (~s0 & s1 & s2 & 1) << 2 |
+                 (s0 & s1 & s2) << 3;
+  type = pe | (pe ^ nz) << 1;
+  return (c ^ (pe ? fix : 0u)) & 0xFu;
+}
+
+template <typename TO, int VEC>
+__global__ __launch_bounds__(kBlock) void decode_dequant_kernel(const uint8_t *__restrict__ cw,
+                                                                const float *__restrict__ scales,
+                                                                TO *__restrict__ out, int64_t rows,
+                                                                int64_t d, int zero_doubles,
+                                                                uint64_t *__restrict__ stats) {
+  const int64_t nchunk = d / VEC;
+  const int64_t total = rows * nchunk;
+  uint32_t n1 = 0, n2 = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / nchunk;
+    const float s = scales[r];
+    Vec<uint8_t, VEC> c = *reinterpret_cast<const Vec<uint8_t, VEC> *>(cw + i * VEC);
+    Vec<TO, VEC> o;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      uint32_t t;
+      uint32_t q = dec84(c.v[k], t);
+      if (zero_doubles && t == 2) q = 0;
+      n1 += t == 1;
+      n2 += t == 2;
+      o.v[k] = from_f32<TO>(((float)q - 8.0f) * s);
+    }
+    *reinterpret_cast<Vec<TO, VEC> *>(out + i * VEC) = o;
+  }
+  if (stats) flush_stats2(stats, n1, n2);
+}
+
+static int lanes_per_row(int64_t chunks) {
+  int l = 1;
+  while (l < chunks && l < kWave) l <<= 1;
+  return l;
+}
+
+template <typename T>
+static void launch_qe(const void *x, int codec, uint8_t *cw, float *scales, int64_t rows, int64_t d,
+                      hipStream_t st) {
+  constexpr int V = 16 / sizeof(T);
+  const T *xt = reinterpret_cast<const T *>(x);
+  bool vec = d % V == 0 && aligned(x, 16) && aligned(cw, V);
+  if (vec) {
+    int lpr = lanes_per_row(d / V);
+    int64_t waves = cdiv(rows, kWave / lpr);
+    hipLaunchKernelGGL((quantize_encode_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave)),
+                       dim3(kBlock), 0, st, xt, codec, cw, scales, rows, d, lpr);
+  } else {
+    int lpr = lanes_per_row(d);
+    int64_t waves = cdiv(rows, kWave / lpr);
+    hipLaunchKernelGGL((quantize_encode_kernel<T, 1>), dim3(grid_for(waves, kBlock / kWave)),
+                       dim3(kBlock), 0, st, xt, codec, cw, scales, rows, d, lpr);
+  }
+}
+
+template <typename TO>
+static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t rows, int64_t d,
+                      int zero_doubles, uint64_t *stats, hipStream_t st) {
+  TO *o = reinterpret_cast<TO *>(out);
+  if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
+    int64_t total = rows * (d / 4);
+    hipLaunchKernelGGL((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),
+                       0, st, cw, scales, o, rows, d, zero_doubles, stats);
+  } else {
+    int64_t total = rows * d;
+    hipLaunchKernelGGL((decode_dequant_kernel<TO, 1>), dim3(grid_for(total, kBlock)), dim3(kBlock),
+                       0, st, cw, scales, o, rows, d, zero_doubles, stats);
+  }
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int kvecc_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
+                                         float *scales, int64_t rows, int64_t d, void *stream) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "quantize_encode_rows: negative size");
+  if (rows == 0) return KVECC_OK;
+  if (d == 0) return set_error(KVECC_EINVAL, "quantize_encode_rows: empty rows");
+  if (!x || !cw || !scales) return set_error(KVECC_EINVAL, "quantize_encode_rows: null pointer");
+  if (codec != KVECC_CODEC_NONE && codec != KVECC_CODEC_H74 && codec != KVECC_CODEC_H84)
+    return set_error(KVECC_EINVAL, "quantize_encode_rows: bad codec %d", codec);
+  hipStream_t st = as_stream(stream);
+  switch (x_dtype) {
+    case KVECC_F32: launch_qe<float>(x, codec, cw, scales, rows, d, st); break;
+    case KVECC_F16: launch_qe<__half>(x, codec, cw, scales, rows, d, st); break;
+    case KVECC_BF16: launch_qe<__hip_bfloat16>(x, codec, cw, scales, rows, d, st); break;
+    default: return set_error(KVECC_EINVAL, "quantize_encode_rows: bad dtype %d", x_dtype);
+  }
+  return check_launch("quantize_encode_rows");
+}
+
+KVECC_API int kvecc_decode_dequant_h84_rows(const uint8_t *cw, const float *scales, void *out,
+                                            int out_dtype, int64_t rows, int64_t d,
+                                            int zero_doubles, uint64_t *stats, void *stream) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "decode_dequant_h84_rows: negative size");
+  if (rows == 0 || d == 0) return KVECC_OK;
+  if (!cw || !scales || !out) return set_error(KVECC_EINVAL, "decode_dequant_h84_rows: null pointer");
+  hipStream_t st = as_stream(stream);
+  switch (out_dtype) {
+    case KVECC_F32: launch_dd<float>(cw, scales, out, rows, d, zero_doubles, stats, st); break;
+    case KVECC_F16: launch_dd<__half>(cw, scales, out, rows, d, zero_doubles, stats, st); break;
+    case KVECC_BF16: launch_dd<__hip_bfloat16>(cw, scales, out, rows, d, zero_doubles, stats, st); break;
+    default: return set_error(KVECC_EINVAL, "decode_dequant_h84_rows: bad dtype %d", out_dtype);
+  }
+  return check_launch("decode_dequant_h84_rows");
+}
+
+}  // extern "C"

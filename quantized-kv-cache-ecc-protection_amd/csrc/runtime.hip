@@ -1,0 +1,196 @@
+// runtime.hip -- error reporting, device queries and the Golay code tables.
+//
+// The Golay tables are built here on the host, from the code's definition
+// (the B matrix of ecc_codecs/triton_kernels/config.py:329-347), and uploaded
+// once per device; they replace the per-device syndrome-table cache of
+// golay_triton.py:304-330.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KVECC_EHIP, "%s: %s", what, hipGetErrorString(e));
+  return KVECC_OK;
+}
+
+constexpr int kMaxDev = 64;
+static std::mutex g_mu;
+static int g_cu[kMaxDev];
+static uint16_t *g_parity[kMaxDev];
+static uint16_t *g_correct[kMaxDev];
+
+int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return 0;
+  return d;
+}
+
+int cu_count() {
+  int d = current_device();
+  if (d < 0 || d >= kMaxDev) return 256;
+  int c = __atomic_load_n(&g_cu[d], __ATOMIC_ACQUIRE);
+  if (c > 0) return c;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0)
+    v = 256;
+  __atomic_store_n(&g_cu[d], v, __ATOMIC_RELEASE);
+  return v;
+}
+
+// Rows of B as 12-bit masks (bit i of row j = B[j][i]); B is symmetric, so
+// these are also its columns, the reference's B_COL_* (golay_triton.py:59-70).
+static const uint16_t kGolayRow[12] = {0xA3B, 0xD1D, 0xE8E, 0xB47, 0xDA3, 0xED1,
+                                       0xF68, 0xBB4, 0x9DA, 0x8ED, 0xC76, 0x7FF};
+
+void build_golay_parity_table(uint16_t *out) {
+  // parity(d) = XOR of the B rows of the set data bits (linear code)
+  for (uint32_t d = 0; d < 4096; ++d) {
+    uint32_t p = 0;
+    for (int j = 0; j < 12; ++j)
+      if (d >> j & 1u) p ^= kGolayRow[j];
+    out[d] = (uint16_t)p;
+  }
+}
+
+static inline uint32_t syndrome24(uint32_t w, const uint16_t *par) {
+  // H = [B^T | I]  =>  syndrome = parity bits received ^ parity(data received)
+  return ((w >> 12) & 0xFFFu) ^ par[w & 0xFFFu];
+}
+
+// error pattern per syndrome exactly as config.py:403-457 orders it
+static void build_error_patterns(int32_t *pat) {
+  uint16_t par[4096];
+  build_golay_parity_table(par);
+  for (int s = 0; s < 4096; ++s) pat[s] = -1;
+  pat[0] = 0;
+  for (int i = 0; i < 24; ++i) pat[syndrome24(1u << i, par)] = (int32_t)(1u << i);
+  for (int i = 0; i < 24; ++i)
+    for (int j = i + 1; j < 24; ++j) {
+      uint32_t e = (1u << i) | (1u << j);
+      uint32_t s = syndrome24(e, par);
+      if (pat[s] < 0) pat[s] = (int32_t)e;
+    }
+  for (int i = 0; i < 24; ++i)
+    for (int j = i + 1; j < 24; ++j)
+      for (int k = j + 1; k < 24; ++k) {
+        uint32_t e = (1u << i) | (1u << j) | (1u << k);
+        uint32_t s = syndrome24(e, par);
+        if (pat[s] < 0) pat[s] = (int32_t)e;
+      }
+}
+
+void build_golay_correct_table(uint16_t *out) {
+  int32_t pat[4096];
+  build_error_patterns(pat);
+  for (int s = 0; s < 4096; ++s) {
+    if (pat[s] < 0) {
+      out[s] = (uint16_t)(4u << 12);  // uncorrectable: data kept, count 4
+    } else {
+      uint32_t e = (uint32_t)pat[s];
+      out[s] = (uint16_t)((e & 0xFFFu) | ((uint32_t)__builtin_popcount(e) << 12));
+    }
+  }
+}
+
+static int ensure_tables(int d) {
+  if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_parity[d] && g_correct[d]) return KVECC_OK;
+  uint16_t host[2][4096];
+  build_golay_parity_table(host[0]);
+  build_golay_correct_table(host[1]);
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
+  if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
+  uint16_t *buf = nullptr;
+  hipError_t e = hipMalloc(&buf, sizeof(host));
+  if (e == hipSuccess) e = hipMemcpy(buf, host, sizeof(host), hipMemcpyHostToDevice);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(KVECC_EHIP, "golay table upload: %s", hipGetErrorString(e));
+  g_parity[d] = buf;
+  g_correct[d] = buf + 4096;
+  return KVECC_OK;
+}
+
+const uint16_t *golay_parity_table_dev() {
+  int d = current_device();
+  if (d >= 0 && d < kMaxDev && g_parity[d]) return g_parity[d];
+  if (ensure_tables(d) != KVECC_OK) return nullptr;
+  return g_parity[d];
+}
+
+const uint16_t *golay_correct_table_dev() {
+  int d = current_device();
+  if (d >= 0 && d < kMaxDev && g_correct[d]) return g_correct[d];
+  if (ensure_tables(d) != KVECC_OK) return nullptr;
+  return g_correct[d];
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API const char *kvecc_version(void) { return "kvecc 0.1.0 (gfx950)"; }
+
+KVECC_API const char *kvecc_last_error(void) { return g_err; }
+
+KVECC_API int kvecc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+KVECC_API int kvecc_init_device(int device) {
+  int n = kvecc_device_count();
+  if (n <= 0) return set_error(KVECC_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= n) return set_error(KVECC_EINVAL, "device %d not in [0,%d)", device, n);
+  return ensure_tables(device);
+}
+
+KVECC_API int kvecc_golay_syndrome_table_host(int32_t *out) {
+  if (!out) return set_error(KVECC_EINVAL, "null output");
+  build_error_patterns(out);
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_golay_h_row_masks_host(uint32_t *out) {
+  if (!out) return set_error(KVECC_EINVAL, "null output");
+  for (int i = 0; i < 12; ++i) out[i] = (uint32_t)kGolayRow[i] | (1u << (12 + i));
+  return KVECC_OK;
+}
+
+KVECC_API uint32_t kvecc_ber_threshold(float ber) {
+  // flip(x) := fp32(x) * 4.6566127342e-10f < ber is a prefix of [0, 2^31):
+  // both the int->float conversion and the multiply round monotonically.
+  const float scale = 4.6566127342e-10f;
+  uint32_t lo = 0, hi = 0x80000000u;  // answer in [lo, hi]
+  while (lo < hi) {
+    uint32_t mid = lo + (hi - lo) / 2;
+    volatile float u = (float)(int32_t)mid * scale;
+    if (u < ber)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+}  // extern "C"

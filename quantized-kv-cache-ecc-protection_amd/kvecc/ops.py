@@ -1,0 +1,466 @@
+"""HIP backend: the reference's codec functions over torch tensors on an MI355X.
+
+Every public function keeps the name, arguments, return convention and error
+behaviour of its counterpart in ecc_codecs/triton_kernels/ (cited per
+function) and dispatches to libkvecc.so through ctypes on the current HIP
+stream.  There is no CPU fallback: a non-GPU tensor raises AssertionError,
+exactly like the reference's ``assert x.is_cuda``.
+
+Two layers:
+  * ``*_into`` / ``*_dev`` functions: asynchronous, write into caller buffers,
+    statistics accumulate in a device int64 tensor (no host sync) -- for
+    pipelines, the shim and benchmarks;
+  * reference-compatible wrappers: same return tuples as the reference, which
+    read the statistics back to Python ints (one sync per call, as the
+    reference does).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .config import ErrorType
+
+_VP = ctypes.c_void_p
+
+
+def _ptr(t):
+    return _VP(t.data_ptr()) if t is not None else _VP(0)
+
+
+def _stream(device):
+    return _VP(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _check_gpu(t, what="Input"):
+    assert t.is_cuda, f"{what} must be on CUDA device"
+
+
+_ready = set()
+
+
+def _ensure_device(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _ready:
+        _lib.call("kvecc_init_device", idx)
+        _ready.add(idx)
+    return idx
+
+
+def new_stats(device, n=2):
+    """Zeroed device statistics accumulator (int64, read as uint64 by the kernels)."""
+    return torch.zeros(n, dtype=torch.int64, device=device)
+
+
+def _flat(t, dtype):
+    f = t.reshape(-1)
+    if f.dtype != dtype:
+        f = f.to(dtype)
+    return f.contiguous()
+
+
+# ============================================================================
+# Hamming(7,4) / Hamming(8,4)
+# ============================================================================
+
+def hamming74_encode_into(flat_in, out):
+    _lib.call("kvecc_hamming74_encode", _ptr(flat_in), _ptr(out), flat_in.numel(),
+              _stream(flat_in.device))
+    return out
+
+
+def hamming84_encode_into(flat_in, out):
+    _lib.call("kvecc_hamming84_encode", _ptr(flat_in), _ptr(out), flat_in.numel(),
+              _stream(flat_in.device))
+    return out
+
+
+def hamming74_decode_into(flat_cw, data, flag=None, stats=None):
+    _lib.call("kvecc_hamming74_decode", _ptr(flat_cw), _ptr(data), _ptr(flag), flat_cw.numel(),
+              _ptr(stats), _stream(flat_cw.device))
+    return data
+
+
+def hamming84_decode_into(flat_cw, data, error_type=None, stats=None):
+    _lib.call("kvecc_hamming84_decode", _ptr(flat_cw), _ptr(data), _ptr(error_type),
+              flat_cw.numel(), _ptr(stats), _stream(flat_cw.device))
+    return data
+
+
+def hamming74_encode(int4_values: torch.Tensor) -> torch.Tensor:
+    """INT4 (uint8 low nibble) -> Hamming(7,4) codewords; hamming74_triton.py:170-201."""
+    _check_gpu(int4_values)
+    flat = _flat(int4_values, torch.uint8)
+    out = torch.empty_like(flat)
+    hamming74_encode_into(flat, out)
+    return out.view(int4_values.shape)
+
+
+def hamming74_decode(codewords: torch.Tensor, return_error_detected: bool = False):
+    """Hamming(7,4) SEC decode; hamming74_triton.py:218-277.
+
+    -> (decoded, (n_corrected,)) or (decoded, error_detected, (n_corrected,))
+    """
+    _check_gpu(codewords)
+    flat = _flat(codewords, torch.uint8)
+    data = torch.empty_like(flat)
+    flag = torch.empty_like(flat)
+    stats = new_stats(flat.device, 1)
+    hamming74_decode_into(flat, data, flag, stats)
+    n = int(stats[0])
+    data = data.view(codewords.shape)
+    flag = flag.view(codewords.shape)
+    if return_error_detected:
+        return data, flag, (n,)
+    return data, (n,)
+
+
+def hamming84_encode(int4_values: torch.Tensor) -> torch.Tensor:
+    """INT4 -> Hamming(8,4) SECDED codewords; hamming84_triton.py:217-254."""
+    _check_gpu(int4_values)
+    flat = _flat(int4_values, torch.uint8)
+    out = torch.empty_like(flat)
+    hamming84_encode_into(flat, out)
+    return out.view(int4_values.shape)
+
+
+def hamming84_decode(codewords: torch.Tensor, return_error_types: bool = False):
+    """Hamming(8,4) SECDED decode; hamming84_triton.py:281-351.
+
+    -> (decoded, (corrected, detected)) or (decoded, error_types, (corrected, detected))
+    Double errors keep their (uncorrected) data and are typed DOUBLE_DETECTED.
+    """
+    _check_gpu(codewords)
+    flat = _flat(codewords, torch.uint8)
+    data = torch.empty_like(flat)
+    etype = torch.empty_like(flat)
+    stats = new_stats(flat.device)
+    hamming84_decode_into(flat, data, etype, stats)
+    corrected, detected = stats.tolist()
+    data = data.view(codewords.shape)
+    etype = etype.view(codewords.shape)
+    if return_error_types:
+        return data, etype, (corrected, detected)
+    return data, (corrected, detected)
+
+
+# ============================================================================
+# Golay(24,12)
+# ============================================================================
+
+def golay_encode_into(flat_triplets, codewords, m):
+    _ensure_device(flat_triplets.device)
+    _lib.call("kvecc_golay_encode", _ptr(flat_triplets), _ptr(codewords), m,
+              _stream(flat_triplets.device))
+    return codewords
+
+
+def golay_decode_into(flat_cw, triplets, counts=None, stats=None):
+    _ensure_device(flat_cw.device)
+    _lib.call("kvecc_golay_decode", _ptr(flat_cw), _ptr(triplets), _ptr(counts), flat_cw.numel(),
+              _ptr(stats), _stream(flat_cw.device))
+    return triplets
+
+
+def golay_encode(triplets: torch.Tensor) -> torch.Tensor:
+    """INT4 triplets [N,3] (or [3]) -> int32 codewords [N]; golay_triton.py:382-422."""
+    _check_gpu(triplets)
+    if triplets.dim() == 1:
+        triplets = triplets.unsqueeze(0)
+    n = triplets.shape[0]
+    flat = _flat(triplets, torch.uint8)
+    if flat.numel() < 3 * n:
+        raise ValueError(f"golay_encode needs 3 values per codeword, got shape {tuple(triplets.shape)}")
+    out = torch.empty(n, dtype=torch.int32, device=triplets.device)
+    golay_encode_into(flat, out, n)
+    return out
+
+
+def golay_decode(codewords: torch.Tensor, return_error_counts: bool = False):
+    """Golay(24,12) decode; golay_triton.py:425-498.
+
+    -> (triplets [N,3], (bits_corrected, uncorrectable)) or
+       (triplets, error_counts [N], (bits_corrected, uncorrectable)).
+    error_count 0..3 = bits corrected, 4 = uncorrectable (data kept).
+    """
+    _check_gpu(codewords)
+    n = codewords.numel()
+    flat = _flat(codewords, torch.int32)
+    trip = torch.empty(n * 3, dtype=torch.uint8, device=codewords.device)
+    counts = torch.empty(n, dtype=torch.uint8, device=codewords.device)
+    stats = new_stats(codewords.device)
+    golay_decode_into(flat, trip, counts, stats)
+    bits, unc = stats.tolist()
+    trip = trip.view(n, 3)
+    if return_error_counts:
+        return trip, counts, (bits, unc)
+    return trip, (bits, unc)
+
+
+def golay_encode_rows(nibbles: torch.Tensor) -> torch.Tensor:
+    """Per-head packing of the shim (ecc_shim.py:623-682): [..., D] nibbles ->
+    [..., ceil(D/3)] codewords, each row zero-padded to a multiple of 3."""
+    _check_gpu(nibbles)
+    d = nibbles.shape[-1]
+    g = (d + 2) // 3
+    flat = _flat(nibbles, torch.uint8)
+    rows = flat.numel() // d if d else 0
+    out = torch.empty(*nibbles.shape[:-1], g, dtype=torch.int32, device=nibbles.device)
+    _ensure_device(nibbles.device)
+    _lib.call("kvecc_golay_encode_rows", _ptr(flat), _ptr(out), rows, d, _stream(nibbles.device))
+    return out
+
+
+def golay_decode_rows(codewords: torch.Tensor, d: int, stats=None) -> torch.Tensor:
+    """Inverse of golay_encode_rows: [..., ceil(d/3)] -> [..., d] nibbles."""
+    _check_gpu(codewords)
+    g = codewords.shape[-1]
+    if g != (d + 2) // 3:
+        raise ValueError(f"{g} codewords per row do not hold {d} values")
+    flat = _flat(codewords, torch.int32)
+    rows = flat.numel() // g if g else 0
+    out = torch.empty(*codewords.shape[:-1], d, dtype=torch.uint8, device=codewords.device)
+    _ensure_device(codewords.device)
+    _lib.call("kvecc_golay_decode_rows", _ptr(flat), _ptr(out), rows, d, _ptr(stats),
+              _stream(codewords.device))
+    return out
+
+
+# ============================================================================
+# Fault injection
+# ============================================================================
+
+def inject_into(flat_in, out, ber, n_bits, seed=0, counts=None, stats=None, global_n=None,
+                offset0=0):
+    """Flat injection into `out` (may be `flat_in`); shard-aware via global_n/offset0."""
+    n = flat_in.numel()
+    gn = n if global_n is None else int(global_n)
+    if flat_in.dtype == torch.uint8:
+        name = "kvecc_inject_u8"
+    elif flat_in.dtype == torch.int32:
+        name = "kvecc_inject_i32"
+    else:
+        raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
+    _lib.call(name, _ptr(flat_in), _ptr(out), _ptr(counts), n, int(n_bits), int(seed), float(ber),
+              gn, int(offset0), _ptr(stats), _stream(flat_in.device))
+    return out
+
+
+def inject_rows_into(flat_in, out, rows, row_len, ber, n_bits, seed_base, stats=None):
+    """Per-row injection: row r uses seed_base + r and N = row_len (shim scheme)."""
+    if flat_in.dtype == torch.uint8:
+        name = "kvecc_inject_rows_u8"
+    elif flat_in.dtype == torch.int32:
+        name = "kvecc_inject_rows_i32"
+    else:
+        raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
+    _lib.call(name, _ptr(flat_in), _ptr(out), int(rows), int(row_len), int(n_bits), int(seed_base),
+              float(ber), _ptr(stats), _stream(flat_in.device))
+    return out
+
+
+def inject_bit_errors_triton(data, ber, n_bits, seed=0, return_stats=False):
+    """Bernoulli bit flips, bit-exact with the reference's Philox stream.
+
+    fault_injection_triton.py:337-424.  ber <= 0 returns `data` itself.
+    -> corrupted, or (corrupted, (total_flips, elements_affected))
+    """
+    _check_gpu(data)
+    if ber <= 0:
+        if return_stats:
+            return data, (0, 0)
+        return data
+    flat = data.reshape(-1)
+    if flat.dtype not in (torch.uint8, torch.int32):
+        raise ValueError(f"Unsupported dtype: {flat.dtype}. Use uint8 or int32.")
+    flat = flat.contiguous()
+    out = torch.empty_like(flat)
+    stats = new_stats(data.device) if return_stats else None
+    inject_into(flat, out, ber, n_bits, seed, stats=stats)
+    out = out.view(data.shape)
+    if return_stats:
+        flips, affected = stats.tolist()
+        return out, (flips, affected)
+    return out
+
+
+inject_bit_errors = inject_bit_errors_triton
+
+
+def inject_bit_errors_triton_batched(data, ber, n_bits, seed=0):
+    """fault_injection_triton.py:427-431 -> (corrupted, total_flips)."""
+    corrupted, (total, _) = inject_bit_errors_triton(data, ber, n_bits, seed, return_stats=True)
+    return corrupted, total
+
+
+def inject_bit_errors_triton_vectorized(data, ber, n_bits, seed=0, return_stats=False):
+    """rand4x variant (a different, also bit-exact stream); fault_injection_triton.py:434-496."""
+    _check_gpu(data)
+    if ber <= 0:
+        if return_stats:
+            return data, (0, 0)
+        return data
+    flat = data.reshape(-1)
+    if flat.dtype == torch.uint8:
+        name = "kvecc_inject_u8_vectorized"
+    elif flat.dtype == torch.int32:
+        name = "kvecc_inject_i32_vectorized"
+    else:
+        raise ValueError(f"Unsupported dtype: {flat.dtype}. Use uint8 or int32.")
+    flat = flat.contiguous()
+    out = torch.empty_like(flat)
+    stats = new_stats(data.device) if return_stats else None
+    _lib.call(name, _ptr(flat), _ptr(out), _VP(0), flat.numel(), int(n_bits), int(seed), float(ber),
+              _ptr(stats), _stream(data.device))
+    out = out.view(data.shape)
+    if return_stats:
+        flips, affected = stats.tolist()
+        return out, (flips, affected)
+    return out
+
+
+# ============================================================================
+# Interpolation
+# ============================================================================
+
+def _seq_layout(shape, seq_dim):
+    """(outer, len, inner) of the reference's sequence axis choice (:206-236)."""
+    nd = len(shape)
+    if nd == 1:
+        return 1, shape[0], 1
+    if nd == 2:  # 2-D input: rows are sequences, seq_dim is ignored
+        return shape[0], shape[1], 1
+    sd = seq_dim % nd
+    outer = 1
+    for s in shape[:sd]:
+        outer *= s
+    inner = 1
+    for s in shape[sd + 1:]:
+        inner *= s
+    return outer, shape[sd], inner
+
+
+def interpolate_into(q, err, out, outer, length, inner, gate=None):
+    _lib.call("kvecc_interpolate", _ptr(q), _ptr(err), _ptr(out), outer, length, inner, _ptr(gate),
+              _stream(q.device))
+    return out
+
+
+def any_equal(x, value, flag=None):
+    """Device int32 flag = any(x == value), no host sync."""
+    if flag is None:
+        flag = torch.empty(1, dtype=torch.int32, device=x.device)
+    _lib.call("kvecc_any_equal_u8", _ptr(x), x.numel(), int(value), _ptr(flag), _stream(x.device))
+    return flag
+
+
+def interpolate_double_errors(q, error_type, original_shape=None, seq_dim=-1):
+    """Replace DOUBLE_DETECTED values by the rounded mean of their sequence
+    neighbours; interpolation_triton.py:162-265.
+
+    The no-double fast path (return q unchanged) is decided on the device: no
+    host sync unless q is not uint8 (its dtype would depend on the branch).
+    """
+    _check_gpu(q)
+    _check_gpu(error_type, "Error type")
+    assert q.shape == error_type.shape, "Shape mismatch between q and error_type"
+    if q.numel() == 0:
+        return q.clone()
+    err = _flat(error_type, torch.uint8)
+    flag = any_equal(err, ErrorType.DOUBLE_DETECTED)
+    if q.dtype != torch.uint8 and int(flag.item()) == 0:
+        return q.clone()
+    qf = _flat(q, torch.uint8)
+    outer, length, inner = _seq_layout(tuple(q.shape), seq_dim)
+    out = torch.empty_like(qf)
+    interpolate_into(qf, err, out, outer, length, inner, gate=flag if q.dtype == torch.uint8 else None)
+    return out.view(q.shape)
+
+
+def interpolate_double_errors_1d(q, error_type):
+    return interpolate_double_errors(q, error_type, seq_dim=-1)
+
+
+def interpolate_double_errors_autotuned(q, error_type, original_shape=None, seq_dim=-1):
+    """Same result as interpolate_double_errors (the reference autotunes Triton
+    block sizes, :272-350; the HIP kernel's geometry is fixed per layout)."""
+    return interpolate_double_errors(q, error_type, original_shape, seq_dim)
+
+
+# ============================================================================
+# Fused quantize + encode / decode + dequantize
+# ============================================================================
+
+_DT = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
+
+
+def quantize_encode_rows_into(x2d, codec_code, cw, scales):
+    if x2d.dtype not in _DT:
+        raise TypeError(f"unsupported input dtype {x2d.dtype}")
+    rows, d = x2d.shape
+    _lib.call("kvecc_quantize_encode_rows", _ptr(x2d), _DT[x2d.dtype], int(codec_code), _ptr(cw),
+              _ptr(scales), rows, d, _stream(x2d.device))
+    return cw, scales
+
+
+def _fused_quantize_encode(input_tensor, codec_code):
+    _check_gpu(input_tensor)
+    shape = input_tensor.shape
+    d = shape[-1]
+    x = input_tensor.reshape(-1, d).contiguous()
+    rows = x.shape[0]
+    cw = torch.empty(rows, d, dtype=torch.uint8, device=input_tensor.device)
+    scales = torch.empty(rows, dtype=torch.float32, device=input_tensor.device)
+    quantize_encode_rows_into(x, codec_code, cw, scales)
+    if input_tensor.dim() == 1:
+        return cw.squeeze(0), scales
+    return cw.view(shape), scales.view(shape[:-1])
+
+
+def fused_quantize_encode_hamming84(input_tensor):
+    """Row absmax INT4 quantization + Hamming(8,4) encode in one kernel;
+    fused_kernels.py:97-160 (matches the shim's torch rounding exactly)."""
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H84)
+
+
+def fused_quantize_encode_hamming74(input_tensor):
+    """fused_kernels.py:222-269 with Hamming(7,4)."""
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H74)
+
+
+def quantize_rows(input_tensor):
+    """INT4 quantization only (codec 'int4'): -> (nibbles uint8, scales f32)."""
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_NONE)
+
+
+def decode_dequant_h84_into(cw2d, scales, out, zero_doubles=True, stats=None):
+    rows, d = cw2d.shape
+    _lib.call("kvecc_decode_dequant_h84_rows", _ptr(cw2d), _ptr(scales), _ptr(out), _DT[out.dtype],
+              rows, d, int(bool(zero_doubles)), _ptr(stats), _stream(cw2d.device))
+    return out
+
+
+def fused_decode_dequantize_hamming84(codewords, scales, output_dtype=torch.float32):
+    """Hamming(8,4) decode + dequantize; fused_kernels.py:372-437.
+
+    Double-error values become 0 before dequantization (:344).
+    -> (dequantized, errors_corrected)
+    """
+    _check_gpu(codewords)
+    _check_gpu(scales, "Scales")
+    shape = codewords.shape
+    d = shape[-1]
+    cw = codewords.reshape(-1, d).contiguous()
+    sc = scales.reshape(-1).to(torch.float32).contiguous()
+    dtype = output_dtype if output_dtype in _DT else torch.float32
+    out = torch.empty(cw.shape, dtype=dtype, device=codewords.device)
+    stats = new_stats(codewords.device)
+    decode_dequant_h84_into(cw, sc, out, True, stats)
+    corrected = int(stats[0])
+    out = out.squeeze(0) if codewords.dim() == 1 else out.view(shape)
+    if output_dtype != dtype:
+        out = out.to(output_dtype)
+    return out, corrected

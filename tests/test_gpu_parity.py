@@ -1,0 +1,322 @@
+"""HIP kernels vs the oracle and the reference's golden vectors (MI355X only).
+
+Bit-exact for every integer output (codewords, data, error types, counts,
+statistics); fp32/fp16 dequantization is compared exactly as well, since the
+arithmetic is the same IEEE sequence (torch's own .to(fp16) rounding).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# Hamming
+# ---------------------------------------------------------------------------
+
+def test_hamming_all_bytes_golden(gpu, golden):
+    import kvecc
+    g = golden("hamming")
+    x = _t(g["inputs"], gpu)
+    assert np.array_equal(_np(kvecc.hamming74_encode(x)), g["enc74"])
+    assert np.array_equal(_np(kvecc.hamming84_encode(x)), g["enc84"])
+    d, f, st = kvecc.hamming74_decode(x, return_error_detected=True)
+    assert np.array_equal(_np(d), g["dec74_data"]) and np.array_equal(_np(f), g["dec74_flag"])
+    assert st == tuple(g["dec74_stats"].tolist())
+    d, t, st = kvecc.hamming84_decode(x, return_error_types=True)
+    assert np.array_equal(_np(d), g["dec84_data"]) and np.array_equal(_np(t), g["dec84_type"])
+    assert st == tuple(g["dec84_stats"].tolist())
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 4095, 4096 * 4 + 33, 3_000_001])
+@pytest.mark.parametrize("offset", [0, 3])
+def test_hamming_random_vs_oracle(gpu, oracle, n, offset):
+    """Vector path, unaligned (byte-offset) views and ragged tails."""
+    import kvecc
+    rng = np.random.default_rng(n + offset)
+    buf = rng.integers(0, 256, size=n + offset, dtype=np.int64).astype(np.uint8)
+    x = _t(buf, gpu)[offset:]
+    ref = buf[offset:]
+    assert np.array_equal(_np(kvecc.hamming84_encode(x)), oracle.hamming84_encode(ref))
+    assert np.array_equal(_np(kvecc.hamming74_encode(x)), oracle.hamming74_encode(ref))
+    d, t, st = kvecc.hamming84_decode(x, return_error_types=True)
+    od, ot, ost = oracle.hamming84_decode(ref)
+    assert np.array_equal(_np(d), od) and np.array_equal(_np(t), ot) and st == ost
+    d, f, st = kvecc.hamming74_decode(x, return_error_detected=True)
+    od, of, ost = oracle.hamming74_decode(ref)
+    assert np.array_equal(_np(d), od) and np.array_equal(_np(f), of) and st == ost
+
+
+def test_hamming84_full_config_roundtrip(gpu):
+    """BASELINE config 2 shape: encode -> decode is the identity, no errors."""
+    import kvecc
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), generator=g, dtype=torch.uint8).to(gpu)
+    cw = kvecc.hamming84_encode(x)
+    d, (c, det) = kvecc.hamming84_decode(cw)
+    assert torch.equal(d, x) and c == 0 and det == 0
+    # flip bit k of every codeword: singles everywhere, all corrected
+    for k in (0, 5, 7):
+        d, t, (c, det) = kvecc.hamming84_decode(cw ^ (1 << k), return_error_types=True)
+        assert torch.equal(d, x)
+        assert c == x.numel() if k < 7 else c == 0
+        if k == 7:
+            assert int((t == 3).sum()) == x.numel()
+
+
+# ---------------------------------------------------------------------------
+# Golay
+# ---------------------------------------------------------------------------
+
+def test_golay_golden(gpu, golden):
+    import kvecc
+    g = golden("golay")
+    out = kvecc.golay_encode(_t(g["enc_in"], gpu))
+    assert np.array_equal(_np(out), g["enc_out"])
+    trip, cnt, st = kvecc.golay_decode(_t(g["dec_in"], gpu), return_error_counts=True)
+    assert np.array_equal(_np(trip), g["dec_trip"])
+    assert np.array_equal(_np(cnt), g["dec_count"])
+    assert st == tuple(g["dec_stats"].tolist())
+
+
+@pytest.mark.parametrize("m", [1, 5, 4095, 4096, 4097, 4096 * 7 + 1001, 1_000_003])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_golay_random_vs_oracle(gpu, oracle, m, offset):
+    import kvecc
+    rng = np.random.default_rng(m * 7 + offset)
+    trip = rng.integers(0, 256, size=(m + offset, 3), dtype=np.int64).astype(np.uint8)
+    t = _t(trip, gpu)[offset:]
+    cw = kvecc.golay_encode(t)
+    ocw = oracle.golay_encode(trip[offset:])
+    assert np.array_equal(_np(cw), ocw)
+    # random 0..5 bit errors plus a few garbage words
+    noisy = ocw.astype(np.int64)
+    nerr = rng.integers(0, 6, size=m)
+    for k in range(6):
+        sel = nerr > k
+        noisy[sel] ^= 1 << rng.integers(0, 24, size=int(sel.sum()))
+    noisy[::97] = rng.integers(-(2**31), 2**31, size=noisy[::97].size)
+    noisy = noisy.astype(np.int32)
+    buf = np.concatenate([np.zeros(offset, np.int32), noisy])
+    x = _t(buf, gpu)[offset:]
+    d, c, st = kvecc.golay_decode(x, return_error_counts=True)
+    od, oc, ost = oracle.golay_decode(noisy)
+    assert np.array_equal(_np(d), od)
+    assert np.array_equal(_np(c), oc)
+    assert st == ost
+
+
+def test_golay_full_config_roundtrip(gpu, oracle):
+    """BASELINE config 3 shape with per-head packing: rows of 128 -> 43 codewords."""
+    import kvecc
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), generator=g, dtype=torch.uint8).to(gpu)
+    cw = kvecc.ops.golay_encode_rows(x)
+    assert cw.shape == (8, 4096, 32, 43)
+    # sample rows against the oracle's padded triplet encode
+    xs = x.view(-1, 128)[:: 997].cpu().numpy()
+    pad = np.zeros((xs.shape[0], 129), np.uint8)
+    pad[:, :128] = xs
+    ref = oracle.golay_encode(pad.reshape(-1, 3)).reshape(-1, 43)
+    assert np.array_equal(_np(cw.view(-1, 43)[:: 997]), ref)
+    stats = kvecc.ops.new_stats(gpu)
+    back = kvecc.ops.golay_decode_rows(cw, 128, stats)
+    assert torch.equal(back, x) and stats.tolist() == [0, 0]
+    # flat triplet API on the padded layout gives the same codewords
+    padded = torch.zeros(8, 4096, 32, 129, dtype=torch.uint8, device=gpu)
+    padded[..., :128] = x
+    cw2 = kvecc.golay_encode(padded.view(-1, 3))
+    assert torch.equal(cw2, cw.view(-1))
+    trip, (bits, unc) = kvecc.golay_decode(cw2)
+    assert torch.equal(trip.view(8, 4096, 32, 129), padded) and bits == 0 and unc == 0
+
+
+# ---------------------------------------------------------------------------
+# Fault injection
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("tag", ["inject", "inject_vec"])
+def test_inject_golden(gpu, golden, manifest, tag):
+    import kvecc
+    g = golden(tag)
+    fn = (kvecc.inject_bit_errors_triton if tag == "inject"
+          else kvecc.inject_bit_errors_triton_vectorized)
+    for i, c in enumerate(manifest[tag]["params"]["cases"]):
+        x = _t(g[f"c{i}_in"], gpu)
+        out, st = fn(x, c["ber"], c["n_bits"], seed=c["seed"], return_stats=True)
+        assert np.array_equal(_np(out), g[f"c{i}_out"]), (tag, c)
+        assert st == tuple(g[f"c{i}_stats"].tolist()), (tag, c)
+
+
+def test_inject_ber_zero_aliases_input(gpu):
+    import kvecc
+    x = torch.arange(100, dtype=torch.uint8, device=gpu)
+    assert kvecc.inject_bit_errors_triton(x, 0.0, 8) is x
+    with pytest.raises(ValueError):
+        kvecc.inject_bit_errors_triton(x.float(), 0.1, 8)
+
+
+@pytest.mark.parametrize("dtype,nb", [("u8", 8), ("u8", 7), ("u8", 4), ("i32", 24), ("u8", 5),
+                                      ("i32", 11)])
+def test_inject_random_vs_oracle(gpu, oracle, dtype, nb):
+    import kvecc
+    rng = np.random.default_rng(nb)
+    n = 200_003
+    if dtype == "u8":
+        x = rng.integers(0, 256, size=n, dtype=np.int64).astype(np.uint8)
+    else:
+        x = rng.integers(-(2**31), 2**31, size=n, dtype=np.int64).astype(np.int32)
+    for seed, ber in ((42, 1e-2), (2**30 + 5, 0.3), (0, 1e-3)):
+        out, st = kvecc.inject_bit_errors_triton(_t(x, gpu), ber, nb, seed=seed, return_stats=True)
+        o, _, ost = oracle.inject(x, ber, nb, seed)
+        assert np.array_equal(_np(out), o) and st == ost, (seed, ber)
+
+
+def test_inject_sharded_equals_flat(gpu):
+    """Monte-Carlo sharding: (global_n, offset0) shards reproduce the flat run."""
+    from kvecc import ops
+    n = 1_000_000
+    x = torch.randint(0, 2**24, (n,), dtype=torch.int32, device=gpu)
+    full = torch.empty_like(x)
+    st_full = ops.new_stats(gpu)
+    ops.inject_into(x, full, 1e-2, 24, seed=42, stats=st_full)
+    parts = torch.empty_like(x)
+    st = ops.new_stats(gpu)
+    bounds = [0, 123_457, 500_000, 999_999, n]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        ops.inject_into(x[a:b], parts[a:b], 1e-2, 24, seed=42, stats=st, global_n=n, offset0=a)
+    assert torch.equal(full, parts) and st.tolist() == st_full.tolist()
+
+
+def test_inject_full_config_sampled(gpu, oracle):
+    """BASELINE config 2/3 sizes: sampled elements vs the oracle + BER fidelity."""
+    import kvecc
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), generator=g, dtype=torch.uint8).to(gpu)
+    cw = kvecc.hamming84_encode(x)
+    out, (flips, aff) = kvecc.inject_bit_errors_triton(cw, 1e-3, 8, seed=42, return_stats=True)
+    n = cw.numel()
+    assert abs(flips / (n * 8) - 1e-3) < 1e-5
+    idx = np.random.default_rng(1).integers(0, n, size=3000)
+    src = _np(cw.view(-1)[torch.from_numpy(idx).to(gpu)])
+    got = _np(out.view(-1)[torch.from_numpy(idx).to(gpu)])
+    for i, s, o in zip(idx, src, got):
+        ref, _, _ = oracle.inject(np.array([s], np.uint8), 1e-3, 8, 42, global_n=n, offset0=int(i))
+        assert ref[0] == o, i
+    # Golay per-head layout, 24 bits per codeword at BER 1e-2
+    cwg = kvecc.ops.golay_encode_rows(x).view(-1)
+    outg, (fg, ag) = kvecc.inject_bit_errors_triton(cwg, 1e-2, 24, seed=42, return_stats=True)
+    m = cwg.numel()
+    assert abs(fg / (m * 24) - 1e-2) < 1e-4
+    idx = np.random.default_rng(2).integers(0, m, size=2000)
+    src = _np(cwg[torch.from_numpy(idx).to(gpu)])
+    got = _np(outg[torch.from_numpy(idx).to(gpu)])
+    for i, s, o in zip(idx, src, got):
+        ref, _, _ = oracle.inject(np.array([s], np.int32), 1e-2, 24, 42, global_n=m, offset0=int(i))
+        assert ref[0] == o, i
+
+
+@pytest.mark.parametrize("dtype,row_len,nb", [("u8", 128, 8), ("u8", 64, 7), ("i32", 43, 24),
+                                              ("u8", 64, 4)])
+def test_inject_rows_vs_oracle(gpu, oracle, dtype, row_len, nb):
+    """Shim per-row scheme: row r is its own call with seed_base + r, N = row_len."""
+    from kvecc import ops
+    rng = np.random.default_rng(row_len)
+    rows = 300
+    if dtype == "u8":
+        x = rng.integers(0, 256, size=rows * row_len, dtype=np.int64).astype(np.uint8)
+    else:
+        x = rng.integers(0, 2**24, size=rows * row_len, dtype=np.int64).astype(np.int32)
+    xt = _t(x, gpu)
+    out = torch.empty_like(xt)
+    st = ops.new_stats(gpu)
+    ops.inject_rows_into(xt, out, rows, row_len, 0.05, nb, seed_base=1000, stats=st)
+    ref = np.concatenate([oracle.inject(x[r * row_len:(r + 1) * row_len], 0.05, nb, 1000 + r)[0]
+                          for r in range(rows)])
+    assert np.array_equal(_np(out), ref)
+    # in place
+    ops.inject_rows_into(xt, xt, rows, row_len, 0.05, nb, seed_base=1000)
+    assert np.array_equal(_np(xt), ref)
+
+
+# ---------------------------------------------------------------------------
+# Interpolation
+# ---------------------------------------------------------------------------
+
+def test_interp_golden(gpu, golden, manifest):
+    import kvecc
+    g = golden("interp")
+    for i, c in enumerate(manifest["interp"]["params"]["cases"]):
+        q = _t(g[f"c{i}_q"], gpu)
+        e = _t(g[f"c{i}_err"], gpu)
+        out = kvecc.interpolate_double_errors(q, e, seq_dim=c["seq_dim"])
+        assert np.array_equal(_np(out), g[f"c{i}_out"]), c
+
+
+@pytest.mark.parametrize("shape,seq_dim", [((1024, 12, 64), 0), ((37, 5, 48), 0),
+                                           ((100, 7, 3), 0), ((4, 1000), -1), ((5000,), -1),
+                                           ((3, 64, 16, 32), 1), ((2, 3, 4, 5), 2), ((1, 16, 16), 0)])
+def test_interp_random_vs_oracle(gpu, oracle, shape, seq_dim):
+    import kvecc
+    rng = np.random.default_rng(len(shape))
+    q = rng.integers(0, 16, size=shape, dtype=np.int64).astype(np.uint8)
+    e = rng.choice(np.array([0, 1, 2, 3], np.uint8), size=shape, p=[0.6, 0.1, 0.25, 0.05])
+    out = kvecc.interpolate_double_errors(_t(q, gpu), _t(e, gpu), seq_dim=seq_dim)
+    assert np.array_equal(_np(out), oracle.interpolate_double_errors(q, e, seq_dim=seq_dim))
+
+
+def test_interp_fast_path_keeps_values(gpu):
+    import kvecc
+    q = torch.tensor([200, 17, 3, 99], dtype=torch.uint8, device=gpu)
+    e = torch.tensor([0, 1, 3, 0], dtype=torch.uint8, device=gpu)
+    assert torch.equal(kvecc.interpolate_double_errors(q, e), q)
+    e[1] = 2
+    assert kvecc.interpolate_double_errors(q, e).tolist() == [15, 15, 3, 15]
+
+
+# ---------------------------------------------------------------------------
+# Fused quantize/encode, decode/dequantize
+# ---------------------------------------------------------------------------
+
+def test_fused_golden(gpu, golden, manifest):
+    import kvecc
+    g = golden("fused")
+    for i, c in enumerate(manifest["fused"]["params"]["cases"]):
+        x = _t(g[f"c{i}_x"], gpu)
+        cw, s = kvecc.fused_quantize_encode_hamming84(x)
+        assert np.array_equal(_np(cw), g[f"c{i}_cw84"]) and np.array_equal(_np(s), g[f"c{i}_s84"])
+        cw, s = kvecc.fused_quantize_encode_hamming74(x)
+        assert np.array_equal(_np(cw), g[f"c{i}_cw74"])
+        out, nc = kvecc.fused_decode_dequantize_hamming84(_t(g[f"c{i}_cw_noisy"], gpu),
+                                                          _t(g[f"c{i}_s84"], gpu))
+        assert np.array_equal(_np(out), g[f"c{i}_dq"]) and nc == int(g[f"c{i}_ncorr"][0])
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(4096, 128), (333, 64), (17, 100), (5, 7), (2, 3, 256)])
+def test_quantize_vs_torch_path(gpu, oracle, dtype, shape):
+    """Exactly the shim's torch rounding (ecc_shim.py:572-580) for every dtype."""
+    import kvecc
+    g = torch.Generator().manual_seed(sum(shape))
+    x = (torch.randn(*shape, generator=g) * 3).to(dtype)
+    x.view(-1, shape[-1])[0] = 0
+    xd = x.to(gpu)
+    q, s = kvecc.ops.quantize_rows(xd)
+    oq, os_ = oracle.quantize_rows(x.float().numpy())
+    assert np.array_equal(_np(q), oq) and np.array_equal(_np(s), os_)
+    cw, s84 = kvecc.fused_quantize_encode_hamming84(xd)
+    assert np.array_equal(_np(cw), oracle.hamming84_encode(oq))
+    # decode + dequant to the input dtype (== torch .to(dtype) of the fp32 result)
+    out, nc = kvecc.fused_decode_dequantize_hamming84(cw, s84, output_dtype=dtype)
+    ref, _ = oracle.decode_dequant_h84(oracle.hamming84_encode(oq), os_)
+    assert torch.equal(out.cpu(), torch.from_numpy(ref).to(dtype)) and nc == 0

@@ -1,0 +1,108 @@
+"""CPU-only checks of the C ABI library (no kernel launches).
+
+* libkvecc.so loads and exports every function include/kvecc.h declares;
+* the host-side code tables of the product equal the oracle's (and hence the
+  reference's golden table);
+* the integer BER threshold the kernels use is exactly the reference's
+  fp32 `tl.rand < ber` test.
+"""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tests.conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "kvecc.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"KVECC_API\s+[\w\s\*]+?\b(kvecc_\w+)\s*\(", text)))
+
+
+def test_header_declares_api():
+    names = _declared()
+    assert "kvecc_golay_decode" in names and "kvecc_inject_u8" in names
+    assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol():
+    from kvecc import _lib
+    lib = _lib.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    # and the Python binding covers the whole ABI
+    assert set(_declared()) == set(_lib.SIGNATURES)
+
+
+def test_exported_symbols_are_only_the_abi():
+    """-fvisibility=hidden: nothing but kvecc_* leaks from the library."""
+    import subprocess
+    from kvecc import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert syms and all(s.startswith("kvecc_") for s in syms), sorted(syms)[:10]
+
+
+def test_version_and_no_device_errors():
+    from kvecc import _lib
+    assert _lib.version().startswith("kvecc")
+    lib = _lib.load()
+    # argument validation runs before any device work
+    rc = lib.kvecc_hamming84_encode(None, None, -1, None)
+    assert rc == -1 and b"negative" in lib.kvecc_last_error()
+    assert lib.kvecc_hamming84_encode(None, None, 0, None) == 0  # empty is valid
+
+
+def test_golay_tables_match_oracle(oracle, golden):
+    from kvecc import config
+    t = config.build_golay_syndrome_table().numpy()
+    assert np.array_equal(t, oracle.golay_syndrome_table())
+    assert np.array_equal(t, golden("golay")["table"])
+    masks = np.zeros(12, np.uint32)
+    from kvecc import _lib
+    _lib.call("kvecc_golay_h_row_masks_host", ctypes.c_void_p(masks.ctypes.data))
+    assert np.array_equal(masks, oracle.golay_h_row_masks())
+    assert tuple(int(m) for m in masks) == config.GOLAY_H_ROW_MASKS
+
+
+def test_config_matrices():
+    import torch
+    from kvecc import config
+    g, h = config.HAMMING74_G.int(), config.HAMMING74_H.int()
+    assert ((g @ h.T) % 2).sum() == 0
+    b = config.GOLAY_B_MATRIX.int()
+    assert torch.equal(b, b.T) and torch.equal((b @ b) % 2, torch.eye(12, dtype=torch.int32))
+    assert config.get_physical_dtype("golay") == torch.int32
+    with pytest.raises(ValueError):
+        config.get_codeword_bits("bch")
+
+
+@pytest.mark.parametrize("ber", [1e-4, 1e-3, 1e-2, 0.05, 0.2, 0.5, 0.999, 1.0, 2.0, 1e-9,
+                                 float("nan"), 0.0, -1.0, 3.3e-3])
+def test_ber_threshold_is_exact(oracle, ber):
+    from kvecc import _lib
+    thr = _lib.load().kvecc_ber_threshold(ber)
+    fber = float(np.float32(ber))
+    probe = set(range(max(0, thr - 300), min(2**31, thr + 300)))
+    rng = np.random.default_rng(0)
+    probe |= set(rng.integers(0, 2**31, size=2000).tolist())
+    probe |= {0, 1, 2**31 - 1}
+    for x in probe:
+        u = oracle.uint_to_uniform(x)  # fold(x) = x for x >= 0
+        assert (u < fber) == (x < thr), (ber, x, thr)
+        # negative words fold to ~x
+        u2 = oracle.uint_to_uniform((~x) & 0xFFFFFFFF)
+        assert (u2 < fber) == (x < thr)
+
+
+def test_backend_registry():
+    from kvecc import backends
+    with pytest.raises(ValueError):
+        backends.get_codec_backend("cuda-triton")
+    assert "hip" in backends.available_backends()
