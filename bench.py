@@ -150,7 +150,7 @@ def main():
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
     tt = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
-    st = stats.clone()
+    st = ops.stats_totals(stats)
     if dist is not None:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(st, op=dist.ReduceOp.SUM)     # the single stats all-reduce
@@ -164,7 +164,7 @@ def main():
         ops.golay_decode_into(cw, out_trip, counts, chk)  # clean codewords round-trip
         torch.cuda.synchronize()
         assert torch.equal(out_trip.view(-1, 3), trip), "encode->decode round trip failed"
-        assert chk.tolist() == [0, 0]
+        assert ops.read_stats(chk) == [0, 0]
 
     # ---- injection throughput (VALU-bound, Philox4x32-10 per bit) ------------
     inject = None
@@ -179,7 +179,7 @@ def main():
         torch.cuda.synchronize()
         inj_ms = e0.elapsed_time(e1) / reps
         inject = {"ms": round(inj_ms, 4), "codewords_per_s": m / (inj_ms * 1e-3),
-                  "philox_per_s": m * 24 / (inj_ms * 1e-3), "flips": int(inj_stats[0]),
+                  "philox_per_s": m * 24 / (inj_ms * 1e-3), "flips": ops.read_stats(inj_stats)[0],
                   "bound": "valu"}
 
     if rank != 0:

@@ -15,8 +15,13 @@
  *   - `stream` is a hipStream_t (NULL = legacy default stream).  Calls only
  *     enqueue work: no allocation, no host synchronisation (graph-capturable
  *     once kvecc_init_device() has run for the device).
- *   - Statistics accumulate (+=) into a caller-provided device uint64_t array,
- *     or are skipped when the pointer is NULL.  Zero it to start a count.
+ *   - Statistics accumulate (+=) into a caller-provided, zero-initialised device
+ *     buffer of KVECC_STATS_WORDS uint64 words, or are skipped when the pointer
+ *     is NULL.  The buffer is sharded: workgroup g adds its partial sums to
+ *     slot (g % KVECC_STATS_SLOTS), one 128-byte line per slot, and statistic k
+ *     (the "stats[k]" named below) is  sum over s of buf[s*KVECC_STATS_STRIDE + k].
+ *     (Thousands of device-scope atomics on ONE address serialise at ~10 ns
+ *     each -- longer than the kernels themselves.)
  *   - Return 0 on success, a negative KVECC_E* code on failure; the message is
  *     available from kvecc_last_error() (thread-local).
  *   - n / m / rows == 0 is valid and enqueues nothing.
@@ -38,6 +43,11 @@ enum {
   KVECC_EHIP = -2,   /* HIP runtime error (launch / memory)                  */
   KVECC_ENODEV = -3  /* no HIP device                                         */
 };
+
+/* statistics buffer geometry (see conventions above) */
+#define KVECC_STATS_SLOTS 32
+#define KVECC_STATS_STRIDE 16 /* uint64 words per slot = one 128-B line */
+#define KVECC_STATS_WORDS (KVECC_STATS_SLOTS * KVECC_STATS_STRIDE)
 
 /* dtype codes for fused kernels */
 enum { KVECC_F32 = 0, KVECC_F16 = 1, KVECC_BF16 = 2 };

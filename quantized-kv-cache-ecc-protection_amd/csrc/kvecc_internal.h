@@ -55,20 +55,31 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// accumulate two per-lane counters into stats[0..1] with one atomic per wave
+// Add two per-lane counters to the sharded statistics buffer (kvecc.h): the
+// workgroup reduces through LDS and its first lane issues one atomic per
+// statistic into slot (blockIdx % KVECC_STATS_SLOTS).  Blocks b and b+8 share
+// an XCD under round-robin dispatch, so each slot's adds come from one XCD.
+// Must be reached by every thread of the block (it contains a barrier).
 __device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32_t b) {
+  __shared__ uint32_t red[2][kBlock / kWave];
   a = wave_sum(a);
   b = wave_sum(b);
+  const int wave = threadIdx.x / kWave;
   if ((threadIdx.x & (kWave - 1)) == 0) {
-    if (a) atomicAdd(reinterpret_cast<unsigned long long *>(stats), (unsigned long long)a);
-    if (b) atomicAdd(reinterpret_cast<unsigned long long *>(stats + 1), (unsigned long long)b);
+    red[0][wave] = a;
+    red[1][wave] = b;
   }
-}
-
-__device__ __forceinline__ void flush_stats1(uint64_t *stats, uint32_t a) {
-  a = wave_sum(a);
-  if ((threadIdx.x & (kWave - 1)) == 0 && a)
-    atomicAdd(reinterpret_cast<unsigned long long *>(stats), (unsigned long long)a);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long sa = 0, sb = 0;
+    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) {
+      sa += red[0][w];
+      sb += red[1][w];
+    }
+    uint64_t *slot = stats + (size_t)(blockIdx.x % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (sa) atomicAdd(reinterpret_cast<unsigned long long *>(slot), sa);
+    if (sb) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), sb);
+  }
 }
 
 // per-byte parity of four packed bytes: bit 0 of each byte = XOR of its 8 bits

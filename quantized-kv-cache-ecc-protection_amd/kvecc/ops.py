@@ -50,9 +50,23 @@ def _ensure_device(device):
     return idx
 
 
-def new_stats(device, n=2):
-    """Zeroed device statistics accumulator (int64, read as uint64 by the kernels)."""
-    return torch.zeros(n, dtype=torch.int64, device=device)
+STATS_SLOTS = 32    # KVECC_STATS_SLOTS
+STATS_STRIDE = 16   # KVECC_STATS_STRIDE (uint64 words per slot)
+
+
+def new_stats(device):
+    """Zeroed sharded statistics buffer (include/kvecc.h: KVECC_STATS_WORDS words)."""
+    return torch.zeros(STATS_SLOTS * STATS_STRIDE, dtype=torch.int64, device=device)
+
+
+def stats_totals(stats, n=2):
+    """Device tensor [n] of statistic totals (sum over the slots); no host sync."""
+    return stats.view(STATS_SLOTS, STATS_STRIDE)[:, :n].sum(0)
+
+
+def read_stats(stats, n=2):
+    """Host ints of the first n statistics (one device->host sync)."""
+    return [int(v) for v in stats_totals(stats, n).tolist()]
 
 
 def _flat(t, dtype):
@@ -108,9 +122,9 @@ def hamming74_decode(codewords: torch.Tensor, return_error_detected: bool = Fals
     flat = _flat(codewords, torch.uint8)
     data = torch.empty_like(flat)
     flag = torch.empty_like(flat)
-    stats = new_stats(flat.device, 1)
+    stats = new_stats(flat.device)
     hamming74_decode_into(flat, data, flag, stats)
-    n = int(stats[0])
+    n = read_stats(stats, 1)[0]
     data = data.view(codewords.shape)
     flag = flag.view(codewords.shape)
     if return_error_detected:
@@ -139,7 +153,7 @@ def hamming84_decode(codewords: torch.Tensor, return_error_types: bool = False):
     etype = torch.empty_like(flat)
     stats = new_stats(flat.device)
     hamming84_decode_into(flat, data, etype, stats)
-    corrected, detected = stats.tolist()
+    corrected, detected = read_stats(stats)
     data = data.view(codewords.shape)
     etype = etype.view(codewords.shape)
     if return_error_types:
@@ -193,7 +207,7 @@ def golay_decode(codewords: torch.Tensor, return_error_counts: bool = False):
     counts = torch.empty(n, dtype=torch.uint8, device=codewords.device)
     stats = new_stats(codewords.device)
     golay_decode_into(flat, trip, counts, stats)
-    bits, unc = stats.tolist()
+    bits, unc = read_stats(stats)
     trip = trip.view(n, 3)
     if return_error_counts:
         return trip, counts, (bits, unc)
@@ -282,7 +296,7 @@ def inject_bit_errors_triton(data, ber, n_bits, seed=0, return_stats=False):
     inject_into(flat, out, ber, n_bits, seed, stats=stats)
     out = out.view(data.shape)
     if return_stats:
-        flips, affected = stats.tolist()
+        flips, affected = read_stats(stats)
         return out, (flips, affected)
     return out
 
@@ -317,7 +331,7 @@ def inject_bit_errors_triton_vectorized(data, ber, n_bits, seed=0, return_stats=
               _ptr(stats), _stream(data.device))
     out = out.view(data.shape)
     if return_stats:
-        flips, affected = stats.tolist()
+        flips, affected = read_stats(stats)
         return out, (flips, affected)
     return out
 
@@ -459,7 +473,7 @@ def fused_decode_dequantize_hamming84(codewords, scales, output_dtype=torch.floa
     out = torch.empty(cw.shape, dtype=dtype, device=codewords.device)
     stats = new_stats(codewords.device)
     decode_dequant_h84_into(cw, sc, out, True, stats)
-    corrected = int(stats[0])
+    corrected = read_stats(stats, 1)[0]
     out = out.squeeze(0) if codewords.dim() == 1 else out.view(shape)
     if output_dtype != dtype:
         out = out.to(output_dtype)
