@@ -13,29 +13,37 @@
 //    instead of the reference's 12 masked popcounts, and the correction comes
 //    from `correct`, which folds the reference's error-pattern table and its
 //    popcount.  Only the data half of an error pattern matters for the output.
-//  * Each lane owns 16 codewords as 4 groups of 4 consecutive codewords, and
-//    each wave-instruction covers one contiguous span (1 KiB of codewords,
-//    768 B of triplets, 256 B of counts), so every access is fully coalesced:
-//    4 x global_load_dwordx4 (codewords) and 4 x (dwordx3 + dword) stores.
-//  * Workgroups walk a contiguous chunk of tiles (grid-stride) so the 16 KiB
-//    table fill is amortised over many tiles.
+//  * Each lane owns kGroups groups of 4 consecutive codewords, and each
+//    wave-instruction covers one contiguous span (1 KiB of codewords, 768 B
+//    of triplets, 256 B of counts), so every access is fully coalesced:
+//    global_load_dwordx4 (codewords), dwordx3 + dword stores (decode), all
+//    non-temporal (plain stores ran at ~65% of the nt rate).
+//  * Geometry measured on MI355X with interleaved cold-cache A/B runs
+//    (tools/exp/run_exp2.py, run_exp3.py): 2 groups per lane, 512-thread
+//    decode / 1024-thread encode workgroups, up to 32 / 16 workgroups per CU
+//    grid-strided.  More work per lane (4 groups) or lane-contiguous layouts
+//    lost 8-45%; computing the parity with VALU instead of the LDS table lost
+//    12-20% (the kernel turns VALU-bound).
 #include "kvecc_internal.h"
 
 namespace kvecc {
 
-constexpr int kCwPerLane = 16;
-constexpr int kTile = kBlock * kCwPerLane;  // 4096 codewords per workgroup tile
+constexpr int kGroups = 2;                          // 4-codeword groups per lane per tile
+constexpr int kDecBlock = 512, kEncBlock = 1024;    // threads per workgroup
+constexpr int kDecTile = kDecBlock * kGroups * 4;   // 4096 codewords
+constexpr int kEncTile = kEncBlock * kGroups * 4;   // 8192 codewords
+constexpr int kWaveCw = kWave * kGroups * 4;        // codewords per wave per tile
 
-// copy both 4096-entry tables (16 KiB) into LDS
+// copy the 4096-entry tables (8 KiB each) into LDS
+template <int BS>
 __device__ __forceinline__ void load_tables(uint16_t *lds, const uint16_t *__restrict__ par,
                                             const uint16_t *__restrict__ cor, bool need_cor) {
   const u32x4 *p = reinterpret_cast<const u32x4 *>(par);
   u32x4 *l = reinterpret_cast<u32x4 *>(lds);
-  // 8 KiB = 512 x 16 B per table
-  for (int i = threadIdx.x; i < 512; i += kBlock) l[i] = p[i];
+  for (int i = threadIdx.x; i < 512; i += BS) l[i] = p[i];
   if (need_cor) {
     const u32x4 *c = reinterpret_cast<const u32x4 *>(cor);
-    for (int i = threadIdx.x; i < 512; i += kBlock) l[512 + i] = c[i];
+    for (int i = threadIdx.x; i < 512; i += BS) l[512 + i] = c[i];
   }
   __syncthreads();
 }
@@ -60,27 +68,27 @@ __device__ __forceinline__ void unpack_triplets(uint32_t w0, uint32_t w1, uint32
   d[3] = pack_data(w2 >> 8, w2 >> 16, w2 >> 24);
 }
 
-__global__ __launch_bounds__(kBlock) void golay_encode_kernel(const uint32_t *__restrict__ trip,
-                                                              u32x4 *__restrict__ cw,
-                                                              int64_t ntiles,
-                                                              const uint16_t *__restrict__ par) {
+__global__ __launch_bounds__(kEncBlock) void golay_encode_kernel(const uint32_t *__restrict__ trip,
+                                                                 u32x4 *__restrict__ cw,
+                                                                 int64_t ntiles,
+                                                                 const uint16_t *__restrict__ par) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[4096];
-  load_tables(lds, par, nullptr, false);
+  load_tables<kEncBlock>(lds, par, nullptr, false);
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    // codeword index of this lane's group g: tile*4096 + wave*1024 + g*256 + lane*4
-    const int64_t base = t * kTile + wave * (kWave * kCwPerLane) + lane * 4;
-    uint32_t w[4][3];
+    // codeword index of this lane's group g: tile + wave*kWaveCw + g*256 + lane*4
+    const int64_t base = t * kEncTile + wave * kWaveCw + lane * 4;
+    uint32_t w[kGroups][3];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < kGroups; ++g) {
       const uint32_t *p = trip + (base + g * 256) * 3 / 4;  // 12 B per 4 codewords
       w[g][0] = ld_stream(p);
       w[g][1] = ld_stream(p + 1);
       w[g][2] = ld_stream(p + 2);
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < kGroups; ++g) {
       uint32_t d[4];
       unpack_triplets(w[g][0], w[g][1], w[g][2], d);
       u32x4 out;
@@ -121,25 +129,25 @@ __device__ __forceinline__ uint32_t decode_one(uint32_t w, const uint16_t *lds, 
 }
 
 template <bool WITH_COUNTS, bool WITH_STATS>
-__global__ __launch_bounds__(kBlock) void golay_decode_kernel(const u32x4 *__restrict__ cw,
-                                                              uint32_t *__restrict__ trip,
-                                                              uint32_t *__restrict__ counts,
-                                                              int64_t ntiles,
-                                                              const uint16_t *__restrict__ par,
-                                                              const uint16_t *__restrict__ cor,
-                                                              uint64_t *__restrict__ stats) {
+__global__ __launch_bounds__(kDecBlock) void golay_decode_kernel(const u32x4 *__restrict__ cw,
+                                                                 uint32_t *__restrict__ trip,
+                                                                 uint32_t *__restrict__ counts,
+                                                                 int64_t ntiles,
+                                                                 const uint16_t *__restrict__ par,
+                                                                 const uint16_t *__restrict__ cor,
+                                                                 uint64_t *__restrict__ stats) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[8192];
-  load_tables(lds, par, cor, true);
+  load_tables<kDecBlock>(lds, par, cor, true);
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   uint32_t bits = 0, unc = 0;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t base = t * kTile + wave * (kWave * kCwPerLane) + lane * 4;
-    u32x4 v[4];
+    const int64_t base = t * kDecTile + wave * kWaveCw + lane * 4;
+    u32x4 v[kGroups];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) v[g] = ld_stream(cw + (base + g * 256) / 4);
+    for (int g = 0; g < kGroups; ++g) v[g] = ld_stream(cw + (base + g * 256) / 4);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < kGroups; ++g) {
       uint32_t c0, c1, c2, c3;
       uint32_t e0 = spread_nibbles(decode_one(v[g].x, lds, c0));
       uint32_t e1 = spread_nibbles(decode_one(v[g].y, lds, c1));
@@ -159,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void golay_decode_kernel(const u32x4 *__res
       }
     }
   }
-  if (WITH_STATS) flush_stats2(stats, bits, unc);
+  if (WITH_STATS) flush_stats2<kDecBlock>(stats, bits, unc);
 }
 
 __global__ __launch_bounds__(kBlock) void golay_decode_tail_kernel(
@@ -245,14 +253,14 @@ KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, in
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
   if (aligned(triplets, 4) && aligned(codewords, 16)) {
-    int64_t ntiles = m / kTile;
+    int64_t ntiles = m / kEncTile;
     if (ntiles > 0) {
-      unsigned g = grid_for(ntiles, 4, 8);  // >= ~4 tiles per workgroup
-      hipLaunchKernelGGL(golay_encode_kernel, dim3(g), dim3(kBlock), 0, st,
+      unsigned g = grid_for(ntiles, 1, 16);  // <= 16 workgroups per CU, grid-strided
+      hipLaunchKernelGGL(golay_encode_kernel, dim3(g), dim3(kEncBlock), 0, st,
                          reinterpret_cast<const uint32_t *>(triplets),
                          reinterpret_cast<u32x4 *>(codewords), ntiles, par);
     }
-    done = ntiles * kTile;
+    done = ntiles * kEncTile;
   }
   if (done < m) {
     unsigned g = grid_for(m - done, kBlock);
@@ -273,22 +281,23 @@ KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, ui
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
   if (aligned(codewords, 16) && aligned(triplets, 4) && (!counts || aligned(counts, 4))) {
-    int64_t ntiles = m / kTile;
+    int64_t ntiles = m / kDecTile;
     if (ntiles > 0) {
-      unsigned g = grid_for(ntiles, 4, 8);
+      unsigned g = grid_for(ntiles, 1, 32);  // <= 32 workgroups per CU, grid-strided
       auto c = reinterpret_cast<const u32x4 *>(codewords);
       auto t = reinterpret_cast<uint32_t *>(triplets);
       auto n = reinterpret_cast<uint32_t *>(counts);
+      const dim3 b(kDecBlock);
       if (counts && stats)
-        hipLaunchKernelGGL((golay_decode_kernel<true, true>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+        hipLaunchKernelGGL((golay_decode_kernel<true, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
       else if (counts)
-        hipLaunchKernelGGL((golay_decode_kernel<true, false>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+        hipLaunchKernelGGL((golay_decode_kernel<true, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
       else if (stats)
-        hipLaunchKernelGGL((golay_decode_kernel<false, true>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+        hipLaunchKernelGGL((golay_decode_kernel<false, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
       else
-        hipLaunchKernelGGL((golay_decode_kernel<false, false>), dim3(g), dim3(kBlock), 0, st, c, t, n, ntiles, par, cor, stats);
+        hipLaunchKernelGGL((golay_decode_kernel<false, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
     }
-    done = ntiles * kTile;
+    done = ntiles * kDecTile;
   }
   if (done < m) {
     unsigned g = grid_for(m - done, kBlock);

@@ -59,9 +59,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // workgroup reduces through LDS and its first lane issues one atomic per
 // statistic into slot (blockIdx % KVECC_STATS_SLOTS).  Blocks b and b+8 share
 // an XCD under round-robin dispatch, so each slot's adds come from one XCD.
-// Must be reached by every thread of the block (it contains a barrier).
+// Must be reached by every thread of the block (it contains a barrier);
+// BS = the kernel's block size.
+template <int BS = kBlock>
 __device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32_t b) {
-  __shared__ uint32_t red[2][kBlock / kWave];
+  __shared__ uint32_t red[2][BS / kWave];
   a = wave_sum(a);
   b = wave_sum(b);
   const int wave = threadIdx.x / kWave;
@@ -72,7 +74,7 @@ __device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long sa = 0, sb = 0;
-    for (int w = 0; w < (int)(blockDim.x / kWave); ++w) {
+    for (int w = 0; w < BS / kWave; ++w) {
       sa += red[0][w];
       sb += red[1][w];
     }

@@ -1,0 +1,69 @@
+"""Summarise a tools/gpu_check.sh run into profiles/<round>/ and profiles/traffic.json.
+
+HBM traffic per launch = FETCH_SIZE * 2 (gfx950 tallies 128-B streaming reads
+at 64 B, MI355X_MICROARCH.md section HBM) + WRITE_SIZE, both in KiB, from two
+separate --pmc passes.  The median over the profiled launches of each kernel
+is reported next to the kernel's algorithmic bytes.
+
+usage: python tools/pmc_summary.py gpurun_out/r01c profiles/r01
+"""
+
+from __future__ import annotations
+
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M = 8 * 4096 * 32 * 43  # codewords of the bench workload
+ALGO = {"golay_decode_kernel": 8 * M, "golay_encode_kernel": 7 * M}
+
+
+def counters(path):
+    per = {}
+    for r in csv.DictReader(open(path)):
+        per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(dst, exist_ok=True)
+    fetch = counters(glob.glob(os.path.join(src, "pmc_fetch", "*counter_collection.csv"))[0])
+    write = counters(glob.glob(os.path.join(src, "pmc_write", "*counter_collection.csv"))[0])
+    stats_csv = glob.glob(os.path.join(src, "prof", "*kernel_stats.csv"))[0]
+    shutil.copy(stats_csv, os.path.join(dst, "kernel_stats.csv"))
+    stats = {r["Name"]: r for r in csv.DictReader(open(stats_csv))}
+    out = {"source": src, "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1",
+           "kernels": {}}
+    for k in sorted(set(fetch) & set(write)):
+        f = statistics.median(fetch[k]) * 1024 * 2
+        w = statistics.median(write[k]) * 1024
+        entry = {"fetch_bytes": f, "write_bytes": w, "hbm_bytes_per_launch": f + w}
+        if k in ALGO:
+            entry["algorithmic_bytes"] = ALGO[k]
+            entry["traffic_over_algorithmic"] = (f + w) / ALGO[k]
+        if k in stats:
+            entry["avg_ns"] = float(stats[k]["AverageNs"])
+            entry["calls"] = int(stats[k]["Calls"])
+        out["kernels"][k] = entry
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    dec = out["kernels"].get("golay_decode_kernel", {})
+    if dec:
+        with open(os.path.join(REPO, "profiles", "traffic.json"), "w") as fh:
+            json.dump({"golay_decode_bytes_per_launch": dec["hbm_bytes_per_launch"],
+                       "source": os.path.join(dst, "pmc_summary.json")}, fh, indent=1)
+    for name in ("bench.log", "status.txt"):
+        p = os.path.join(src, name)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(dst, name))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
