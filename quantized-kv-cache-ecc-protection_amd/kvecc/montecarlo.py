@@ -1,0 +1,213 @@
+"""Batch-sharded Monte-Carlo fault-injection sweep (BASELINE config 5).
+
+Counterpart of the reference's sweep drivers (evaluation/sweep.py:352-626,
+evaluation/experiments/monte_carlo.py:75-395 and the flat-injection Monte
+Carlo of evaluation/experiments/quantization_ecc_comparison.py:72-247), cut
+down to the codec path: for every (codec, BER, seed) trial, a synthetic INT4
+KV tensor [B, L, H, D] is encoded, corrupted with the reference's Philox bit
+flips, decoded (and interpolated for "hamming84_interp"), and five counters
+are kept: [flips, elements affected, corrected, detected/uncorrectable,
+residual nibble mismatches vs the ground truth].
+
+MI355X layout: one process per GPU; rank r owns batch rows [b0, b1).  The
+fault pattern of a shard is the one the unsharded run would draw, because the
+flat injection is told the global element count and the shard's global
+offset; the ground truth itself is drawn from the same Philox stream
+(BER 0.5 over 4 bits of a zero tensor = uniform nibbles), so it is identical
+for any shard decomposition and reproducible by the test oracle.  Counters
+stay on the device for the whole sweep; the only collective is ONE
+all_reduce(SUM) of the [trials, 5] int64 table at the end (RCCL over xGMI on
+MI355X, gloo in the CPU tests).  Finished trials are appended to a JSONL file,
+so an interrupted sweep resumes where it stopped.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+STAT_NAMES = ("flips", "affected", "corrected", "detected", "mismatches")
+CODECS = ("hamming74", "hamming84", "hamming84_interp", "golay")
+N_BITS = {"hamming74": 7, "hamming84": 8, "hamming84_interp": 8, "golay": 24}
+
+
+@dataclass
+class MonteCarloConfig:
+    shape: tuple = (8, 4096, 32, 128)  # [B, L, H, D]
+    codecs: tuple = CODECS
+    bers: tuple = (1e-4, 1e-3, 1e-2)
+    seeds: tuple = (42, 101, 997)
+    data_seed: int = 0
+    output: str | None = None  # JSONL of finished trials (resume)
+    meta: dict = field(default_factory=dict)
+
+    def trials(self):
+        return [(c, float(b), int(s)) for c in self.codecs for b in self.bers for s in self.seeds]
+
+
+def trial_key(codec, ber, seed):
+    return f"{codec}|{ber:.6g}|{seed}"
+
+
+def shard_bounds(batch, rank, world):
+    """Contiguous split of the batch axis; the first batch % world ranks get one more row."""
+    base, extra = divmod(batch, world)
+    b0 = rank * base + min(rank, extra)
+    return b0, b0 + base + (1 if rank < extra else 0)
+
+
+class HipShard:
+    """One rank's shard of the sweep on an MI355X (kvecc HIP kernels)."""
+
+    def __init__(self, cfg: MonteCarloConfig, rank: int, world: int, device):
+        from . import ops
+        self.ops = ops
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        b, l, h, d = cfg.shape
+        self.b0, self.b1 = shard_bounds(b, rank, world)
+        self.sb = self.b1 - self.b0
+        per_b = l * h * d
+        self.n_total = b * per_b
+        self.off = self.b0 * per_b
+        self.g = (d + 2) // 3
+        self.m_total = b * l * h * self.g
+        self.m_off = self.b0 * l * h * self.g
+        shape = (self.sb, l, h, d)
+        # ground truth: uniform nibbles from the Philox stream, shard-consistent
+        self.x = torch.zeros(shape, dtype=torch.uint8, device=self.dev)
+        if self.sb:
+            ops.inject_into(self.x.view(-1), self.x.view(-1), 0.5, 4, cfg.data_seed,
+                            global_n=self.n_total, offset0=self.off)
+        self.cw8 = torch.empty_like(self.x)
+        self.dec = torch.empty_like(self.x)
+        self.et = torch.empty_like(self.x)
+        self.itp = torch.empty_like(self.x)
+        self.cw32 = torch.empty((self.sb, l, h, self.g), dtype=torch.int32, device=self.dev)
+        self.st_inj = ops.new_stats(self.dev)
+        self.st_dec = ops.new_stats(self.dev)
+
+    def run_trial(self, codec, ber, seed, row):
+        """Accumulate this shard's 5 counters of one trial into `row` (device int64[5])."""
+        ops = self.ops
+        if self.sb == 0:
+            return row
+        self.st_inj.zero_()
+        self.st_dec.zero_()
+        x = self.x.view(-1)
+        if codec == "golay":
+            cw = ops.golay_encode_rows(self.x)
+            flat = cw.view(-1)
+            ops.inject_into(flat, flat, ber, 24, seed, stats=self.st_inj, global_n=self.m_total,
+                            offset0=self.m_off)
+            out = ops.golay_decode_rows(cw, self.cfg.shape[3], stats=self.st_dec)
+        else:
+            enc = ops.hamming74_encode_into if codec == "hamming74" else ops.hamming84_encode_into
+            enc(x, self.cw8.view(-1))
+            c = self.cw8.view(-1)
+            ops.inject_into(c, c, ber, N_BITS[codec], seed, stats=self.st_inj,
+                            global_n=self.n_total, offset0=self.off)
+            if codec == "hamming74":
+                ops.hamming74_decode_into(c, self.dec.view(-1), None, self.st_dec)
+                out = self.dec
+            else:
+                ops.hamming84_decode_into(c, self.dec.view(-1), self.et.view(-1), self.st_dec)
+                out = self.dec
+                if codec == "hamming84_interp":
+                    _, l, h, d = self.cfg.shape
+                    # temporal neighbours along L, each (b, h, d) column a sequence
+                    ops.interpolate_into(self.dec.view(-1), self.et.view(-1), self.itp.view(-1),
+                                         self.sb, l, h * d)
+                    out = self.itp
+        row[0:2] += ops.stats_totals(self.st_inj, 2)
+        row[2:4] += ops.stats_totals(self.st_dec, 2)
+        row[4] += (out != self.x).sum()
+        return row
+
+
+def _load_done(path):
+    done = {}
+    if path and os.path.exists(path):
+        with open(path) as f:
+            for line in f:
+                line = line.strip()
+                if line:
+                    r = json.loads(line)
+                    done[r["key"]] = r
+    return done
+
+
+def run_sweep(cfg: MonteCarloConfig, shard, dist=None, rank=0):
+    """Run every unfinished trial on `shard`, reduce once, return the result rows.
+
+    `shard` provides run_trial(codec, ber, seed, row) and a `.dev` device.
+    """
+    done = _load_done(cfg.output) if rank == 0 else {}
+    if dist is not None:
+        obj = [sorted(done)]
+        dist.broadcast_object_list(obj, src=0)
+        done_keys = set(obj[0])
+    else:
+        done_keys = set(done)
+    todo = [t for t in cfg.trials() if trial_key(*t) not in done_keys]
+    table = torch.zeros((max(len(todo), 1), len(STAT_NAMES)), dtype=torch.int64, device=shard.dev)
+    t0 = time.perf_counter()
+    for i, (codec, ber, seed) in enumerate(todo):
+        shard.run_trial(codec, ber, seed, table[i])
+    if shard.dev.type == "cuda":
+        torch.cuda.synchronize(shard.dev)
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        dist.all_reduce(table, op=dist.ReduceOp.SUM)  # the sweep's single collective
+    rows = []
+    vals = table.cpu().tolist()
+    b, l, h, d = cfg.shape
+    for i, (codec, ber, seed) in enumerate(todo):
+        r = {"key": trial_key(codec, ber, seed), "codec": codec, "ber": ber, "seed": seed,
+             "shape": list(cfg.shape), "values": b * l * h * d,
+             **{k: int(v) for k, v in zip(STAT_NAMES, vals[i])}}
+        rows.append(r)
+    if rank == 0 and cfg.output and rows:
+        with open(cfg.output, "a") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+    all_rows = [done[k] for k in sorted(done)] + rows
+    return all_rows, elapsed
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Sharded Monte-Carlo ECC sweep (torchrun-able)")
+    ap.add_argument("--shape", type=int, nargs=4, default=[8, 4096, 32, 128])
+    ap.add_argument("--codecs", nargs="*", default=list(CODECS))
+    ap.add_argument("--bers", type=float, nargs="*", default=[1e-4, 1e-3, 1e-2])
+    ap.add_argument("--seeds", type=int, nargs="*", default=[42, 101, 997])
+    ap.add_argument("--output", default=None)
+    args = ap.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = MonteCarloConfig(shape=tuple(args.shape), codecs=tuple(args.codecs),
+                           bers=tuple(args.bers), seeds=tuple(args.seeds), output=args.output)
+    shard = HipShard(cfg, rank, world, dev)
+    rows, elapsed = run_sweep(cfg, shard, dist, rank)
+    if rank == 0:
+        for r in rows:
+            print(json.dumps(r))
+        print(json.dumps({"trials": len(rows), "seconds": elapsed, "world": world}))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
