@@ -1,0 +1,112 @@
+"""The ECC shim (patch_model_with_ecc_attention) against the reference's run.
+
+tests/golden/shim_gpt2.npz holds the reference shim's logits and
+get_ecc_stats() for a random-init 2-layer GPT-2 (weights stored in the
+fixture) at seq_len 24, for each codec (tools/gen_golden.py:gen_shim).
+Statistics must match exactly (they depend only on the bits of the cache);
+logits are float outputs of HF matmuls + SDPA and are compared with a
+tolerance (GPU vs CPU summation order).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+LOGIT_ATOL = 2e-3
+LOGIT_RTOL = 2e-3
+
+
+def test_config_validation():
+    from kvecc.ecc_shim import ECCShimConfig
+    with pytest.raises(ValueError):
+        ECCShimConfig(codec="reed-solomon")
+    c = ECCShimConfig(codec="golay", ber=1e-3, backend="hip")
+    assert c.backend == "hip" and c.block_size == 16 and c.seed == 42
+
+
+def test_block_manager_layout_cpu():
+    from kvecc.ecc_shim import SimpleBlockManager
+    m = SimpleBlockManager(8, 16, 3, 4, 128, device="cpu", codec="golay")
+    assert m.k_cache.shape == (8, 3, 4, 16 * 43) and m.k_cache.dtype == torch.int32
+    m2 = SimpleBlockManager(8, 16, 3, 4, 64, device="cpu", codec="hamming84")
+    assert m2.k_cache.shape == (8, 3, 4, 16 * 64) and m2.k_scales.shape == (8, 3, 4, 16)
+    m2.allocate(0, 40)
+    assert m2.block_table[0, :3].tolist() == [0, 1, 2] and m2.get_context_len(0) == 40
+    blk, slot = m2.slots(0, 40)
+    assert blk.tolist() == [0] * 16 + [1] * 16 + [2] * 8 and slot[17].item() == 1
+    with pytest.raises(RuntimeError):
+        m2.allocate(1, 16 * 6)
+    m2.reset()
+    assert len(m2.free_blocks) == 8 and int(m2.block_table.max()) == -1
+
+
+def _model(golden, manifest, device):
+    from transformers import GPT2Config, GPT2LMHeadModel
+    g = golden("shim_gpt2")
+    cfg = GPT2Config(**{k: v for k, v in manifest["shim_gpt2"]["params"]["model"].items()
+                        if k in ("n_layer", "n_head", "n_embd", "n_positions", "vocab_size")})
+    model = GPT2LMHeadModel(cfg).eval()
+    state = {k[2:].replace("__", "."): torch.from_numpy(v) for k, v in g.items()
+             if k.startswith("w_")}
+    model.load_state_dict(state, strict=True)
+    return model.to(device), torch.from_numpy(g["input_ids"]).to(device), g
+
+
+@pytest.mark.gpu
+def test_shim_gpt2_matches_reference(gpu, golden, manifest):
+    from kvecc.ecc_shim import (ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention,
+                                reset_ecc_cache)
+    model, ids, g = _model(golden, manifest, gpu)
+    for i, run in enumerate(manifest["shim_gpt2"]["params"]["runs"]):
+        cfg = ECCShimConfig(codec=run["codec"], ber=run["ber"], inject_errors=run["ber"] > 0,
+                            seed=42, block_size=16, use_interpolation=run["use_interpolation"])
+        with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=16):
+            reset_ecc_cache(model)
+            out = model(ids)
+            st = get_ecc_stats(model)
+        assert st == run["stats"], (run["codec"], st, run["stats"])
+        ref = g[f"r{i}_logits"]
+        got = out.logits.float().cpu().numpy()
+        assert np.allclose(got, ref, atol=LOGIT_ATOL, rtol=LOGIT_RTOL), \
+            (run["codec"], float(np.abs(got - ref).max()))
+
+
+@pytest.mark.gpu
+def test_shim_cache_bits_match_oracle(gpu):
+    """Cache codewords after one write equal the reference loop restated with
+    the oracle: quantize rows, encode, per-row seeds (K: s+r, V: s+r+1)."""
+    from oracle import oracle
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    torch.manual_seed(0)
+    b, s, hk, d = 2, 20, 3, 64
+    for codec, nb in (("hamming84", 8), ("golay", 24), ("hamming74", 7), ("int4", 4)):
+        cfg = ECCShimConfig(codec=codec, ber=0.05, inject_errors=True, seed=7)
+        mgr = SimpleBlockManager(4, 16, 2, hk, d, device=gpu, codec=codec)
+        be = ECCBackend(mgr, cfg, num_heads=hk)
+        k = torch.randn(b, s, hk * d, device=gpu, dtype=torch.float16)
+        v = torch.randn(b, s, hk * d, device=gpu, dtype=torch.float16)
+        be._injection_count = 5
+        be.write(k, v, layer_idx=1)
+        assert be._injection_count == 5 + b * s * hk
+        for which, x, cache in ((0, k, mgr.k_cache), (1, v, mgr.v_cache)):
+            q, _ = oracle.quantize_rows(x.float().cpu().numpy().reshape(b, s, hk, d))
+            last = q[-1]  # last batch wins
+            for pos in range(s):
+                for h in range(hk):
+                    r = ((b - 1) * s + pos) * hk + h
+                    row = last[pos, h]
+                    if codec == "golay":
+                        pad = np.zeros(66, np.uint8)
+                        pad[:d] = row
+                        enc = oracle.golay_encode(pad.reshape(-1, 3))
+                    elif codec == "hamming84":
+                        enc = oracle.hamming84_encode(row)
+                    elif codec == "hamming74":
+                        enc = oracle.hamming74_encode(row)
+                    else:
+                        enc = row
+                    exp, _, _ = oracle.inject(enc, 0.05, nb, 7 + 5 + r + which)
+                    blk, slot = pos // 16, pos % 16
+                    per = exp.size
+                    got = cache[blk, 1, h, slot * per:(slot + 1) * per].cpu().numpy()
+                    assert np.array_equal(got, exp), (codec, which, pos, h)
