@@ -48,36 +48,50 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="time budget of the CPU baseline sample (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-inject", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
 
-def cpu_baseline(budget_s):
-    """The C oracle (a single-threaded port of the reference path) timed on the
-    host: Golay encode + decode of a bounded sample of the same workload."""
+def cpu_baseline(budget_s, threads):
+    """The C oracle (a port of the reference path) timed on the host: Golay
+    encode + decode of a bounded sample of the same workload, one chunk per
+    host thread (ctypes releases the GIL, so the threads run in parallel)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     import numpy as np
     from oracle import oracle
     oracle.lib()
     g = np.random.default_rng(0)
-    m = 1 << 18
-    trip = g.integers(0, 16, size=(m, 3), dtype=np.int64).astype(np.uint8)
-    cw = oracle.golay_encode(trip)
-    noisy, _, _ = oracle.inject(cw[: 1 << 12], BER, 24, SEED)  # keep it cheap; decode sees errors
-    cw[: 1 << 12] = noisy
-    done = 0
-    t0 = time.perf_counter()
-    while True:
+    m = 1 << 16  # codewords per chunk
+    chunks = []
+    for t in range(threads):
+        trip = g.integers(0, 16, size=(m, 3), dtype=np.int64).astype(np.uint8)
+        cw = oracle.golay_encode(trip)
+        noisy, _, _ = oracle.inject(cw[: 1 << 11], BER, 24, SEED)  # decode sees errors
+        cw[: 1 << 11] = noisy
+        chunks.append((trip, cw))
+
+    def work(i):
+        trip, cw = chunks[i]
         oracle.golay_encode(trip)
         oracle.golay_decode(cw)
-        done += m
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": done / el, "unit": "codewords/s", "cores": 1, "kind": "port",
-            "sample": f"{done} codewords ({done // m} x {m}) Golay encode+decode, "
-                      f"{el:.1f} s, oracle/kvecc_oracle.c single thread"}
+        return m
+
+    done = 0
+    with ThreadPoolExecutor(threads) as pool:
+        t0 = time.perf_counter()
+        while True:
+            done += sum(pool.map(work, range(threads)))
+            el = time.perf_counter() - t0
+            if el >= budget_s:
+                break
+    return {"value": done / el, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "sample": f"{done} codewords of Golay encode+decode (BER 1e-2 on a slice) in {el:.1f} s, "
+                      f"oracle/kvecc_oracle.c on {threads} host threads"}
 
 
 def main():
@@ -197,7 +211,7 @@ def main():
             traffic = json.load(f).get("golay_decode_bytes_per_launch")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
     line = {
         "metric": "INT4 codewords/sec encode+decode (Golay24, L=4096) + achieved HBM GB/s",
         "value": value,
