@@ -157,6 +157,37 @@ KVECC_API int kvecc_decode_dequant_h84_rows(const uint8_t *cw, const float *scal
                                             int out_dtype, int64_t rows, int64_t d,
                                             int zero_doubles, uint64_t *stats, void *stream);
 
+/* ---- Host ("cpu") backend ------------------------------------------------- */
+/* The reference has no CPU codec backend (every wrapper asserts x.is_cuda,
+ * e.g. hamming74_triton.py:185,246, golay_triton.py:399,456); BASELINE config 1 asks
+ * for backend="cpu".  These are the host twins of the entry points above:
+ * same arguments minus the stream, HOST pointers, the same codec algebra
+ * (csrc/codec_math.h) run by `threads` std::threads (<= 0: all cores).
+ * `stats` is a plain host uint64 array (stats[0], stats[1] += ...), not the
+ * sharded device buffer. */
+KVECC_API int kvecc_cpu_hamming74_encode(const uint8_t *in, uint8_t *out, int64_t n, int threads);
+KVECC_API int kvecc_cpu_hamming84_encode(const uint8_t *in, uint8_t *out, int64_t n, int threads);
+KVECC_API int kvecc_cpu_hamming74_decode(const uint8_t *cw, uint8_t *data, uint8_t *flag, int64_t n,
+                                         uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_hamming84_decode(const uint8_t *cw, uint8_t *data, uint8_t *etype, int64_t n,
+                                         uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_golay_encode(const uint8_t *trip, int32_t *cw, int64_t m, int threads);
+KVECC_API int kvecc_cpu_golay_decode(const int32_t *cw, uint8_t *trip, uint8_t *counts, int64_t m,
+                                     uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
+                                  int n_bits, int64_t seed, float ber, int64_t global_n,
+                                  int64_t offset0, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_inject_i32(const int32_t *in, int32_t *out, uint8_t *counts, int64_t n,
+                                   int n_bits, int64_t seed, float ber, int64_t global_n,
+                                   int64_t offset0, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
+                                    int64_t outer, int64_t len, int64_t inner, int threads);
+KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
+                                             float *scales, int64_t rows, int64_t d, int threads);
+KVECC_API int kvecc_cpu_decode_dequant_h84_rows(const uint8_t *cw, const float *scales, void *out,
+                                                int out_dtype, int64_t rows, int64_t d,
+                                                int zero_doubles, uint64_t *stats, int threads);
+
 #ifdef __cplusplus
 }
 #endif

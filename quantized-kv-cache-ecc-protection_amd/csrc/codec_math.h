@@ -1,0 +1,214 @@
+// codec_math.h -- the codec algebra, shared by the gfx950 kernels and the
+// host ("cpu" backend) implementation: one definition of every bit operation.
+//
+// References (ecc_codecs/triton_kernels/): hamming74_triton.py:48-162,
+// hamming84_triton.py:50-209, golay_triton.py:99-295,
+// fault_injection_triton.py:57-334 with triton/language/random.py:12-143,
+// interpolation_triton.py:120-159, fused_kernels.py:18-357.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define KV_HD __host__ __device__ __forceinline__
+#else
+#define KV_HD inline
+#endif
+
+namespace kvecc {
+
+// ---- bytes in a 32-bit word ----------------------------------------------------
+
+// per-byte parity of four packed bytes: bit 0 of each byte = XOR of its 8 bits
+KV_HD uint32_t byte_parity4(uint32_t y) {
+  y ^= y >> 4;
+  y ^= y >> 2;
+  y ^= y >> 1;
+  return y & 0x01010101u;
+}
+
+// ---- Hamming(7,4) / Hamming(8,4), four codewords per word (SWAR) -------------
+
+KV_HD uint32_t h74_encode4(uint32_t w) {
+  uint32_t x = w & 0x0F0F0F0Fu;
+  uint32_t d0 = x & 0x01010101u, d1 = (x >> 1) & 0x01010101u;
+  uint32_t d2 = (x >> 2) & 0x01010101u, d3 = (x >> 3) & 0x01010101u;
+  return x | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6;
+}
+
+KV_HD uint32_t h84_encode4(uint32_t w) {
+  uint32_t x = w & 0x0F0F0F0Fu;
+  uint32_t d0 = x & 0x01010101u, d1 = (x >> 1) & 0x01010101u;
+  uint32_t d2 = (x >> 2) & 0x01010101u, d3 = (x >> 3) & 0x01010101u;
+  // parity of the 7-bit word reduces to d0^d1^d2 (p0^p1^p2 = d3)
+  return x | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6 |
+         (d0 ^ d1 ^ d2) << 7;
+}
+
+// Syndrome bits (bit 0 of each byte) of four packed codewords, rows of H
+// (config.py:296-304): s0 over bits {0,1,3,4}, s1 {0,2,3,5}, s2 {1,2,3,6}.
+struct HammingSyndrome {
+  uint32_t nz, fix;
+  KV_HD explicit HammingSyndrome(uint32_t w) {
+    uint32_t s0 = byte_parity4(w & 0x1B1B1B1Bu);
+    uint32_t s1 = byte_parity4(w & 0x2D2D2D2Du);
+    uint32_t s2 = byte_parity4(w & 0x4E4E4E4Eu);
+    nz = s0 | s1 | s2;
+    // data bit k is in error iff the syndrome equals column k of H:
+    // d0 -> 3, d1 -> 5, d2 -> 6, d3 -> 7 (parity-bit positions 1,2,4 leave data alone)
+    fix = (s0 & s1 & ~s2) | (s0 & ~s1 & s2) << 1 | (~s0 & s1 & s2) << 2 | (s0 & s1 & s2) << 3;
+  }
+};
+
+// SECDED decode of four packed codewords: data nibbles, ErrorType bytes
+KV_HD void h84_decode4(uint32_t w, uint32_t &data, uint32_t &type, uint32_t &n_single,
+                       uint32_t &n_double) {
+  HammingSyndrome s(w);
+  uint32_t pe = byte_parity4(w);  // stored overall parity != parity(bits 0..6)
+  data = (w ^ (s.fix & (pe * 0x0Fu))) & 0x0F0F0F0Fu;  // correct only SINGLE (pe && nz)
+  // (nz,pe) = (0,0)->0, (1,1)->1, (1,0)->2, (0,1)->3 (hamming84_triton.py:185-187)
+  type = pe | (pe ^ s.nz) << 1;
+  n_single += __builtin_popcount(pe & s.nz);
+  n_double += __builtin_popcount(~pe & s.nz);
+}
+
+KV_HD void h74_decode4(uint32_t w, uint32_t &data, uint32_t &flag, uint32_t &n_flag) {
+  HammingSyndrome s(w);
+  data = (w ^ s.fix) & 0x0F0F0F0Fu;  // doubles are miscorrected, as in the reference
+  flag = s.nz;
+  n_flag += __builtin_popcount(s.nz);
+}
+
+// single nibble -> codeword (codec: 0 raw, 1 H74, 2 H84 -- KVECC_CODEC_*)
+KV_HD uint32_t encode_nibble(uint32_t v, int codec) {
+  if (codec == 2) return h84_encode4(v) & 0xFFu;
+  if (codec == 1) return h74_encode4(v) & 0xFFu;
+  return v;
+}
+
+// ---- Golay(24,12) ---------------------------------------------------------------
+
+KV_HD uint32_t golay_pack(uint32_t b0, uint32_t b1, uint32_t b2) {
+  return (b0 & 0xFu) | (b1 & 0xFu) << 4 | (b2 & 0xFu) << 8;
+}
+
+// 12-bit data word -> its three nibbles in three consecutive bytes
+KV_HD uint32_t golay_spread(uint32_t d) {
+  return (d & 0xFu) | (d & 0xF0u) << 4 | (d & 0xF00u) << 8;
+}
+
+// 4 consecutive triplets (12 bytes, little endian in 3 words) -> 4 data words
+KV_HD void golay_unpack4(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t d[4]) {
+  d[0] = golay_pack(w0, w0 >> 8, w0 >> 16);
+  d[1] = golay_pack(w0 >> 24, w1, w1 >> 8);
+  d[2] = golay_pack(w1 >> 16, w1 >> 24, w2);
+  d[3] = golay_pack(w2 >> 8, w2 >> 16, w2 >> 24);
+}
+
+// decode one codeword with the parity / correction tables (runtime.hip):
+// returns the 12-bit data, `c` = corrected bits 0..3 or 4 (uncorrectable)
+KV_HD uint32_t golay_decode1(uint32_t w, const uint16_t *par, const uint16_t *cor, uint32_t &c) {
+  uint32_t lo = w & 0xFFFu;
+  uint32_t e = cor[((w >> 12) & 0xFFFu) ^ par[lo]];
+  c = e >> 12;
+  return lo ^ (e & 0xFFFu);
+}
+
+// ---- Philox4x32-10 and the injection draw ------------------------------------
+
+constexpr uint32_t kPhiloxA = 0xD2511F53u, kPhiloxB = 0xCD9E8D57u;
+constexpr uint32_t kKeyA = 0x9E3779B9u, kKeyB = 0xBB67AE85u;
+
+KV_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(a, b);  // v_mul_hi_u32 (the 64-bit mad form measured 1.6x slower)
+#else
+  return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+KV_HD void philox_rounds(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, uint32_t k0,
+                         uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hb = mulhi32(kPhiloxB, c2), lb = kPhiloxB * c2;
+    uint32_t ha = mulhi32(kPhiloxA, c0), la = kPhiloxA * c0;
+    c0 = hb ^ c1 ^ k0;
+    c2 = ha ^ c3 ^ k1;
+    c1 = lb;
+    c3 = la;
+    k0 += kKeyA;
+    k1 += kKeyB;
+  }
+}
+
+// tl.rand(key, ctr): first Philox output word for counter (ctr,0,0,0), key
+// sign-extended to 64 bits (random.py:46-110)
+KV_HD uint32_t philox_word0(uint32_t ctr, uint32_t key) {
+  uint32_t c0 = ctr, c1 = 0, c2 = 0, c3 = 0;
+  philox_rounds(c0, c1, c2, c3, key, (uint32_t)((int32_t)key >> 31));
+  return c0;
+}
+
+// `uint_to_uniform_float(x) < ber` as an integer test against kvecc_ber_threshold
+KV_HD bool philox_below(uint32_t x, uint32_t thr) {
+  uint32_t f = x ^ (uint32_t)((int32_t)x >> 31);  // fold: x < 0 ? -x-1 : x
+  return f < thr;
+}
+
+// flip mask of one element for the per-bit scheme; key_base = key of bit 0
+template <int NB>
+KV_HD uint32_t philox_flip_mask(uint32_t key_base, uint32_t ctr, uint32_t thr, int nb_rt) {
+  uint32_t m = 0;
+  if (NB >= 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) m |= (uint32_t)philox_below(philox_word0(ctr, key_base + b), thr) << b;
+  } else {
+    for (int b = 0; b < nb_rt; ++b)
+      m |= (uint32_t)philox_below(philox_word0(ctr, key_base + b), thr) << b;
+  }
+  return m;
+}
+
+// rand4x variant: batch k of 4 bits uses key seed*N + off + k*N, words c0..c3
+KV_HD uint32_t philox_flip_mask_vec(uint32_t seedn, uint32_t nn, uint32_t off, uint32_t thr,
+                                    int nb) {
+  uint32_t m = 0;
+  for (int k = 0; 4 * k < nb; ++k) {
+    const uint32_t key = seedn + off + (uint32_t)k * nn;
+    uint32_t c0 = off, c1 = 0, c2 = 0, c3 = 0;
+    philox_rounds(c0, c1, c2, c3, key, (uint32_t)((int32_t)key >> 31));
+    const uint32_t w[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * k + j < nb) m |= (uint32_t)philox_below(w[j], thr) << (4 * k + j);
+  }
+  return m;
+}
+
+// ---- interpolation, four bytes per word --------------------------------------------
+
+// per byte: min(15, x)
+KV_HD uint32_t sat15(uint32_t x) {
+  uint32_t hi = (x >> 4) & 0x0F0F0F0Fu;                     // high nibble per byte
+  uint32_t over = ((hi + 0x0F0F0F0Fu) >> 4) & 0x01010101u;  // 1 where x > 15
+  return (x & ~(over * 0xFFu)) | (over * 0x0Fu);
+}
+
+// per byte: (a + b + 1) >> 1 without overflow
+KV_HD uint32_t avg_up(uint32_t a, uint32_t b) { return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu); }
+
+// per byte: 0xFF where err == 2, else 0
+KV_HD uint32_t is_double(uint32_t e) {
+  uint32_t v = e ^ 0x02020202u;
+  uint32_t nonzero = (((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+  return ((~nonzero & 0x80808080u) >> 7) * 0xFFu;
+}
+
+// err == 2 ? min(15, (L+R+1)>>1) : min(15, q)  -- the kernel's fp32 formula, exact
+KV_HD uint32_t interp_word(uint32_t q, uint32_t l, uint32_t r, uint32_t e) {
+  uint32_t m = is_double(e);
+  return sat15((avg_up(l, r) & m) | (q & ~m));
+}
+
+}  // namespace kvecc

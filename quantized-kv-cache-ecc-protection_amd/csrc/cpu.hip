@@ -1,0 +1,336 @@
+// cpu.hip -- the host ("cpu") codec backend: same algebra as the gfx950
+// kernels (codec_math.h), run over host memory with std::thread workers.
+//
+// This is the explicit `backend="cpu"` of kvecc.backends (BASELINE config 1:
+// Hamming(7,4) on the host, no GPU) -- never a fallback of the "hip" backend.
+// Statistics are plain host uint64 arrays (+=), not the sharded device buffer.
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "kvecc_internal.h"
+
+namespace kvecc {
+namespace {
+
+int clamp_threads(int threads, int64_t work, int64_t grain) {
+  int hw = (int)std::thread::hardware_concurrency();
+  if (threads <= 0) threads = hw > 0 ? hw : 1;
+  int64_t useful = std::max<int64_t>(1, work / std::max<int64_t>(1, grain));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(threads, useful));
+}
+
+// run fn(begin, end, thread_index) over [0, n) in `threads` contiguous chunks
+// whose boundaries are multiples of `align`
+template <class F>
+void parallel_for(int64_t n, int threads, int64_t align, F fn) {
+  int t = clamp_threads(threads, n, 1 << 16);
+  if (t == 1) {
+    fn((int64_t)0, n, 0);
+    return;
+  }
+  int64_t chunk = (n + t - 1) / t;
+  chunk = (chunk + align - 1) / align * align;
+  std::vector<std::thread> pool;
+  for (int i = 0; i < t; ++i) {
+    int64_t b = i * chunk, e = std::min<int64_t>(n, b + chunk);
+    if (b >= e) break;
+    pool.emplace_back(fn, b, e, i);
+  }
+  for (auto &th : pool) th.join();
+}
+
+inline uint32_t load4(const uint8_t *p) {
+  uint32_t w;
+  std::memcpy(&w, p, 4);
+  return w;
+}
+inline void store4(uint8_t *p, uint32_t w) { std::memcpy(p, &w, 4); }
+
+template <class Op>
+void map_bytes(const uint8_t *in, uint8_t *out, int64_t n, int threads, Op op) {
+  parallel_for(n, threads, 64, [&](int64_t b, int64_t e, int) {
+    int64_t i = b;
+    for (; i + 4 <= e; i += 4) store4(out + i, op(load4(in + i)));
+    for (; i < e; ++i) out[i] = (uint8_t)op(in[i]);
+  });
+}
+
+struct Acc2 {
+  uint64_t a = 0, b = 0;
+  char pad[48];
+};
+
+void add_stats(uint64_t *stats, const std::vector<Acc2> &acc, int n) {
+  if (!stats) return;
+  for (auto &x : acc) {
+    stats[0] += x.a;
+    if (n > 1) stats[1] += x.b;
+  }
+}
+
+template <typename T>
+float to_f32(const void *p, int64_t i) {
+  return (float)reinterpret_cast<const T *>(p)[i];
+}
+
+float load_x(const void *x, int dtype, int64_t i) {
+  if (dtype == KVECC_F16) return __half2float(reinterpret_cast<const __half *>(x)[i]);
+  if (dtype == KVECC_BF16) return __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(x)[i]);
+  return reinterpret_cast<const float *>(x)[i];
+}
+
+void store_y(void *y, int dtype, int64_t i, float v) {
+  if (dtype == KVECC_F16)
+    reinterpret_cast<__half *>(y)[i] = __float2half_rn(v);
+  else if (dtype == KVECC_BF16)
+    reinterpret_cast<__hip_bfloat16 *>(y)[i] = __float2bfloat16(v);
+  else
+    reinterpret_cast<float *>(y)[i] = v;
+}
+
+bool bad(int64_t n) { return n < 0; }
+
+}  // namespace
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int kvecc_cpu_hamming74_encode(const uint8_t *in, uint8_t *out, int64_t n, int threads) {
+  if (bad(n)) return set_error(KVECC_EINVAL, "cpu_hamming74_encode: negative n");
+  if (n && (!in || !out)) return set_error(KVECC_EINVAL, "cpu_hamming74_encode: null pointer");
+  map_bytes(in, out, n, threads, [](uint32_t w) { return h74_encode4(w); });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_hamming84_encode(const uint8_t *in, uint8_t *out, int64_t n, int threads) {
+  if (bad(n)) return set_error(KVECC_EINVAL, "cpu_hamming84_encode: negative n");
+  if (n && (!in || !out)) return set_error(KVECC_EINVAL, "cpu_hamming84_encode: null pointer");
+  map_bytes(in, out, n, threads, [](uint32_t w) { return h84_encode4(w); });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_hamming74_decode(const uint8_t *cw, uint8_t *data, uint8_t *flag, int64_t n,
+                                         uint64_t *stats, int threads) {
+  if (bad(n)) return set_error(KVECC_EINVAL, "cpu_hamming74_decode: negative n");
+  if (n && (!cw || !data)) return set_error(KVECC_EINVAL, "cpu_hamming74_decode: null pointer");
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, n, 1 << 16)));
+  parallel_for(n, threads, 64, [&](int64_t b, int64_t e, int t) {
+    uint32_t c = 0;
+    int64_t i = b;
+    for (; i + 4 <= e; i += 4) {
+      uint32_t d, f;
+      h74_decode4(load4(cw + i), d, f, c);
+      store4(data + i, d);
+      if (flag) store4(flag + i, f);
+    }
+    for (; i < e; ++i) {
+      uint32_t d, f;
+      h74_decode4(cw[i], d, f, c);
+      data[i] = (uint8_t)d;
+      if (flag) flag[i] = (uint8_t)f;
+    }
+    acc[t].a += c;
+  });
+  add_stats(stats, acc, 1);
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_hamming84_decode(const uint8_t *cw, uint8_t *data, uint8_t *etype, int64_t n,
+                                         uint64_t *stats, int threads) {
+  if (bad(n)) return set_error(KVECC_EINVAL, "cpu_hamming84_decode: negative n");
+  if (n && (!cw || !data)) return set_error(KVECC_EINVAL, "cpu_hamming84_decode: null pointer");
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, n, 1 << 16)));
+  parallel_for(n, threads, 64, [&](int64_t b, int64_t e, int t) {
+    uint32_t c1 = 0, c2 = 0;
+    int64_t i = b;
+    for (; i + 4 <= e; i += 4) {
+      uint32_t d, ty;
+      h84_decode4(load4(cw + i), d, ty, c1, c2);
+      store4(data + i, d);
+      if (etype) store4(etype + i, ty);
+    }
+    for (; i < e; ++i) {
+      uint32_t d, ty;
+      h84_decode4(cw[i], d, ty, c1, c2);
+      data[i] = (uint8_t)d;
+      if (etype) etype[i] = (uint8_t)ty;
+    }
+    acc[t].a += c1;
+    acc[t].b += c2;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_golay_encode(const uint8_t *trip, int32_t *cw, int64_t m, int threads) {
+  if (bad(m)) return set_error(KVECC_EINVAL, "cpu_golay_encode: negative m");
+  if (m && (!trip || !cw)) return set_error(KVECC_EINVAL, "cpu_golay_encode: null pointer");
+  static uint16_t par[4096];
+  static bool ready = [] { build_golay_parity_table(par); return true; }();
+  (void)ready;
+  parallel_for(m, threads, 64, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      uint32_t d = golay_pack(trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]);
+      cw[i] = (int32_t)(d | (uint32_t)par[d] << 12);
+    }
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_golay_decode(const int32_t *cw, uint8_t *trip, uint8_t *counts, int64_t m,
+                                     uint64_t *stats, int threads) {
+  if (bad(m)) return set_error(KVECC_EINVAL, "cpu_golay_decode: negative m");
+  if (m && (!trip || !cw)) return set_error(KVECC_EINVAL, "cpu_golay_decode: null pointer");
+  static uint16_t tab[8192];
+  static bool ready = [] {
+    build_golay_parity_table(tab);
+    build_golay_correct_table(tab + 4096);
+    return true;
+  }();
+  (void)ready;
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, m, 1 << 16)));
+  parallel_for(m, threads, 64, [&](int64_t b, int64_t e, int t) {
+    uint64_t bits = 0, unc = 0;
+    for (int64_t i = b; i < e; ++i) {
+      uint32_t c;
+      uint32_t d = golay_decode1((uint32_t)cw[i], tab, tab + 4096, c);
+      trip[3 * i] = (uint8_t)(d & 0xF);
+      trip[3 * i + 1] = (uint8_t)(d >> 4 & 0xF);
+      trip[3 * i + 2] = (uint8_t)(d >> 8);
+      if (counts) counts[i] = (uint8_t)c;
+      bits += c & 3u;
+      unc += c >> 2;
+    }
+    acc[t].a += bits;
+    acc[t].b += unc;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
+}  // extern "C"
+
+template <typename T>
+static int cpu_inject(const T *in, T *out, uint8_t *counts, int64_t n, int n_bits, int64_t seed,
+                      float ber, int64_t global_n, int64_t offset0, uint64_t *stats, int threads,
+                      const char *name) {
+  if (n < 0 || global_n < 0 || offset0 < 0) return set_error(KVECC_EINVAL, "%s: negative size", name);
+  if (n && (!in || !out)) return set_error(KVECC_EINVAL, "%s: null pointer", name);
+  if (offset0 + n > global_n) return set_error(KVECC_EINVAL, "%s: shard exceeds global_n", name);
+  const uint32_t seedmul = (uint32_t)((uint64_t)seed * (uint64_t)(uint32_t)((uint64_t)global_n * (uint64_t)n_bits));
+  const uint32_t thr = kvecc_ber_threshold(ber);
+  const int nb = sizeof(T) == 1 ? (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits))
+                                : (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits));
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, n, 1 << 12)));
+  parallel_for(n, threads, 64, [&](int64_t b, int64_t e, int t) {
+    uint64_t flips = 0, hit = 0;
+    for (int64_t i = b; i < e; ++i) {
+      const uint32_t g = (uint32_t)(offset0 + i);
+      const uint32_t m = philox_flip_mask<-1>(seedmul + g * (uint32_t)n_bits, g, thr, nb);
+      out[i] = (T)((uint32_t)in[i] ^ m);
+      uint32_t c = __builtin_popcount(m);
+      if (counts) counts[i] = (uint8_t)c;
+      flips += c;
+      hit += c != 0;
+    }
+    acc[t].a += flips;
+    acc[t].b += hit;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
+extern "C" {
+
+KVECC_API int kvecc_cpu_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
+                                  int n_bits, int64_t seed, float ber, int64_t global_n,
+                                  int64_t offset0, uint64_t *stats, int threads) {
+  return cpu_inject<uint8_t>(in, out, counts, n, n_bits, seed, ber, global_n, offset0, stats,
+                             threads, "cpu_inject_u8");
+}
+
+KVECC_API int kvecc_cpu_inject_i32(const int32_t *in, int32_t *out, uint8_t *counts, int64_t n,
+                                   int n_bits, int64_t seed, float ber, int64_t global_n,
+                                   int64_t offset0, uint64_t *stats, int threads) {
+  return cpu_inject<int32_t>(in, out, counts, n, n_bits, seed, ber, global_n, offset0, stats,
+                             threads, "cpu_inject_i32");
+}
+
+KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
+                                    int64_t outer, int64_t len, int64_t inner, int threads) {
+  if (outer < 0 || len < 0 || inner < 0) return set_error(KVECC_EINVAL, "cpu_interpolate: negative size");
+  const int64_t total = outer * len * inner;
+  if (total && (!q || !err || !out)) return set_error(KVECC_EINVAL, "cpu_interpolate: null pointer");
+  parallel_for(total, threads, 64, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      const int64_t l = (i / inner) % len;
+      const int64_t row = i - l * inner;
+      const uint32_t left = q[row + (l > 0 ? l - 1 : 0) * inner];
+      const uint32_t right = q[row + (l + 1 < len ? l + 1 : len - 1) * inner];
+      out[i] = (uint8_t)interp_word(q[i], left, right, err[i]);
+    }
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
+                                             float *scales, int64_t rows, int64_t d, int threads) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: negative size");
+  if (rows == 0) return KVECC_OK;
+  if (d == 0) return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: empty rows");
+  if (!x || !cw || !scales) return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: null pointer");
+  if (x_dtype < KVECC_F32 || x_dtype > KVECC_BF16)
+    return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: bad dtype %d", x_dtype);
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_H84)
+    return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: bad codec %d", codec);
+  parallel_for(rows, threads, 1, [&](int64_t b, int64_t e, int) {
+    for (int64_t r = b; r < e; ++r) {
+      float amax = 0.0f;
+      for (int64_t j = 0; j < d; ++j) amax = std::max(amax, std::fabs(load_x(x, x_dtype, r * d + j)));
+      float scale = amax / 7.0f;
+      if (scale == 0.0f) scale = 1.0f;
+      scales[r] = scale;
+      for (int64_t j = 0; j < d; ++j) {
+        float q = std::rint(load_x(x, x_dtype, r * d + j) / scale);
+        q = std::min(std::max(q, -8.0f), 7.0f);
+        cw[r * d + j] = (uint8_t)encode_nibble((uint32_t)(int)(q + 8.0f), codec);
+      }
+    }
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_decode_dequant_h84_rows(const uint8_t *cw, const float *scales, void *out,
+                                                int out_dtype, int64_t rows, int64_t d,
+                                                int zero_doubles, uint64_t *stats, int threads) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_decode_dequant_h84_rows: negative size");
+  if (rows == 0 || d == 0) return KVECC_OK;
+  if (!cw || !scales || !out) return set_error(KVECC_EINVAL, "cpu_decode_dequant_h84_rows: null pointer");
+  if (out_dtype < KVECC_F32 || out_dtype > KVECC_BF16)
+    return set_error(KVECC_EINVAL, "cpu_decode_dequant_h84_rows: bad dtype %d", out_dtype);
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, rows, 1)));
+  parallel_for(rows, threads, 1, [&](int64_t b, int64_t e, int t) {
+    uint32_t n1 = 0, n2 = 0;
+    for (int64_t r = b; r < e; ++r)
+      for (int64_t j = 0; j < d; ++j) {
+        uint32_t data, type;
+        h84_decode4(cw[r * d + j], data, type, n1, n2);
+        if (zero_doubles && type == 2) data = 0;
+        store_y(out, out_dtype, r * d + j, ((float)data - 8.0f) * scales[r]);
+      }
+    acc[t].a += n1;
+    acc[t].b += n2;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
+}  // extern "C"

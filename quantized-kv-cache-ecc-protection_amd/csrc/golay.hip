@@ -48,25 +48,8 @@ __device__ __forceinline__ void load_tables(uint16_t *lds, const uint16_t *__res
   __syncthreads();
 }
 
-__device__ __forceinline__ uint32_t pack_data(uint32_t b0, uint32_t b1, uint32_t b2) {
-  return (b0 & 0xFu) | (b1 & 0xFu) << 4 | (b2 & 0xFu) << 8;
-}
-
-// 12-bit data word -> its three nibbles in three consecutive bytes
-__device__ __forceinline__ uint32_t spread_nibbles(uint32_t d) {
-  return (d & 0xFu) | (d & 0xF0u) << 4 | (d & 0xF00u) << 8;
-}
-
+// triplet packing / unpacking and the table decode: codec_math.h
 // ---- encode -------------------------------------------------------------------
-
-// 4 consecutive triplets (12 bytes, little endian in 3 words) -> 4 data words
-__device__ __forceinline__ void unpack_triplets(uint32_t w0, uint32_t w1, uint32_t w2,
-                                                uint32_t d[4]) {
-  d[0] = pack_data(w0, w0 >> 8, w0 >> 16);
-  d[1] = pack_data(w0 >> 24, w1, w1 >> 8);
-  d[2] = pack_data(w1 >> 16, w1 >> 24, w2);
-  d[3] = pack_data(w2 >> 8, w2 >> 16, w2 >> 24);
-}
 
 __global__ __launch_bounds__(kEncBlock) void golay_encode_kernel(const uint32_t *__restrict__ trip,
                                                                  u32x4 *__restrict__ cw,
@@ -90,7 +73,7 @@ __global__ __launch_bounds__(kEncBlock) void golay_encode_kernel(const uint32_t 
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
       uint32_t d[4];
-      unpack_triplets(w[g][0], w[g][1], w[g][2], d);
+      golay_unpack4(w[g][0], w[g][1], w[g][2], d);
       u32x4 out;
       out.x = d[0] | (uint32_t)lds[d[0]] << 12;
       out.y = d[1] | (uint32_t)lds[d[1]] << 12;
@@ -108,24 +91,17 @@ __global__ __launch_bounds__(kBlock) void golay_encode_tail_kernel(const uint8_t
                                                                    const uint16_t *__restrict__ par) {
   for (int64_t i = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m;
        i += (int64_t)gridDim.x * kBlock) {
-    uint32_t d = pack_data(trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]);
+    uint32_t d = golay_pack(trip[3 * i], trip[3 * i + 1], trip[3 * i + 2]);
     cw[i] = (int32_t)(d | (uint32_t)par[d] << 12);
   }
 }
 
 // ---- decode -------------------------------------------------------------------
 
-struct GolayStats {
-  uint32_t bits = 0, unc = 0;
-};
-
-// returns the 12-bit data word, count in `c`
+// LDS holds parity[4096] then correct[4096]; returns the 12-bit data word,
+// `c` = 0..3 corrected bits or 4 = uncorrectable (data kept)
 __device__ __forceinline__ uint32_t decode_one(uint32_t w, const uint16_t *lds, uint32_t &c) {
-  uint32_t lo = w & 0xFFFu;
-  uint32_t syn = ((w >> 12) & 0xFFFu) ^ lds[lo];
-  uint32_t e = lds[4096 + syn];
-  c = e >> 12;  // 0..3 corrected bits, 4 = uncorrectable (data kept)
-  return lo ^ (e & 0xFFFu);
+  return golay_decode1(w, lds, lds + 4096, c);
 }
 
 template <bool WITH_COUNTS, bool WITH_STATS>
@@ -149,10 +125,10 @@ __global__ __launch_bounds__(kDecBlock) void golay_decode_kernel(const u32x4 *__
 #pragma unroll
     for (int g = 0; g < kGroups; ++g) {
       uint32_t c0, c1, c2, c3;
-      uint32_t e0 = spread_nibbles(decode_one(v[g].x, lds, c0));
-      uint32_t e1 = spread_nibbles(decode_one(v[g].y, lds, c1));
-      uint32_t e2 = spread_nibbles(decode_one(v[g].z, lds, c2));
-      uint32_t e3 = spread_nibbles(decode_one(v[g].w, lds, c3));
+      uint32_t e0 = golay_spread(decode_one(v[g].x, lds, c0));
+      uint32_t e1 = golay_spread(decode_one(v[g].y, lds, c1));
+      uint32_t e2 = golay_spread(decode_one(v[g].z, lds, c2));
+      uint32_t e3 = golay_spread(decode_one(v[g].w, lds, c3));
       uint32_t *p = trip + (base + g * 256) * 3 / 4;
       st_stream(p, e0 | e1 << 24);
       st_stream(p + 1, e1 >> 8 | e2 << 16);
@@ -207,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void golay_encode_rows_kernel(
     uint32_t b0 = row[c];
     uint32_t b1 = c + 1 < d ? row[c + 1] : 0u;
     uint32_t b2 = c + 2 < d ? row[c + 2] : 0u;
-    uint32_t dw = pack_data(b0, b1, b2);
+    uint32_t dw = golay_pack(b0, b1, b2);
     cw[i] = (int32_t)(dw | (uint32_t)par[dw] << 12);
   }
 }

@@ -21,39 +21,12 @@ namespace kvecc {
 constexpr int kUnroll = 1;   // 16-B vectors per lane per tile
 constexpr int kPerCu = 64;   // workgroups per CU before grid-striding
 
+// encoders and decoders: codec_math.h (shared with the host backend)
 struct H74Enc {
-  __device__ __forceinline__ static uint32_t op(uint32_t w) {
-    uint32_t x = w & 0x0F0F0F0Fu;
-    uint32_t d0 = x & 0x01010101u, d1 = (x >> 1) & 0x01010101u;
-    uint32_t d2 = (x >> 2) & 0x01010101u, d3 = (x >> 3) & 0x01010101u;
-    return x | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6;
-  }
+  __device__ __forceinline__ static uint32_t op(uint32_t w) { return h74_encode4(w); }
 };
-
 struct H84Enc {
-  __device__ __forceinline__ static uint32_t op(uint32_t w) {
-    uint32_t x = w & 0x0F0F0F0Fu;
-    uint32_t d0 = x & 0x01010101u, d1 = (x >> 1) & 0x01010101u;
-    uint32_t d2 = (x >> 2) & 0x01010101u, d3 = (x >> 3) & 0x01010101u;
-    // parity of the 7-bit word reduces to d0^d1^d2 (p0^p1^p2 = d3)
-    return x | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6 |
-           (d0 ^ d1 ^ d2) << 7;
-  }
-};
-
-// Syndrome bits (bit 0 of each byte) of four packed codewords, rows of H
-// (config.py:296-304): s0 over bits {0,1,3,4}, s1 {0,2,3,5}, s2 {1,2,3,6}.
-struct Syn {
-  uint32_t s0, s1, s2, nz, fix;
-  __device__ __forceinline__ explicit Syn(uint32_t w) {
-    s0 = byte_parity4(w & 0x1B1B1B1Bu);
-    s1 = byte_parity4(w & 0x2D2D2D2Du);
-    s2 = byte_parity4(w & 0x4E4E4E4Eu);
-    nz = s0 | s1 | s2;
-    // data bit k is in error iff the syndrome equals column k of H:
-    // d0 -> 3, d1 -> 5, d2 -> 6, d3 -> 7 (parity-bit positions 1,2,4 leave data alone)
-    fix = (s0 & s1 & ~s2) | (s0 & ~s1 & s2) << 1 | (~s0 & s1 & s2) << 2 | (s0 & s1 & s2) << 3;
-  }
+  __device__ __forceinline__ static uint32_t op(uint32_t w) { return h84_encode4(w); }
 };
 
 template <class Op>
@@ -91,24 +64,13 @@ __global__ __launch_bounds__(kBlock) void encode_bytes_kernel(const uint8_t *__r
     out[i] = (uint8_t)Op::op(in[i]);
 }
 
-// SECDED decode of four packed codewords
 __device__ __forceinline__ void dec84_word(uint32_t w, uint32_t &data, uint32_t &type,
                                            uint32_t &n_single, uint32_t &n_double) {
-  Syn s(w);
-  uint32_t pe = byte_parity4(w);  // stored overall parity != parity(bits 0..6)
-  data = (w ^ (s.fix & (pe * 0x0Fu))) & 0x0F0F0F0Fu;  // correct only SINGLE (pe && nz)
-  // type: (nz,pe) = (0,0)->0, (1,1)->1, (1,0)->2, (0,1)->3 (hamming84_triton.py:185-187)
-  type = pe | (pe ^ s.nz) << 1;
-  n_single += __builtin_popcount(pe & s.nz);
-  n_double += __builtin_popcount(~pe & s.nz);
+  h84_decode4(w, data, type, n_single, n_double);
 }
-
 __device__ __forceinline__ void dec74_word(uint32_t w, uint32_t &data, uint32_t &flag,
                                            uint32_t &n_flag) {
-  Syn s(w);
-  data = (w ^ s.fix) & 0x0F0F0F0Fu;  // doubles are miscorrected, as in the reference
-  flag = s.nz;
-  n_flag += __builtin_popcount(s.nz);
+  h74_decode4(w, data, flag, n_flag);
 }
 
 template <bool H84, bool WITH_AUX, bool WITH_STATS>

@@ -20,49 +20,12 @@
 
 namespace kvecc {
 
-constexpr uint32_t kPhiloxA = 0xD2511F53u, kPhiloxB = 0xCD9E8D57u;
-constexpr uint32_t kKeyA = 0x9E3779B9u, kKeyB = 0xBB67AE85u;
-
-__device__ __forceinline__ void philox_rounds(uint32_t &c0, uint32_t &c1, uint32_t &c2,
-                                              uint32_t &c3, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    uint32_t hb = __umulhi(kPhiloxB, c2), lb = kPhiloxB * c2;
-    uint32_t ha = __umulhi(kPhiloxA, c0), la = kPhiloxA * c0;
-    c0 = hb ^ c1 ^ k0;
-    c2 = ha ^ c3 ^ k1;
-    c1 = lb;
-    c3 = la;
-    k0 += kKeyA;
-    k1 += kKeyB;
-  }
-}
-
-// tl.rand(key, ctr): first Philox output word for counter (ctr,0,0,0)
-__device__ __forceinline__ uint32_t philox_word0(uint32_t ctr, uint32_t key) {
-  uint32_t c0 = ctr, c1 = 0, c2 = 0, c3 = 0;
-  philox_rounds(c0, c1, c2, c3, key, (uint32_t)((int32_t)key >> 31));
-  return c0;
-}
-
-__device__ __forceinline__ bool below(uint32_t x, uint32_t thr) {
-  // fold(int32 x) as a non-negative value; compare with the integer threshold
-  uint32_t f = x ^ (uint32_t)((int32_t)x >> 31);
-  return f < thr;
-}
-
-// flip mask of one element for the per-bit scheme; key_base = key of bit 0
+// Philox rounds, the integer BER test and the per-element flip masks live in
+// codec_math.h (shared with the host backend).
 template <int NB>
 __device__ __forceinline__ uint32_t flip_mask(uint32_t key_base, uint32_t ctr, uint32_t thr,
                                               int nb_rt) {
-  uint32_t m = 0;
-  if (NB >= 0) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b) m |= (uint32_t)below(philox_word0(ctr, key_base + b), thr) << b;
-  } else {
-    for (int b = 0; b < nb_rt; ++b) m |= (uint32_t)below(philox_word0(ctr, key_base + b), thr) << b;
-  }
-  return m;
+  return philox_flip_mask<NB>(key_base, ctr, thr, nb_rt);
 }
 
 struct InjectArgs {
@@ -197,17 +160,7 @@ __global__ __launch_bounds__(kBlock) void inject_vec_kernel(const T *in,
   uint32_t flips = 0, hit = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kBlock) {
-    const uint32_t off = (uint32_t)i;
-    uint32_t m = 0;
-    for (int k = 0; 4 * k < nb; ++k) {
-      const uint32_t key = seedn + off + (uint32_t)k * nn;
-      uint32_t c0 = off, c1 = 0, c2 = 0, c3 = 0;
-      philox_rounds(c0, c1, c2, c3, key, (uint32_t)((int32_t)key >> 31));
-      const uint32_t w[4] = {c0, c1, c2, c3};
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (4 * k + j < nb) m |= (uint32_t)below(w[j], thr) << (4 * k + j);
-    }
+    const uint32_t m = philox_flip_mask_vec(seedn, nn, (uint32_t)i, thr, nb);
     out[i] = (T)((uint32_t)in[i] ^ m);
     uint32_t c = __builtin_popcount(m);
     if (counts) counts[i] = (uint8_t)c;

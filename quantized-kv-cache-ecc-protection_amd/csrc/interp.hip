@@ -21,30 +21,7 @@ namespace kvecc {
 
 constexpr int kRows = 8;
 
-// per byte: min(15, x)
-__device__ __forceinline__ uint32_t sat15(uint32_t x) {
-  uint32_t hi = (x >> 4) & 0x0F0F0F0Fu;                // high nibble per byte
-  uint32_t over = ((hi + 0x0F0F0F0Fu) >> 4) & 0x01010101u;  // 1 where x > 15
-  return (x & ~(over * 0xFFu)) | (over * 0x0Fu);
-}
-
-// per byte: (a + b + 1) >> 1 without overflow
-__device__ __forceinline__ uint32_t avg_up(uint32_t a, uint32_t b) {
-  return (a | b) - (((a ^ b) >> 1) & 0x7F7F7F7Fu);
-}
-
-// per byte: 0xFF where err == 2, else 0
-__device__ __forceinline__ uint32_t is_double(uint32_t e) {
-  uint32_t v = e ^ 0x02020202u;
-  uint32_t nonzero = (((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
-  return ((~nonzero & 0x80808080u) >> 7) * 0xFFu;
-}
-
-__device__ __forceinline__ uint32_t interp_word(uint32_t q, uint32_t l, uint32_t r, uint32_t e) {
-  uint32_t m = is_double(e);
-  return sat15((avg_up(l, r) & m) | (q & ~m));
-}
-
+// sat15 / avg_up / is_double / interp_word (four bytes per word): codec_math.h
 __device__ __forceinline__ u32x4 interp_vec(u32x4 q, u32x4 l, u32x4 r, u32x4 e) {
   u32x4 o;
   o.x = interp_word(q.x, l.x, r.x, e.x);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "codec_math.h"
 #include "kvecc.h"
 
 namespace kvecc {
@@ -82,14 +83,6 @@ __device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32
     if (sa) atomicAdd(reinterpret_cast<unsigned long long *>(slot), sa);
     if (sb) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), sb);
   }
-}
-
-// per-byte parity of four packed bytes: bit 0 of each byte = XOR of its 8 bits
-__device__ __forceinline__ uint32_t byte_parity4(uint32_t y) {
-  y ^= y >> 4;
-  y ^= y >> 2;
-  y ^= y >> 1;
-  return y & 0x01010101u;
 }
 
 // nontemporal streaming load/store helpers (data touched exactly once)

@@ -41,14 +41,8 @@ __device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) {
   return __float2bfloat16(v);
 }
 
-// single-value encoders (same algebra as hamming.hip, one byte)
-__device__ __forceinline__ uint32_t enc_nibble(uint32_t v, int codec) {
-  uint32_t d0 = v & 1, d1 = v >> 1 & 1, d2 = v >> 2 & 1, d3 = v >> 3 & 1;
-  uint32_t h = v | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6;
-  if (codec == KVECC_CODEC_H84) return h | (d0 ^ d1 ^ d2) << 7;
-  if (codec == KVECC_CODEC_H74) return h;
-  return v;
-}
+// single-value encoder: codec_math.h encode_nibble (KVECC_CODEC_* codes)
+__device__ __forceinline__ uint32_t enc_nibble(uint32_t v, int codec) { return encode_nibble(v, codec); }
 
 __device__ __forceinline__ float row_max(float v, int lpr) {
   for (int off = lpr >> 1; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, kWave));
@@ -105,15 +99,11 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
   }
 }
 
-// Hamming(8,4) decode of one codeword byte: data, type (hamming84_triton.py:145-206)
+// Hamming(8,4) decode of one codeword byte: data, type (codec_math.h h84_decode4)
 __device__ __forceinline__ uint32_t dec84(uint32_t c, uint32_t &type) {
-  uint32_t s0 = __builtin_popcount(c & 0x1Bu) & 1, s1 = __builtin_popcount(c & 0x2Du) & 1;
-  uint32_t s2 = __builtin_popcount(c & 0x4Eu) & 1, pe = __builtin_popcount(c) & 1;
-  uint32_t nz = s0 | s1 | s2;
-  uint32_t fix = (s0 & s1 & ~s2 & 1) | (s0 & ~s1 & s2 & 1) << 1 | (~s0 & s1 & s2 & 1) << 2 |
-                 (s0 & s1 & s2) << 3;
-  type = pe | (pe ^ nz) << 1;
-  return (c ^ (pe ? fix : 0u)) & 0xFu;
+  uint32_t data, n1 = 0, n2 = 0;
+  h84_decode4(c & 0xFFu, data, type, n1, n2);
+  return data;
 }
 
 template <typename TO, int VEC>

@@ -47,6 +47,18 @@ SIGNATURES = {
     "kvecc_any_equal_u8": [_vp, _i64, _u8, _vp, _vp],
     "kvecc_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _vp],
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
+    # host backend (threads instead of a stream)
+    "kvecc_cpu_hamming74_encode": [_vp, _vp, _i64, _int],
+    "kvecc_cpu_hamming84_encode": [_vp, _vp, _i64, _int],
+    "kvecc_cpu_hamming74_decode": [_vp, _vp, _vp, _i64, _vp, _int],
+    "kvecc_cpu_hamming84_decode": [_vp, _vp, _vp, _i64, _vp, _int],
+    "kvecc_cpu_golay_encode": [_vp, _vp, _i64, _int],
+    "kvecc_cpu_golay_decode": [_vp, _vp, _vp, _i64, _vp, _int],
+    "kvecc_cpu_inject_u8": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
+    "kvecc_cpu_inject_i32": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
+    "kvecc_cpu_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _int],
+    "kvecc_cpu_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _int],
+    "kvecc_cpu_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _int],
 }
 _RESTYPE = {
     "kvecc_version": ctypes.c_char_p,

@@ -8,7 +8,8 @@ table and a factory that raises ValueError on unknown names.
 
 A backend is any object exposing the reference's codec function set
 (`FUNCTIONS`).  "hip" is the MI355X implementation and the default; it never
-falls back to anything else.
+falls back to anything else.  "cpu" is the host twin built from the same
+codec algebra (kvecc.cpu_ops); it is used only when asked for by name.
 """
 
 from __future__ import annotations
@@ -28,6 +29,7 @@ FUNCTIONS = (
 # backend name -> module implementing FUNCTIONS
 CODEC_BACKENDS = {
     "hip": "kvecc.ops",
+    "cpu": "kvecc.cpu_ops",  # host twin (BASELINE config 1); explicit, never a fallback
 }
 
 DEFAULT_BACKEND = "hip"
@@ -57,6 +59,9 @@ def get_codec_backend(backend: str = DEFAULT_BACKEND) -> types.ModuleType:
         raise ValueError(f"codec backend '{backend}' lacks {missing}")
     if key == "hip":
         require_hip()
+    elif key == "cpu":
+        from . import _lib
+        _lib.load()
     return mod
 
 

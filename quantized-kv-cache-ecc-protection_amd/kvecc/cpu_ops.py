@@ -1,0 +1,307 @@
+"""Host ("cpu") codec backend: the reference's codec function set on CPU tensors.
+
+The reference has no CPU codec backend -- every Triton wrapper asserts
+``x.is_cuda`` (hamming74_triton.py:185,246; hamming84_triton.py:237,316;
+golay_triton.py:399,456; fault_injection_triton.py:369; interpolation_triton.py:195;
+fused_kernels.py:117,234,388).  BASELINE config 1 (``backend="cpu"``) needs one, so this module
+runs the ``kvecc_cpu_*`` entry points of libkvecc.so: the same codec algebra
+as the gfx950 kernels (csrc/codec_math.h is compiled for both), on host
+memory, over ``std::thread`` workers.  Return values and error behaviour
+mirror kvecc.ops (and therefore the reference wrappers) exactly.
+
+This is an explicitly selected backend (``get_codec_backend("cpu")``), never a
+fallback of the "hip" one; it needs libkvecc.so but no GPU.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+from . import _lib
+from .config import ErrorType
+
+_VP = ctypes.c_void_p
+
+# worker threads per call; <= 0 means every host core.  Defaults to
+# OMP_NUM_THREADS when set (the process's CPU share), like torch's own pool.
+NUM_THREADS = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+
+
+def set_num_threads(n: int) -> None:
+    global NUM_THREADS
+    NUM_THREADS = int(n)
+
+
+def _ptr(t):
+    return _VP(t.data_ptr()) if t is not None else _VP(0)
+
+
+def _check_cpu(t, what="Input"):
+    if t.device.type != "cpu":
+        raise AssertionError(f"{what} must be a CPU tensor for the 'cpu' codec backend")
+
+
+def _flat(t, dtype):
+    f = t.reshape(-1)
+    if f.dtype != dtype:
+        f = f.to(dtype)
+    return f.contiguous()
+
+
+def _stats():
+    return torch.zeros(2, dtype=torch.int64)
+
+
+# ============================================================================
+# Hamming
+# ============================================================================
+
+def hamming74_encode(int4_values: torch.Tensor) -> torch.Tensor:
+    """INT4 -> Hamming(7,4) codewords (host twin of ops.hamming74_encode)."""
+    _check_cpu(int4_values)
+    flat = _flat(int4_values, torch.uint8)
+    out = torch.empty_like(flat)
+    _lib.call("kvecc_cpu_hamming74_encode", _ptr(flat), _ptr(out), flat.numel(), NUM_THREADS)
+    return out.view(int4_values.shape)
+
+
+def hamming74_decode(codewords: torch.Tensor, return_error_detected: bool = False):
+    """-> (decoded, (n_corrected,)) or (decoded, error_detected, (n_corrected,))"""
+    _check_cpu(codewords)
+    flat = _flat(codewords, torch.uint8)
+    data = torch.empty_like(flat)
+    flag = torch.empty_like(flat)
+    st = _stats()
+    _lib.call("kvecc_cpu_hamming74_decode", _ptr(flat), _ptr(data), _ptr(flag), flat.numel(),
+              _ptr(st), NUM_THREADS)
+    n = int(st[0])
+    data = data.view(codewords.shape)
+    if return_error_detected:
+        return data, flag.view(codewords.shape), (n,)
+    return data, (n,)
+
+
+def hamming84_encode(int4_values: torch.Tensor) -> torch.Tensor:
+    _check_cpu(int4_values)
+    flat = _flat(int4_values, torch.uint8)
+    out = torch.empty_like(flat)
+    _lib.call("kvecc_cpu_hamming84_encode", _ptr(flat), _ptr(out), flat.numel(), NUM_THREADS)
+    return out.view(int4_values.shape)
+
+
+def hamming84_decode(codewords: torch.Tensor, return_error_types: bool = False):
+    """-> (decoded, (corrected, detected)) or (decoded, error_types, (corrected, detected))"""
+    _check_cpu(codewords)
+    flat = _flat(codewords, torch.uint8)
+    data = torch.empty_like(flat)
+    etype = torch.empty_like(flat)
+    st = _stats()
+    _lib.call("kvecc_cpu_hamming84_decode", _ptr(flat), _ptr(data), _ptr(etype), flat.numel(),
+              _ptr(st), NUM_THREADS)
+    corrected, detected = int(st[0]), int(st[1])
+    data = data.view(codewords.shape)
+    if return_error_types:
+        return data, etype.view(codewords.shape), (corrected, detected)
+    return data, (corrected, detected)
+
+
+# ============================================================================
+# Golay(24,12)
+# ============================================================================
+
+def golay_encode(triplets: torch.Tensor) -> torch.Tensor:
+    """INT4 triplets [N,3] (or [3]) -> int32 codewords [N]."""
+    _check_cpu(triplets)
+    if triplets.dim() == 1:
+        triplets = triplets.unsqueeze(0)
+    n = triplets.shape[0]
+    flat = _flat(triplets, torch.uint8)
+    if flat.numel() < 3 * n:
+        raise ValueError(f"golay_encode needs 3 values per codeword, got shape {tuple(triplets.shape)}")
+    out = torch.empty(n, dtype=torch.int32)
+    _lib.call("kvecc_cpu_golay_encode", _ptr(flat), _ptr(out), n, NUM_THREADS)
+    return out
+
+
+def golay_decode(codewords: torch.Tensor, return_error_counts: bool = False):
+    """-> (triplets [N,3], (bits_corrected, uncorrectable)) or
+       (triplets, error_counts [N], (bits_corrected, uncorrectable))"""
+    _check_cpu(codewords)
+    n = codewords.numel()
+    flat = _flat(codewords, torch.int32)
+    trip = torch.empty(n * 3, dtype=torch.uint8)
+    counts = torch.empty(n, dtype=torch.uint8)
+    st = _stats()
+    _lib.call("kvecc_cpu_golay_decode", _ptr(flat), _ptr(trip), _ptr(counts), n, _ptr(st),
+              NUM_THREADS)
+    trip = trip.view(n, 3)
+    if return_error_counts:
+        return trip, counts, (int(st[0]), int(st[1]))
+    return trip, (int(st[0]), int(st[1]))
+
+
+def golay_encode_rows(nibbles: torch.Tensor) -> torch.Tensor:
+    """Per-head packing of the shim (ecc_shim.py:623-682), host version."""
+    _check_cpu(nibbles)
+    d = nibbles.shape[-1]
+    g = (d + 2) // 3
+    x = nibbles.reshape(-1, d).to(torch.uint8)
+    padded = torch.zeros(x.shape[0], 3 * g, dtype=torch.uint8)
+    padded[:, :d] = x
+    cw = golay_encode(padded.view(-1, 3))
+    return cw.view(*nibbles.shape[:-1], g)
+
+
+def golay_decode_rows(codewords: torch.Tensor, d: int, stats=None) -> torch.Tensor:
+    """Inverse of golay_encode_rows; `stats` (int64 [2]) accumulates on the host."""
+    _check_cpu(codewords)
+    g = codewords.shape[-1]
+    if g != (d + 2) // 3:
+        raise ValueError(f"{g} codewords per row do not hold {d} values")
+    trip, (bits, unc) = golay_decode(codewords.reshape(-1))
+    if stats is not None:
+        stats[0] += bits
+        stats[1] += unc
+    return trip.view(-1, 3 * g)[:, :d].reshape(*codewords.shape[:-1], d).contiguous()
+
+
+# ============================================================================
+# Fault injection
+# ============================================================================
+
+def inject_into(flat_in, out, ber, n_bits, seed=0, counts=None, stats=None, global_n=None,
+                offset0=0, threads=None):
+    """Host twin of ops.inject_into; `stats` is an int64 [2] host tensor."""
+    n = flat_in.numel()
+    gn = n if global_n is None else int(global_n)
+    if flat_in.dtype == torch.uint8:
+        name = "kvecc_cpu_inject_u8"
+    elif flat_in.dtype == torch.int32:
+        name = "kvecc_cpu_inject_i32"
+    else:
+        raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
+    _lib.call(name, _ptr(flat_in), _ptr(out), _ptr(counts), n, int(n_bits), int(seed), float(ber),
+              gn, int(offset0), _ptr(stats), NUM_THREADS if threads is None else int(threads))
+    return out
+
+
+def inject_bit_errors_triton(data, ber, n_bits, seed=0, return_stats=False):
+    """Bernoulli bit flips on the reference's Philox stream; ber <= 0 returns `data`.
+    -> corrupted, or (corrupted, (total_flips, elements_affected))"""
+    _check_cpu(data)
+    if ber <= 0:
+        if return_stats:
+            return data, (0, 0)
+        return data
+    flat = data.reshape(-1)
+    if flat.dtype not in (torch.uint8, torch.int32):
+        raise ValueError(f"Unsupported dtype: {flat.dtype}. Use uint8 or int32.")
+    flat = flat.contiguous()
+    out = torch.empty_like(flat)
+    st = _stats()
+    inject_into(flat, out, ber, n_bits, seed, stats=st)
+    out = out.view(data.shape)
+    if return_stats:
+        return out, (int(st[0]), int(st[1]))
+    return out
+
+
+inject_bit_errors = inject_bit_errors_triton
+
+
+def inject_bit_errors_triton_batched(data, ber, n_bits, seed=0):
+    corrupted, (total, _) = inject_bit_errors_triton(data, ber, n_bits, seed, return_stats=True)
+    return corrupted, total
+
+
+# ============================================================================
+# Interpolation
+# ============================================================================
+
+def _seq_layout(shape, seq_dim):
+    from .ops import _seq_layout as layout  # pure shape arithmetic, no device code
+    return layout(shape, seq_dim)
+
+
+def interpolate_double_errors(q, error_type, original_shape=None, seq_dim=-1):
+    """Host twin of ops.interpolate_double_errors (interpolation_triton.py:162-265)."""
+    _check_cpu(q)
+    _check_cpu(error_type, "Error type")
+    assert q.shape == error_type.shape, "Shape mismatch between q and error_type"
+    if q.numel() == 0:
+        return q.clone()
+    err = _flat(error_type, torch.uint8)
+    if not bool((err == ErrorType.DOUBLE_DETECTED).any()):
+        return q.clone()
+    qf = _flat(q, torch.uint8)
+    outer, length, inner = _seq_layout(tuple(q.shape), seq_dim)
+    out = torch.empty_like(qf)
+    _lib.call("kvecc_cpu_interpolate", _ptr(qf), _ptr(err), _ptr(out), outer, length, inner,
+              NUM_THREADS)
+    return out.view(q.shape)
+
+
+def interpolate_double_errors_1d(q, error_type):
+    return interpolate_double_errors(q, error_type, seq_dim=-1)
+
+
+def interpolate_double_errors_autotuned(q, error_type, original_shape=None, seq_dim=-1):
+    return interpolate_double_errors(q, error_type, original_shape, seq_dim)
+
+
+# ============================================================================
+# Fused quantize + encode / decode + dequantize
+# ============================================================================
+
+_DT = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
+
+
+def _fused_quantize_encode(input_tensor, codec_code):
+    _check_cpu(input_tensor)
+    if input_tensor.dtype not in _DT:
+        raise TypeError(f"unsupported input dtype {input_tensor.dtype}")
+    shape = input_tensor.shape
+    d = shape[-1]
+    x = input_tensor.reshape(-1, d).contiguous()
+    rows = x.shape[0]
+    cw = torch.empty(rows, d, dtype=torch.uint8)
+    scales = torch.empty(rows, dtype=torch.float32)
+    _lib.call("kvecc_cpu_quantize_encode_rows", _ptr(x), _DT[x.dtype], int(codec_code), _ptr(cw),
+              _ptr(scales), rows, d, NUM_THREADS)
+    if input_tensor.dim() == 1:
+        return cw.squeeze(0), scales
+    return cw.view(shape), scales.view(shape[:-1])
+
+
+def fused_quantize_encode_hamming84(input_tensor):
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H84)
+
+
+def fused_quantize_encode_hamming74(input_tensor):
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H74)
+
+
+def quantize_rows(input_tensor):
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_NONE)
+
+
+def fused_decode_dequantize_hamming84(codewords, scales, output_dtype=torch.float32):
+    """-> (dequantized, errors_corrected); double errors become 0 (fused_kernels.py:344)."""
+    _check_cpu(codewords)
+    _check_cpu(scales, "Scales")
+    shape = codewords.shape
+    d = shape[-1]
+    cw = codewords.reshape(-1, d).contiguous()
+    sc = scales.reshape(-1).to(torch.float32).contiguous()
+    dtype = output_dtype if output_dtype in _DT else torch.float32
+    out = torch.empty(cw.shape, dtype=dtype)
+    st = _stats()
+    _lib.call("kvecc_cpu_decode_dequant_h84_rows", _ptr(cw), _ptr(sc), _ptr(out), _DT[dtype],
+              cw.shape[0], d, 1, _ptr(st), NUM_THREADS)
+    out = out.squeeze(0) if codewords.dim() == 1 else out.view(shape)
+    if output_dtype != dtype:
+        out = out.to(output_dtype)
+    return out, int(st[0])

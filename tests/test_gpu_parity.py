@@ -320,3 +320,45 @@ def test_quantize_vs_torch_path(gpu, oracle, dtype, shape):
     out, nc = kvecc.fused_decode_dequantize_hamming84(cw, s84, output_dtype=dtype)
     ref, _ = oracle.decode_dequant_h84(oracle.hamming84_encode(oq), os_)
     assert torch.equal(out.cpu(), torch.from_numpy(ref).to(dtype)) and nc == 0
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE sizes: HIP backend vs the host backend (chain of trust: the
+# host backend is pinned to the golden vectors in tests/test_cpu_backend.py)
+# ---------------------------------------------------------------------------
+
+def test_config2_full_size_vs_cpu_backend(gpu):
+    """Config 2: H84 encode + inject(BER 1e-3) + decode on [8,4096,32,128]."""
+    import kvecc
+    from kvecc import cpu_ops
+    g = torch.Generator().manual_seed(2)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), dtype=torch.uint8, generator=g)
+    cw_h = cpu_ops.hamming84_encode(x)
+    noisy_h, st_h = cpu_ops.inject_bit_errors_triton(cw_h, 1e-3, 8, seed=7, return_stats=True)
+    dec_h, et_h, dst_h = cpu_ops.hamming84_decode(noisy_h, return_error_types=True)
+    cw = kvecc.hamming84_encode(x.to(gpu))
+    assert torch.equal(cw.cpu(), cw_h)
+    noisy, st = kvecc.inject_bit_errors_triton(cw, 1e-3, 8, seed=7, return_stats=True)
+    assert st == st_h and torch.equal(noisy.cpu(), noisy_h)
+    dec, et, dst = kvecc.hamming84_decode(noisy, return_error_types=True)
+    assert dst == dst_h
+    assert torch.equal(dec.cpu(), dec_h) and torch.equal(et.cpu(), et_h)
+
+
+def test_config3_full_size_vs_cpu_backend(gpu):
+    """Config 3: Golay triplets of [8,4096,32,128] (per-head padding, 43 cw/head),
+    inject(BER 1e-2, 24 bits) + decode."""
+    import kvecc
+    from kvecc import cpu_ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), dtype=torch.uint8, generator=g)
+    cw_h = cpu_ops.golay_encode_rows(x).reshape(-1)
+    noisy_h, st_h = cpu_ops.inject_bit_errors_triton(cw_h, 1e-2, 24, seed=11, return_stats=True)
+    trip_h, cnt_h, dst_h = cpu_ops.golay_decode(noisy_h, return_error_counts=True)
+    cw = kvecc.golay_encode_rows(x.to(gpu)).reshape(-1)
+    assert torch.equal(cw.cpu(), cw_h)
+    noisy, st = kvecc.inject_bit_errors_triton(cw, 1e-2, 24, seed=11, return_stats=True)
+    assert st == st_h and torch.equal(noisy.cpu(), noisy_h)
+    trip, cnt, dst = kvecc.golay_decode(noisy, return_error_counts=True)
+    assert dst == dst_h
+    assert torch.equal(trip.cpu(), trip_h) and torch.equal(cnt.cpu(), cnt_h)
