@@ -174,12 +174,28 @@ KVECC_API int kvecc_cpu_hamming84_decode(const uint8_t *cw, uint8_t *data, uint8
 KVECC_API int kvecc_cpu_golay_encode(const uint8_t *trip, int32_t *cw, int64_t m, int threads);
 KVECC_API int kvecc_cpu_golay_decode(const int32_t *cw, uint8_t *trip, uint8_t *counts, int64_t m,
                                      uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords, int64_t rows,
+                                          int64_t d, int threads);
+KVECC_API int kvecc_cpu_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles, int64_t rows,
+                                          int64_t d, uint64_t *stats, int threads);
 KVECC_API int kvecc_cpu_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
                                   int n_bits, int64_t seed, float ber, int64_t global_n,
                                   int64_t offset0, uint64_t *stats, int threads);
 KVECC_API int kvecc_cpu_inject_i32(const int32_t *in, int32_t *out, uint8_t *counts, int64_t n,
                                    int n_bits, int64_t seed, float ber, int64_t global_n,
                                    int64_t offset0, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_inject_u8_vectorized(const uint8_t *in, uint8_t *out, uint8_t *counts,
+                                             int64_t n, int n_bits, int64_t seed, float ber,
+                                             uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_inject_i32_vectorized(const int32_t *in, int32_t *out, uint8_t *counts,
+                                              int64_t n, int n_bits, int64_t seed, float ber,
+                                              uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_inject_rows_u8(const uint8_t *in, uint8_t *out, int64_t rows,
+                                       int64_t row_len, int n_bits, int64_t seed_base, float ber,
+                                       uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_inject_rows_i32(const int32_t *in, int32_t *out, int64_t rows,
+                                        int64_t row_len, int n_bits, int64_t seed_base, float ber,
+                                        uint64_t *stats, int threads);
 KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
                                     int64_t outer, int64_t len, int64_t inner, int threads);
 KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,

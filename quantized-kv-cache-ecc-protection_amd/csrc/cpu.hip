@@ -216,6 +216,60 @@ KVECC_API int kvecc_cpu_golay_decode(const int32_t *cw, uint8_t *trip, uint8_t *
   return KVECC_OK;
 }
 
+KVECC_API int kvecc_cpu_golay_encode_rows(const uint8_t *nibbles, int32_t *cw, int64_t rows,
+                                          int64_t d, int threads) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_golay_encode_rows: negative size");
+  if (rows && d && (!nibbles || !cw)) return set_error(KVECC_EINVAL, "cpu_golay_encode_rows: null pointer");
+  static uint16_t par[4096];
+  static bool ready = [] { build_golay_parity_table(par); return true; }();
+  (void)ready;
+  const int64_t g = (d + 2) / 3;
+  parallel_for(rows, threads, 1, [&](int64_t b, int64_t e, int) {
+    for (int64_t r = b; r < e; ++r)
+      for (int64_t k = 0; k < g; ++k) {
+        const uint8_t *x = nibbles + r * d + 3 * k;
+        const int64_t left = d - 3 * k;  // zero padding of the last group
+        uint32_t dw = golay_pack(x[0], left > 1 ? x[1] : 0, left > 2 ? x[2] : 0);
+        cw[r * g + k] = (int32_t)(dw | (uint32_t)par[dw] << 12);
+      }
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_golay_decode_rows(const int32_t *cw, uint8_t *nibbles, int64_t rows,
+                                          int64_t d, uint64_t *stats, int threads) {
+  if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_golay_decode_rows: negative size");
+  if (rows && d && (!nibbles || !cw)) return set_error(KVECC_EINVAL, "cpu_golay_decode_rows: null pointer");
+  static uint16_t tab[8192];
+  static bool ready = [] {
+    build_golay_parity_table(tab);
+    build_golay_correct_table(tab + 4096);
+    return true;
+  }();
+  (void)ready;
+  const int64_t g = (d + 2) / 3;
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, rows, 1)));
+  parallel_for(rows, threads, 1, [&](int64_t b, int64_t e, int t) {
+    uint64_t bits = 0, unc = 0;
+    for (int64_t r = b; r < e; ++r)
+      for (int64_t k = 0; k < g; ++k) {
+        uint32_t c;
+        const uint32_t dw = golay_decode1((uint32_t)cw[r * g + k], tab, tab + 4096, c);
+        bits += c & 3u;
+        unc += c >> 2;
+        uint8_t *o = nibbles + r * d + 3 * k;
+        const int64_t left = d - 3 * k;
+        o[0] = (uint8_t)(dw & 0xF);
+        if (left > 1) o[1] = (uint8_t)(dw >> 4 & 0xF);
+        if (left > 2) o[2] = (uint8_t)(dw >> 8);
+      }
+    acc[t].a += bits;
+    acc[t].b += unc;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
 }  // extern "C"
 
 template <typename T>
@@ -248,6 +302,65 @@ static int cpu_inject(const T *in, T *out, uint8_t *counts, int64_t n, int n_bit
   return KVECC_OK;
 }
 
+template <typename T>
+static int cpu_inject_rows(const T *in, T *out, int64_t rows, int64_t row_len, int n_bits,
+                           int64_t seed_base, float ber, uint64_t *stats, int threads,
+                           const char *name) {
+  if (rows < 0 || row_len < 0) return set_error(KVECC_EINVAL, "%s: negative size", name);
+  const int64_t total = rows * row_len;
+  if (total && (!in || !out)) return set_error(KVECC_EINVAL, "%s: null pointer", name);
+  const uint32_t rowmul = (uint32_t)((uint64_t)row_len * (uint64_t)n_bits);
+  const uint32_t sb = (uint32_t)(uint64_t)seed_base;
+  const uint32_t thr = kvecc_ber_threshold(ber);
+  const int nb = sizeof(T) == 1 ? (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits))
+                                : (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits));
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, total, 1 << 12)));
+  parallel_for(total, threads, 64, [&](int64_t b, int64_t e, int t) {
+    uint64_t flips = 0, hit = 0;
+    for (int64_t i = b; i < e; ++i) {
+      const int64_t r = i / row_len;
+      const uint32_t j = (uint32_t)(i - r * row_len);
+      const uint32_t m = philox_flip_mask<-1>((sb + (uint32_t)r) * rowmul + j * (uint32_t)n_bits,
+                                              j, thr, nb);
+      out[i] = (T)((uint32_t)in[i] ^ m);
+      uint32_t c = __builtin_popcount(m);
+      flips += c;
+      hit += c != 0;
+    }
+    acc[t].a += flips;
+    acc[t].b += hit;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
+template <typename T>
+static int cpu_inject_vec(const T *in, T *out, uint8_t *counts, int64_t n, int n_bits,
+                          int64_t seed, float ber, uint64_t *stats, int threads, const char *name) {
+  if (n < 0) return set_error(KVECC_EINVAL, "%s: negative n", name);
+  if (n && (!in || !out)) return set_error(KVECC_EINVAL, "%s: null pointer", name);
+  const uint32_t seedn = (uint32_t)((uint64_t)seed * (uint64_t)n);
+  const uint32_t thr = kvecc_ber_threshold(ber);
+  const int nb = sizeof(T) == 1 ? (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits))
+                                : (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits));
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, n, 1 << 12)));
+  parallel_for(n, threads, 64, [&](int64_t b, int64_t e, int t) {
+    uint64_t flips = 0, hit = 0;
+    for (int64_t i = b; i < e; ++i) {
+      const uint32_t m = philox_flip_mask_vec(seedn, (uint32_t)n, (uint32_t)i, thr, nb);
+      out[i] = (T)((uint32_t)in[i] ^ m);
+      uint32_t c = __builtin_popcount(m);
+      if (counts) counts[i] = (uint8_t)c;
+      flips += c;
+      hit += c != 0;
+    }
+    acc[t].a += flips;
+    acc[t].b += hit;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
 extern "C" {
 
 KVECC_API int kvecc_cpu_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
@@ -262,6 +375,34 @@ KVECC_API int kvecc_cpu_inject_i32(const int32_t *in, int32_t *out, uint8_t *cou
                                    int64_t offset0, uint64_t *stats, int threads) {
   return cpu_inject<int32_t>(in, out, counts, n, n_bits, seed, ber, global_n, offset0, stats,
                              threads, "cpu_inject_i32");
+}
+
+KVECC_API int kvecc_cpu_inject_u8_vectorized(const uint8_t *in, uint8_t *out, uint8_t *counts,
+                                             int64_t n, int n_bits, int64_t seed, float ber,
+                                             uint64_t *stats, int threads) {
+  return cpu_inject_vec<uint8_t>(in, out, counts, n, n_bits, seed, ber, stats, threads,
+                                 "cpu_inject_u8_vectorized");
+}
+
+KVECC_API int kvecc_cpu_inject_i32_vectorized(const int32_t *in, int32_t *out, uint8_t *counts,
+                                              int64_t n, int n_bits, int64_t seed, float ber,
+                                              uint64_t *stats, int threads) {
+  return cpu_inject_vec<int32_t>(in, out, counts, n, n_bits, seed, ber, stats, threads,
+                                 "cpu_inject_i32_vectorized");
+}
+
+KVECC_API int kvecc_cpu_inject_rows_u8(const uint8_t *in, uint8_t *out, int64_t rows,
+                                       int64_t row_len, int n_bits, int64_t seed_base, float ber,
+                                       uint64_t *stats, int threads) {
+  return cpu_inject_rows<uint8_t>(in, out, rows, row_len, n_bits, seed_base, ber, stats, threads,
+                                  "cpu_inject_rows_u8");
+}
+
+KVECC_API int kvecc_cpu_inject_rows_i32(const int32_t *in, int32_t *out, int64_t rows,
+                                        int64_t row_len, int n_bits, int64_t seed_base, float ber,
+                                        uint64_t *stats, int threads) {
+  return cpu_inject_rows<int32_t>(in, out, rows, row_len, n_bits, seed_base, ber, stats, threads,
+                                  "cpu_inject_rows_i32");
 }
 
 KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,

@@ -54,6 +54,12 @@ SIGNATURES = {
     "kvecc_cpu_hamming84_decode": [_vp, _vp, _vp, _i64, _vp, _int],
     "kvecc_cpu_golay_encode": [_vp, _vp, _i64, _int],
     "kvecc_cpu_golay_decode": [_vp, _vp, _vp, _i64, _vp, _int],
+    "kvecc_cpu_golay_encode_rows": [_vp, _vp, _i64, _i64, _int],
+    "kvecc_cpu_golay_decode_rows": [_vp, _vp, _i64, _i64, _vp, _int],
+    "kvecc_cpu_inject_u8_vectorized": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _vp, _int],
+    "kvecc_cpu_inject_i32_vectorized": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _vp, _int],
+    "kvecc_cpu_inject_rows_u8": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _int],
+    "kvecc_cpu_inject_rows_i32": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _int],
     "kvecc_cpu_inject_u8": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
     "kvecc_cpu_inject_i32": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
     "kvecc_cpu_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _int],

@@ -55,9 +55,45 @@ def _stats():
     return torch.zeros(2, dtype=torch.int64)
 
 
+# ---- statistics (host twin of ops.new_stats / read_stats) -------------------
+def new_stats(device=None):
+    """Host statistics buffer: int64 [2], stats[k] += ... by every *_into call."""
+    return _stats()
+
+
+def stats_totals(stats, n=2):
+    return stats[:n].clone()
+
+
+def read_stats(stats, n=2):
+    return [int(v) for v in stats[:n].tolist()]
+
+
 # ============================================================================
 # Hamming
 # ============================================================================
+
+def hamming74_encode_into(flat_in, out):
+    _lib.call("kvecc_cpu_hamming74_encode", _ptr(flat_in), _ptr(out), flat_in.numel(), NUM_THREADS)
+    return out
+
+
+def hamming84_encode_into(flat_in, out):
+    _lib.call("kvecc_cpu_hamming84_encode", _ptr(flat_in), _ptr(out), flat_in.numel(), NUM_THREADS)
+    return out
+
+
+def hamming74_decode_into(flat_cw, data, flag=None, stats=None):
+    _lib.call("kvecc_cpu_hamming74_decode", _ptr(flat_cw), _ptr(data), _ptr(flag), flat_cw.numel(),
+              _ptr(stats), NUM_THREADS)
+    return data
+
+
+def hamming84_decode_into(flat_cw, data, error_type=None, stats=None):
+    _lib.call("kvecc_cpu_hamming84_decode", _ptr(flat_cw), _ptr(data), _ptr(error_type),
+              flat_cw.numel(), _ptr(stats), NUM_THREADS)
+    return data
+
 
 def hamming74_encode(int4_values: torch.Tensor) -> torch.Tensor:
     """INT4 -> Hamming(7,4) codewords (host twin of ops.hamming74_encode)."""
@@ -112,6 +148,17 @@ def hamming84_decode(codewords: torch.Tensor, return_error_types: bool = False):
 # Golay(24,12)
 # ============================================================================
 
+def golay_encode_into(flat_triplets, codewords, m):
+    _lib.call("kvecc_cpu_golay_encode", _ptr(flat_triplets), _ptr(codewords), m, NUM_THREADS)
+    return codewords
+
+
+def golay_decode_into(flat_cw, triplets, counts=None, stats=None):
+    _lib.call("kvecc_cpu_golay_decode", _ptr(flat_cw), _ptr(triplets), _ptr(counts),
+              flat_cw.numel(), _ptr(stats), NUM_THREADS)
+    return triplets
+
+
 def golay_encode(triplets: torch.Tensor) -> torch.Tensor:
     """INT4 triplets [N,3] (or [3]) -> int32 codewords [N]."""
     _check_cpu(triplets)
@@ -144,28 +191,30 @@ def golay_decode(codewords: torch.Tensor, return_error_counts: bool = False):
 
 
 def golay_encode_rows(nibbles: torch.Tensor) -> torch.Tensor:
-    """Per-head packing of the shim (ecc_shim.py:623-682), host version."""
+    """Per-head packing of the shim (ecc_shim.py:623-682): [..., D] nibbles ->
+    [..., ceil(D/3)] codewords, each row zero-padded to a multiple of 3."""
     _check_cpu(nibbles)
     d = nibbles.shape[-1]
     g = (d + 2) // 3
-    x = nibbles.reshape(-1, d).to(torch.uint8)
-    padded = torch.zeros(x.shape[0], 3 * g, dtype=torch.uint8)
-    padded[:, :d] = x
-    cw = golay_encode(padded.view(-1, 3))
-    return cw.view(*nibbles.shape[:-1], g)
+    flat = _flat(nibbles, torch.uint8)
+    rows = flat.numel() // d if d else 0
+    out = torch.empty(*nibbles.shape[:-1], g, dtype=torch.int32)
+    _lib.call("kvecc_cpu_golay_encode_rows", _ptr(flat), _ptr(out), rows, d, NUM_THREADS)
+    return out
 
 
 def golay_decode_rows(codewords: torch.Tensor, d: int, stats=None) -> torch.Tensor:
-    """Inverse of golay_encode_rows; `stats` (int64 [2]) accumulates on the host."""
+    """Inverse of golay_encode_rows: [..., ceil(d/3)] -> [..., d] nibbles."""
     _check_cpu(codewords)
     g = codewords.shape[-1]
     if g != (d + 2) // 3:
         raise ValueError(f"{g} codewords per row do not hold {d} values")
-    trip, (bits, unc) = golay_decode(codewords.reshape(-1))
-    if stats is not None:
-        stats[0] += bits
-        stats[1] += unc
-    return trip.view(-1, 3 * g)[:, :d].reshape(*codewords.shape[:-1], d).contiguous()
+    flat = _flat(codewords, torch.int32)
+    rows = flat.numel() // g if g else 0
+    out = torch.empty(*codewords.shape[:-1], d, dtype=torch.uint8)
+    _lib.call("kvecc_cpu_golay_decode_rows", _ptr(flat), _ptr(out), rows, d, _ptr(stats),
+              NUM_THREADS)
+    return out
 
 
 # ============================================================================
@@ -185,6 +234,19 @@ def inject_into(flat_in, out, ber, n_bits, seed=0, counts=None, stats=None, glob
         raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
     _lib.call(name, _ptr(flat_in), _ptr(out), _ptr(counts), n, int(n_bits), int(seed), float(ber),
               gn, int(offset0), _ptr(stats), NUM_THREADS if threads is None else int(threads))
+    return out
+
+
+def inject_rows_into(flat_in, out, rows, row_len, ber, n_bits, seed_base, stats=None):
+    """Per-row injection: row r uses seed_base + r and N = row_len (shim scheme)."""
+    if flat_in.dtype == torch.uint8:
+        name = "kvecc_cpu_inject_rows_u8"
+    elif flat_in.dtype == torch.int32:
+        name = "kvecc_cpu_inject_rows_i32"
+    else:
+        raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
+    _lib.call(name, _ptr(flat_in), _ptr(out), int(rows), int(row_len), int(n_bits), int(seed_base),
+              float(ber), _ptr(stats), NUM_THREADS)
     return out
 
 
@@ -217,6 +279,31 @@ def inject_bit_errors_triton_batched(data, ber, n_bits, seed=0):
     return corrupted, total
 
 
+def inject_bit_errors_triton_vectorized(data, ber, n_bits, seed=0, return_stats=False):
+    """rand4x variant (fault_injection_triton.py:434-496), host twin."""
+    _check_cpu(data)
+    if ber <= 0:
+        if return_stats:
+            return data, (0, 0)
+        return data
+    flat = data.reshape(-1)
+    if flat.dtype == torch.uint8:
+        name = "kvecc_cpu_inject_u8_vectorized"
+    elif flat.dtype == torch.int32:
+        name = "kvecc_cpu_inject_i32_vectorized"
+    else:
+        raise ValueError(f"Unsupported dtype: {flat.dtype}. Use uint8 or int32.")
+    flat = flat.contiguous()
+    out = torch.empty_like(flat)
+    st = _stats()
+    _lib.call(name, _ptr(flat), _ptr(out), _VP(0), flat.numel(), int(n_bits), int(seed), float(ber),
+              _ptr(st), NUM_THREADS)
+    out = out.view(data.shape)
+    if return_stats:
+        return out, (int(st[0]), int(st[1]))
+    return out
+
+
 # ============================================================================
 # Interpolation
 # ============================================================================
@@ -224,6 +311,24 @@ def inject_bit_errors_triton_batched(data, ber, n_bits, seed=0):
 def _seq_layout(shape, seq_dim):
     from .ops import _seq_layout as layout  # pure shape arithmetic, no device code
     return layout(shape, seq_dim)
+
+
+def any_equal(x, value, flag=None):
+    """int32 flag [1] = any(x == value) (host twin of ops.any_equal)."""
+    if flag is None:
+        flag = torch.empty(1, dtype=torch.int32)
+    flag.fill_(int(bool((x == value).any())))
+    return flag
+
+
+def interpolate_into(q, err, out, outer, length, inner, gate=None):
+    """Host twin of ops.interpolate_into; `gate` (a host int32 flag) == 0 copies q."""
+    if gate is not None and int(gate.reshape(-1)[0]) == 0:
+        out.copy_(q)
+        return out
+    _lib.call("kvecc_cpu_interpolate", _ptr(q), _ptr(err), _ptr(out), outer, length, inner,
+              NUM_THREADS)
+    return out
 
 
 def interpolate_double_errors(q, error_type, original_shape=None, seq_dim=-1):
@@ -257,6 +362,22 @@ def interpolate_double_errors_autotuned(q, error_type, original_shape=None, seq_
 # ============================================================================
 
 _DT = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
+
+
+def quantize_encode_rows_into(x2d, codec_code, cw, scales):
+    if x2d.dtype not in _DT:
+        raise TypeError(f"unsupported input dtype {x2d.dtype}")
+    rows, d = x2d.shape
+    _lib.call("kvecc_cpu_quantize_encode_rows", _ptr(x2d), _DT[x2d.dtype], int(codec_code), _ptr(cw),
+              _ptr(scales), rows, d, NUM_THREADS)
+    return cw, scales
+
+
+def decode_dequant_h84_into(cw2d, scales, out, zero_doubles=True, stats=None):
+    rows, d = cw2d.shape
+    _lib.call("kvecc_cpu_decode_dequant_h84_rows", _ptr(cw2d), _ptr(scales), _ptr(out),
+              _DT[out.dtype], rows, d, int(bool(zero_doubles)), _ptr(stats), NUM_THREADS)
+    return out
 
 
 def _fused_quantize_encode(input_tensor, codec_code):

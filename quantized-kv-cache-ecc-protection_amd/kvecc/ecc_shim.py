@@ -26,7 +26,6 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
 from .backends import get_codec_backend
 
 try:  # optional, as in the reference (:54)
@@ -216,16 +215,16 @@ class ECCBackend:
         self.num_kv_groups = num_heads // self.num_kv_heads
         self._injection_count = 0
         self._total_values = 0
-        self._stats = ops.new_stats(manager.k_cache.device)  # device counters
+        self._stats = self.codec_backend.new_stats(manager.k_cache.device)  # backend counters
 
     # counters read lazily (one sync) -------------------------------------------
     @property
     def _errors_corrected(self):
-        return ops.read_stats(self._stats, 2)[0]
+        return self.codec_backend.read_stats(self._stats, 2)[0]
 
     @property
     def _errors_detected(self):
-        return ops.read_stats(self._stats, 2)[1]
+        return self.codec_backend.read_stats(self._stats, 2)[1]
 
     def reset_stats(self):
         self._injection_count = 0
@@ -235,7 +234,7 @@ class ECCBackend:
     def _inject_rows(self, enc, rows, row_len, seed_base):
         """Per-row injection of the reference's write loop, in place."""
         flat = enc.view(-1) if enc.dtype != torch.float8_e4m3fn else enc.view(torch.uint8).view(-1)
-        ops.inject_rows_into(flat, flat, rows, row_len, self.config.ber,
+        self.codec_backend.inject_rows_into(flat, flat, rows, row_len, self.config.ber,
                              _N_BITS[self.config.codec], seed_base)
 
     def write(self, k, v, layer_idx, seq_id=0):
@@ -253,6 +252,7 @@ class ECCBackend:
         kr = k.reshape(batch, seq_len, hk, d)
         vr = v.reshape(batch, seq_len, hk, d)
         codec = cfg.codec
+        ops = self.codec_backend
         for which, x, cache, scales in ((0, kr, mgr.k_cache, mgr.k_scales),
                                         (1, vr, mgr.v_cache, mgr.v_scales)):
             if codec == "fp16":
@@ -289,6 +289,7 @@ class ECCBackend:
     def _decode(self, enc, stats):
         """Codewords [ctx, heads, *] -> INT4 [ctx, heads, head_dim] (stats += ...)."""
         codec, d = self.config.codec, self.head_dim
+        ops = self.codec_backend
         if codec == "golay":
             return ops.golay_decode_rows(enc, d, stats=stats)
         flat = enc.reshape(-1)
@@ -592,7 +593,7 @@ def get_ecc_stats(model):
         stats["sequences"] = len(m.seq_to_blocks)
     if hasattr(model, "_ecc_backend"):
         be = model._ecc_backend
-        corrected, detected = ops.read_stats(be._stats, 2)
+        corrected, detected = be.codec_backend.read_stats(be._stats, 2)
         stats["injection_count"] = be._injection_count
         stats["errors_corrected"] = corrected
         stats["errors_detected"] = detected

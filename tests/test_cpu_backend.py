@@ -169,3 +169,53 @@ def test_fused_low_precision(cpu, dtype):
     dq, _ = cpu.fused_decode_dequantize_hamming84(cw, s, output_dtype=dtype)
     dq32, _ = cpu.fused_decode_dequantize_hamming84(cw, s, output_dtype=torch.float32)
     assert dq.dtype == dtype and torch.equal(dq, dq32.to(dtype))
+
+
+def test_inject_vectorized_golden(cpu, golden, manifest):
+    g = golden("inject_vec")
+    for i, c in enumerate(manifest["inject_vec"]["params"]["cases"]):
+        x = T(g[f"c{i}_in"])
+        out, st = cpu.inject_bit_errors_triton_vectorized(x, c["ber"], c["n_bits"], c["seed"],
+                                                          return_stats=True)
+        if c["ber"] > 0:
+            assert np.array_equal(out.numpy(), g[f"c{i}_out"]), c
+            assert st == tuple(g[f"c{i}_stats"].tolist()), c
+
+
+@pytest.mark.parametrize("dtype,row_len,nb", [("u8", 128, 8), ("u8", 64, 7), ("i32", 43, 24),
+                                              ("u8", 64, 4)])
+def test_inject_rows_vs_oracle(cpu, oracle, dtype, row_len, nb):
+    """Shim per-row scheme: row r is its own call with seed_base + r, N = row_len."""
+    rng = np.random.default_rng(row_len)
+    rows = 200
+    if dtype == "u8":
+        x = rng.integers(0, 256, size=rows * row_len, dtype=np.int64).astype(np.uint8)
+    else:
+        x = rng.integers(0, 2**24, size=rows * row_len, dtype=np.int64).astype(np.int32)
+    xt = T(x)
+    out = torch.empty_like(xt)
+    st = cpu.new_stats()
+    cpu.inject_rows_into(xt, out, rows, row_len, 0.05, nb, seed_base=1000, stats=st)
+    refs = [oracle.inject(x[r * row_len:(r + 1) * row_len], 0.05, nb, 1000 + r) for r in range(rows)]
+    assert np.array_equal(out.numpy(), np.concatenate([r[0] for r in refs]))
+    assert cpu.read_stats(st) == [sum(r[2][0] for r in refs), sum(r[2][1] for r in refs)]
+    cpu.inject_rows_into(xt, xt, rows, row_len, 0.05, nb, seed_base=1000)  # in place
+    assert np.array_equal(xt.numpy(), out.numpy())
+
+
+def test_golay_rows_vs_flat(cpu):
+    """Row packing equals explicit zero padding + flat encode; decode stats add up."""
+    g = torch.Generator().manual_seed(8)
+    for d in (128, 100, 64, 5):
+        x = torch.randint(0, 16, (7, 3, d), dtype=torch.uint8, generator=g)
+        gs = (d + 2) // 3
+        pad = torch.zeros(7, 3, 3 * gs, dtype=torch.uint8)
+        pad[..., :d] = x
+        cw = cpu.golay_encode_rows(x)
+        assert torch.equal(cw.reshape(-1), cpu.golay_encode(pad.view(-1, 3)))
+        noisy = cpu.inject_bit_errors_triton(cw, 0.05, 24, seed=1)
+        st = cpu.new_stats()
+        dec = cpu.golay_decode_rows(noisy, d, stats=st)
+        trip, (bits, unc) = cpu.golay_decode(noisy.reshape(-1))
+        assert torch.equal(dec, trip.view(7, 3, 3 * gs)[..., :d])
+        assert cpu.read_stats(st) == [bits, unc]

@@ -349,13 +349,13 @@ def test_config3_full_size_vs_cpu_backend(gpu):
     """Config 3: Golay triplets of [8,4096,32,128] (per-head padding, 43 cw/head),
     inject(BER 1e-2, 24 bits) + decode."""
     import kvecc
-    from kvecc import cpu_ops
+    from kvecc import cpu_ops, ops
     g = torch.Generator().manual_seed(3)
     x = torch.randint(0, 16, (8, 4096, 32, 128), dtype=torch.uint8, generator=g)
     cw_h = cpu_ops.golay_encode_rows(x).reshape(-1)
     noisy_h, st_h = cpu_ops.inject_bit_errors_triton(cw_h, 1e-2, 24, seed=11, return_stats=True)
     trip_h, cnt_h, dst_h = cpu_ops.golay_decode(noisy_h, return_error_counts=True)
-    cw = kvecc.golay_encode_rows(x.to(gpu)).reshape(-1)
+    cw = ops.golay_encode_rows(x.to(gpu)).reshape(-1)
     assert torch.equal(cw.cpu(), cw_h)
     noisy, st = kvecc.inject_bit_errors_triton(cw, 1e-2, 24, seed=11, return_stats=True)
     assert st == st_h and torch.equal(noisy.cpu(), noisy_h)

@@ -52,14 +52,14 @@ def _model(golden, manifest, device):
     return model.to(device), torch.from_numpy(g["input_ids"]).to(device), g
 
 
-@pytest.mark.gpu
-def test_shim_gpt2_matches_reference(gpu, golden, manifest):
+def _shim_matches_reference(device, backend, golden, manifest):
     from kvecc.ecc_shim import (ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention,
                                 reset_ecc_cache)
-    model, ids, g = _model(golden, manifest, gpu)
+    model, ids, g = _model(golden, manifest, device)
     for i, run in enumerate(manifest["shim_gpt2"]["params"]["runs"]):
         cfg = ECCShimConfig(codec=run["codec"], ber=run["ber"], inject_errors=run["ber"] > 0,
-                            seed=42, block_size=16, use_interpolation=run["use_interpolation"])
+                            seed=42, block_size=16, use_interpolation=run["use_interpolation"],
+                            backend=backend)
         with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=16):
             reset_ecc_cache(model)
             out = model(ids)
@@ -72,15 +72,22 @@ def test_shim_gpt2_matches_reference(gpu, golden, manifest):
 
 
 @pytest.mark.gpu
-def test_shim_cache_bits_match_oracle(gpu):
-    """Cache codewords after one write equal the reference loop restated with
-    the oracle: quantize rows, encode, per-row seeds (K: s+r, V: s+r+1)."""
+def test_shim_gpt2_matches_reference(gpu, golden, manifest):
+    _shim_matches_reference(gpu, "hip", golden, manifest)
+
+
+def test_shim_gpt2_matches_reference_cpu_backend(golden, manifest):
+    """The same end-to-end run on the host backend (model and cache on the CPU)."""
+    _shim_matches_reference(torch.device("cpu"), "cpu", golden, manifest)
+
+
+def _cache_bits_match_oracle(gpu, backend):
     from oracle import oracle
     from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
     torch.manual_seed(0)
     b, s, hk, d = 2, 20, 3, 64
     for codec, nb in (("hamming84", 8), ("golay", 24), ("hamming74", 7), ("int4", 4)):
-        cfg = ECCShimConfig(codec=codec, ber=0.05, inject_errors=True, seed=7)
+        cfg = ECCShimConfig(codec=codec, ber=0.05, inject_errors=True, seed=7, backend=backend)
         mgr = SimpleBlockManager(4, 16, 2, hk, d, device=gpu, codec=codec)
         be = ECCBackend(mgr, cfg, num_heads=hk)
         k = torch.randn(b, s, hk * d, device=gpu, dtype=torch.float16)
@@ -110,3 +117,14 @@ def test_shim_cache_bits_match_oracle(gpu):
                     per = exp.size
                     got = cache[blk, 1, h, slot * per:(slot + 1) * per].cpu().numpy()
                     assert np.array_equal(got, exp), (codec, which, pos, h)
+
+
+@pytest.mark.gpu
+def test_shim_cache_bits_match_oracle(gpu):
+    """Cache codewords after one write equal the reference loop restated with
+    the oracle: quantize rows, encode, per-row seeds (K: s+r, V: s+r+1)."""
+    _cache_bits_match_oracle(gpu, "hip")
+
+
+def test_shim_cache_bits_match_oracle_cpu_backend():
+    _cache_bits_match_oracle(torch.device("cpu"), "cpu")
