@@ -52,7 +52,7 @@ enum {
 /* dtype codes for fused kernels */
 enum { KVECC_F32 = 0, KVECC_F16 = 1, KVECC_BF16 = 2 };
 /* codec codes for fused kernels */
-enum { KVECC_CODEC_NONE = 0, KVECC_CODEC_H74 = 1, KVECC_CODEC_H84 = 2 };
+enum { KVECC_CODEC_NONE = 0, KVECC_CODEC_H74 = 1, KVECC_CODEC_H84 = 2, KVECC_CODEC_GOLAY = 3 };
 
 /* ---- runtime --------------------------------------------------------------- */
 KVECC_API const char *kvecc_version(void);
@@ -157,6 +157,37 @@ KVECC_API int kvecc_decode_dequant_h84_rows(const uint8_t *cw, const float *scal
                                             int out_dtype, int64_t rows, int64_t d,
                                             int zero_doubles, uint64_t *stats, void *stream);
 
+/* ---- ECC shim: KV-cache write and read -------------------------------------- */
+/* ecc_shim.py:557-721 (ECCBackend.write) for codec KVECC_CODEC_NONE (int4),
+ * H74, H84, GOLAY in ONE launch: K and V [batch, seq, hkv*d] (x_dtype,
+ * contiguous) are quantized per (pos, head) row (absmax/7, round-half-even),
+ * encoded, injected with the row's own seed when `inject` and ber > 0
+ * (K: seed0 + r, V: seed0 + r + 1, r = (b*seq + pos)*hkv + h; n_bits per
+ * codeword as ecc_shim.py:555-560) and stored into the paged caches -- only the
+ * last batch, which is what the reference's same-slot writes leave behind.
+ * Caches: [blocks, num_layers, hkv, block_size, P] with P = d (uint8) or
+ * ceil(d/3) (int32, Golay per-head padding); scales fp32 [blocks, num_layers,
+ * hkv, block_size]; token pos lives in physical block block_table[pos / block_size]
+ * (device int32).  d <= 512. */
+KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
+                               int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
+                               int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
+                               float *k_scales, float *v_scales, const int32_t *block_table,
+                               int64_t num_layers, int64_t block_size, int64_t layer,
+                               void *stream);
+/* ecc_shim.py:990-1071 (ECCBackend.attend, decode side) in ONE launch: gather
+ * the first ctx tokens of layer `layer`, decode (H74: stats[0] += #flagged;
+ * H84: stats[0] += #SINGLE_CORRECTED, stats[1] += #DOUBLE_DETECTED; Golay:
+ * stats[0] += bits corrected, stats[1] += #uncorrectable; stats may be NULL),
+ * interpolate H84 double errors along the context when `interp`, dequantize
+ * (q - 8) * scale in fp32 and store k_out / v_out as [hkv, ctx, d] in out_dtype
+ * (RNE).  Byte codecs need d % 4 == 0. */
+KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,
+                              const float *v_scales, const int32_t *block_table, int64_t ctx,
+                              int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
+                              int64_t layer, int codec, int interp, void *k_out, void *v_out,
+                              int out_dtype, uint64_t *stats, void *stream);
+
 /* ---- Host ("cpu") backend ------------------------------------------------- */
 /* The reference has no CPU codec backend (every wrapper asserts x.is_cuda,
  * e.g. hamming74_triton.py:185,246, golay_triton.py:399,456); BASELINE config 1 asks
@@ -203,6 +234,17 @@ KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int cod
 KVECC_API int kvecc_cpu_decode_dequant_h84_rows(const uint8_t *cw, const float *scales, void *out,
                                                 int out_dtype, int64_t rows, int64_t d,
                                                 int zero_doubles, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
+                                   int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
+                                   int inject, float ber, int64_t seed0, void *k_cache,
+                                   void *v_cache, float *k_scales, float *v_scales,
+                                   const int32_t *block_table, int64_t num_layers,
+                                   int64_t block_size, int64_t layer, int threads);
+KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,
+                                  const float *v_scales, const int32_t *block_table, int64_t ctx,
+                                  int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
+                                  int64_t layer, int codec, int interp, void *k_out, void *v_out,
+                                  int out_dtype, uint64_t *stats, int threads);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@
 // interpolation_triton.py:120-159, fused_kernels.py:18-357.
 #pragma once
 
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -86,10 +87,44 @@ KV_HD uint32_t encode_nibble(uint32_t v, int codec) {
   return v;
 }
 
+// ---- INT4 row quantization (shim torch path, ecc_shim.py:572-580) -----------------
+
+// correctly rounded fp32 division on both sides (torch's x / scale)
+KV_HD float div_rn(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __fdiv_rn(a, b);
+#else
+  return a / b;
+#endif
+}
+
+// scale = absmax / 7, 0 -> 1 (compute_quantization_scales, paged_cache_ecc.py:302-334)
+KV_HD float row_scale(float amax) {
+  float s = div_rn(amax, 7.0f);
+  return s == 0.0f ? 1.0f : s;
+}
+
+// round_half_even(x / scale) clamped to [-8, 7], + 8
+KV_HD uint32_t quantize_nibble(float x, float scale) {
+  float q = rintf(div_rn(x, scale));
+  q = fminf(fmaxf(q, -8.0f), 7.0f);
+  return (uint32_t)(int)(q + 8.0f);
+}
+
 // ---- Golay(24,12) ---------------------------------------------------------------
 
 KV_HD uint32_t golay_pack(uint32_t b0, uint32_t b1, uint32_t b2) {
   return (b0 & 0xFu) | (b1 & 0xFu) << 4 | (b2 & 0xFu) << 8;
+}
+
+// 12 parity bits of a data word: bit i = parity(d & B_COL[i]) (golay_triton.py:59-70,130-155)
+KV_HD uint32_t golay_parity12(uint32_t d) {
+  constexpr uint32_t kBCol[12] = {0xA3B, 0xD1D, 0xE8E, 0xB47, 0xDA3, 0xED1,
+                                  0xF68, 0xBB4, 0x9DA, 0x8ED, 0xC76, 0x7FF};
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) p |= ((uint32_t)__builtin_popcount(d & kBCol[i]) & 1u) << i;
+  return p;
 }
 
 // 12-bit data word -> its three nibbles in three consecutive bytes

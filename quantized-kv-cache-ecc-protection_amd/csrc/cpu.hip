@@ -74,11 +74,6 @@ void add_stats(uint64_t *stats, const std::vector<Acc2> &acc, int n) {
   }
 }
 
-template <typename T>
-float to_f32(const void *p, int64_t i) {
-  return (float)reinterpret_cast<const T *>(p)[i];
-}
-
 float load_x(const void *x, int dtype, int64_t i) {
   if (dtype == KVECC_F16) return __half2float(reinterpret_cast<const __half *>(x)[i]);
   if (dtype == KVECC_BF16) return __bfloat162float(reinterpret_cast<const __hip_bfloat16 *>(x)[i]);
@@ -469,6 +464,154 @@ KVECC_API int kvecc_cpu_decode_dequant_h84_rows(const uint8_t *cw, const float *
       }
     acc[t].a += n1;
     acc[t].b += n2;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
+// ---- shim write / read (host twins of shim.hip) ------------------------------
+
+KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
+                                   int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
+                                   int inject, float ber, int64_t seed0, void *k_cache,
+                                   void *v_cache, float *k_scales, float *v_scales,
+                                   const int32_t *block_table, int64_t num_layers,
+                                   int64_t block_size, int64_t layer, int threads) {
+  if (batch < 0 || seq < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_shim_write: negative size");
+  if (batch == 0 || seq == 0 || hkv == 0) return KVECC_OK;
+  if (d < 1) return set_error(KVECC_EINVAL, "cpu_shim_write: empty rows");
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+    return set_error(KVECC_EINVAL, "cpu_shim_write: bad codec %d", codec);
+  if (x_dtype < KVECC_F32 || x_dtype > KVECC_BF16)
+    return set_error(KVECC_EINVAL, "cpu_shim_write: bad dtype %d", x_dtype);
+  if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
+    return set_error(KVECC_EINVAL, "cpu_shim_write: bad cache geometry");
+  if (!k || !v || !k_cache || !v_cache || !k_scales || !v_scales || !block_table)
+    return set_error(KVECC_EINVAL, "cpu_shim_write: null pointer");
+  const bool golay = codec == KVECC_CODEC_GOLAY;
+  const int64_t g = golay ? (d + 2) / 3 : d;
+  const uint32_t rowmul = (uint32_t)((uint64_t)g * (uint64_t)n_bits);
+  const uint32_t thr = kvecc_ber_threshold(ber);
+  const bool inj = inject != 0 && ber > 0.0f;
+  const int nb = golay ? (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits))
+                       : (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits));
+  const int64_t per_side = seq * hkv;
+  parallel_for(2 * per_side, threads, 1, [&](int64_t b, int64_t e, int) {
+    std::vector<uint8_t> nib(3 * g + 3);
+    for (int64_t item = b; item < e; ++item) {
+      const int side = (int)(item / per_side);
+      const int64_t rr = item - side * per_side;
+      const int64_t pos = rr / hkv, h = rr - pos * hkv;
+      const int64_t r = (batch - 1) * per_side + rr;
+      const uint32_t key0 = ((uint32_t)(uint64_t)seed0 + (uint32_t)r + (uint32_t)side) * rowmul;
+      const int64_t slot =
+          (((int64_t)block_table[pos / block_size] * num_layers + layer) * hkv + h) * block_size +
+          pos % block_size;
+      const void *x = side ? v : k;
+      float amax = 0.0f;
+      for (int64_t j = 0; j < d; ++j) amax = std::max(amax, std::fabs(load_x(x, x_dtype, r * d + j)));
+      const float scale = row_scale(amax);
+      (side ? v_scales : k_scales)[slot] = scale;
+      if (!golay) {
+        uint8_t *c = reinterpret_cast<uint8_t *>(side ? v_cache : k_cache) + slot * g;
+        for (int64_t j = 0; j < d; ++j) {
+          uint32_t cw = encode_nibble(quantize_nibble(load_x(x, x_dtype, r * d + j), scale), codec);
+          if (inj) cw ^= philox_flip_mask<-1>(key0 + (uint32_t)j * (uint32_t)n_bits, (uint32_t)j, thr, nb);
+          c[j] = (uint8_t)cw;
+        }
+      } else {
+        std::fill(nib.begin(), nib.end(), 0);
+        for (int64_t j = 0; j < d; ++j) nib[j] = (uint8_t)quantize_nibble(load_x(x, x_dtype, r * d + j), scale);
+        int32_t *c = reinterpret_cast<int32_t *>(side ? v_cache : k_cache) + slot * g;
+        for (int64_t q = 0; q < g; ++q) {
+          const uint32_t dw = golay_pack(nib[3 * q], nib[3 * q + 1], nib[3 * q + 2]);
+          uint32_t cw = dw | golay_parity12(dw) << 12;
+          if (inj) cw ^= philox_flip_mask<-1>(key0 + (uint32_t)q * (uint32_t)n_bits, (uint32_t)q, thr, nb);
+          c[q] = (int32_t)cw;
+        }
+      }
+    }
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,
+                                  const float *v_scales, const int32_t *block_table, int64_t ctx,
+                                  int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
+                                  int64_t layer, int codec, int interp, void *k_out, void *v_out,
+                                  int out_dtype, uint64_t *stats, int threads) {
+  if (ctx < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_shim_read: negative size");
+  if (ctx == 0 || hkv == 0 || d == 0) return KVECC_OK;
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+    return set_error(KVECC_EINVAL, "cpu_shim_read: bad codec %d", codec);
+  if (interp && codec != KVECC_CODEC_H84)
+    return set_error(KVECC_EINVAL, "cpu_shim_read: interpolation needs the hamming84 codec");
+  if (out_dtype < KVECC_F32 || out_dtype > KVECC_BF16)
+    return set_error(KVECC_EINVAL, "cpu_shim_read: bad dtype %d", out_dtype);
+  if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
+    return set_error(KVECC_EINVAL, "cpu_shim_read: bad cache geometry");
+  if (!k_cache || !v_cache || !k_scales || !v_scales || !block_table || !k_out || !v_out)
+    return set_error(KVECC_EINVAL, "cpu_shim_read: null pointer");
+  static uint16_t tab[8192];
+  static bool ready = [] {
+    build_golay_parity_table(tab);
+    build_golay_correct_table(tab + 4096);
+    return true;
+  }();
+  (void)ready;
+  const bool golay = codec == KVECC_CODEC_GOLAY;
+  const int64_t g = golay ? (d + 2) / 3 : d;
+  auto slot_of = [&](int64_t l, int64_t h) {
+    return (((int64_t)block_table[l / block_size] * num_layers + layer) * hkv + h) * block_size +
+           l % block_size;
+  };
+  const int64_t per_side = hkv * ctx;
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, 2 * per_side, 1)));
+  parallel_for(2 * per_side, threads, 1, [&](int64_t b, int64_t e, int t) {
+    uint32_t n1 = 0, n2 = 0;
+    uint64_t bits = 0, unc = 0;
+    for (int64_t item = b; item < e; ++item) {
+      const int side = (int)(item / per_side);
+      const int64_t hl = item - side * per_side;
+      const int64_t h = hl / ctx, l = hl % ctx;
+      const int64_t slot = slot_of(l, h);
+      const float s = (side ? v_scales : k_scales)[slot];
+      void *out = side ? v_out : k_out;
+      const int64_t o = (h * ctx + l) * d;
+      if (golay) {
+        const int32_t *c = reinterpret_cast<const int32_t *>(side ? v_cache : k_cache) + slot * g;
+        for (int64_t q = 0; q < g; ++q) {
+          uint32_t cnt;
+          const uint32_t dw = golay_decode1((uint32_t)c[q], tab, tab + 4096, cnt);
+          bits += cnt & 3u;
+          unc += cnt >> 2;
+          for (int64_t u = 0; u < 3 && 3 * q + u < d; ++u)
+            store_y(out, out_dtype, o + 3 * q + u, ((float)(dw >> (4 * u) & 0xFu) - 8.0f) * s);
+        }
+        continue;
+      }
+      const uint8_t *base = reinterpret_cast<const uint8_t *>(side ? v_cache : k_cache);
+      const uint8_t *c = base + slot * d;
+      const uint8_t *cl = base + slot_of(l > 0 ? l - 1 : 0, h) * d;
+      const uint8_t *cr = base + slot_of(l + 1 < ctx ? l + 1 : ctx - 1, h) * d;
+      for (int64_t j = 0; j < d; ++j) {
+        uint32_t q = c[j], type = 0;
+        if (codec == KVECC_CODEC_H84) {
+          h84_decode4(c[j], q, type, n1, n2);
+          if (interp) {
+            uint32_t ql, qr, tt, u1 = 0, u2 = 0;
+            h84_decode4(cl[j], ql, tt, u1, u2);
+            h84_decode4(cr[j], qr, tt, u1, u2);
+            q = interp_word(q, ql, qr, type) & 0xFFu;
+          }
+        } else if (codec == KVECC_CODEC_H74) {
+          h74_decode4(c[j], q, type, n1);
+        }
+        store_y(out, out_dtype, o + j, ((float)q - 8.0f) * s);
+      }
+    }
+    acc[t].a += golay ? bits : n1;
+    acc[t].b += golay ? unc : n2;
   });
   add_stats(stats, acc, 2);
   return KVECC_OK;

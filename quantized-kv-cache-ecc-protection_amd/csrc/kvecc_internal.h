@@ -1,6 +1,8 @@
 // kvecc_internal.h -- shared device/host helpers for the gfx950 codec kernels.
 #pragma once
 
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -48,6 +50,30 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int per_cu = 8) {
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
 // ---- device helpers ----------------------------------------------------------
+
+// element conversions of the fused kernels (fp32 / fp16 / bf16, RNE on the way out)
+template <typename T>
+__device__ __forceinline__ float to_f32(T v);
+template <>
+__device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ float to_f32<__half>(__half v) { return __half2float(v); }
+template <>
+__device__ __forceinline__ float to_f32<__hip_bfloat16>(__hip_bfloat16 v) {
+  return __bfloat162float(v);
+}
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float v);
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ __half from_f32<__half>(float v) { return __float2half_rn(v); }
+template <>
+__device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) {
+  return __float2bfloat16(v);
+}
+
 
 // wave-wide sum (all 64 lanes participate)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {

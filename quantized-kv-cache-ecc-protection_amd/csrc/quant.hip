@@ -12,34 +12,11 @@
 // per load), so a wave processes 64 / LPR rows at once and the absmax is a
 // short __shfl_xor butterfly inside the row's lane group.  Loads are 16 B per
 // lane, the 8-bit codewords leave as VEC-byte stores.
-#include <hip/hip_bf16.h>
-#include <hip/hip_fp16.h>
-
 #include "kvecc_internal.h"
 
 namespace kvecc {
 
-template <typename T>
-__device__ __forceinline__ float to_f32(T v);
-template <>
-__device__ __forceinline__ float to_f32<float>(float v) { return v; }
-template <>
-__device__ __forceinline__ float to_f32<__half>(__half v) { return __half2float(v); }
-template <>
-__device__ __forceinline__ float to_f32<__hip_bfloat16>(__hip_bfloat16 v) {
-  return __bfloat162float(v);
-}
-
-template <typename T>
-__device__ __forceinline__ T from_f32(float v);
-template <>
-__device__ __forceinline__ float from_f32<float>(float v) { return v; }
-template <>
-__device__ __forceinline__ __half from_f32<__half>(float v) { return __float2half_rn(v); }
-template <>
-__device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) {
-  return __float2bfloat16(v);
-}
+// to_f32 / from_f32: kvecc_internal.h
 
 // single-value encoder: codec_math.h encode_nibble (KVECC_CODEC_* codes)
 __device__ __forceinline__ uint32_t enc_nibble(uint32_t v, int codec) { return encode_nibble(v, codec); }

@@ -1,0 +1,350 @@
+// shim.hip -- the ECC shim's KV-cache write and read as one launch each.
+//
+// Reference: kv_cache/ecc_shim.py.  Write (:557-721): per (batch, pos, head)
+// row, quantize (absmax/7, torch round-half-even), encode, inject with the
+// row's own seed (K: seed0 + r, V: seed0 + r + 1, r = the row's running index)
+// and store into the paged cache; every batch writes the same seq_id slots, so
+// only the last batch's rows survive (:626-637).  Read (:990-1071): gather the
+// context's codewords, decode (stats += corrected / detected), optionally
+// interpolate H(8,4) double errors along the context axis, dequantize
+// ((q - 8) * scale) and hand K/V to attention.
+//
+// The reference runs these as Python loops issuing per-row Triton launches;
+// here the write is one launch (a wave per surviving row of K or V, the row's
+// absmax is a wave reduction, Golay triplets go through LDS) and the read is
+// one launch (a lane per 4 codewords of a row, neighbours re-decoded for
+// interpolation, output written head-major [Hkv, ctx, D] in the attention
+// dtype so it feeds SDPA without a permute copy).
+//
+// Cache layout (SimpleBlockManager): codewords [blocks, layers, Hkv, bs, P]
+// with P = D (uint8) or ceil(D/3) (int32 Golay); scales fp32 [blocks, layers,
+// Hkv, bs]; logical block b of the sequence is physical block table[b].
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+constexpr int kMaxShimD = 512;  // a lane holds <= 8 elements of a row
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+struct ShimGeom {
+  const int32_t *table;
+  int64_t hkv, d, g;  // g = codewords per token row: d, or ceil(d/3) for Golay
+  int64_t layers, bs, layer;
+  __device__ __forceinline__ int64_t slot(int64_t pos, int64_t h) const {
+    const int64_t blk = table[pos / bs];
+    return ((blk * layers + layer) * hkv + h) * bs + pos % bs;
+  }
+};
+
+struct ShimWriteArgs {
+  ShimGeom geo;
+  const void *x[2];  // K, V: [batch, seq, hkv * d], contiguous
+  void *cache[2];
+  float *scales[2];
+  int64_t batch, seq;
+  uint32_t seed0, rowmul, nbits, thr;
+  int nb_eff, inject;
+};
+
+// one wave per (side, pos, head) row of the last batch
+template <typename T, int CODEC, int NB>
+__global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
+  __shared__ uint8_t nib[kWavesPerBlock][kMaxShimD + 4];
+  const ShimGeom &geo = a.geo;
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int64_t per_side = a.seq * geo.hkv;
+  const int64_t item = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  const bool live = item < 2 * per_side;
+  const int side = live ? (int)(item / per_side) : 0;
+  const int64_t rr = live ? item - side * per_side : 0;
+  const int64_t pos = rr / geo.hkv, h = rr - pos * geo.hkv;
+  const int64_t r = (a.batch - 1) * per_side + rr;  // running row index of the write
+  const uint32_t key0 = (a.seed0 + (uint32_t)r + (uint32_t)side) * a.rowmul;
+  const int64_t slot = live ? geo.slot(pos, h) : 0;
+
+  constexpr int kPer = kMaxShimD / kWave;
+  float v[kPer];
+  float amax = 0.0f;
+  if (live) {
+    const T *x = reinterpret_cast<const T *>(a.x[side]) + r * geo.d;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int64_t e = lane + (int64_t)i * kWave;
+      v[i] = e < geo.d ? to_f32<T>(x[e]) : 0.0f;
+      amax = fmaxf(amax, fabsf(v[i]));
+    }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, kWave));
+  const float scale = row_scale(amax);
+  if (live && lane == 0) a.scales[side][slot] = scale;
+
+  if (CODEC != KVECC_CODEC_GOLAY) {
+    if (!live) return;
+    uint8_t *c = reinterpret_cast<uint8_t *>(a.cache[side]) + slot * geo.g;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t e = lane + i * kWave;
+      if (e < geo.d) {
+        uint32_t cw = encode_nibble(quantize_nibble(v[i], scale), CODEC);
+        if (a.inject) cw ^= philox_flip_mask<NB>(key0 + e * a.nbits, e, a.thr, a.nb_eff);
+        c[e] = (uint8_t)cw;
+      }
+    }
+    return;
+  }
+  // Golay: the row's nibbles go through LDS, then one lane per codeword of 3
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int64_t e = lane + (int64_t)i * kWave;
+      if (e < geo.d) nib[w][e] = (uint8_t)quantize_nibble(v[i], scale);
+    }
+    if (lane < 3 * geo.g - geo.d) nib[w][geo.d + lane] = 0;  // per-head zero padding
+  }
+  __syncthreads();
+  if (!live) return;
+  int32_t *c = reinterpret_cast<int32_t *>(a.cache[side]) + slot * geo.g;
+  for (int64_t k = lane; k < geo.g; k += kWave) {
+    const uint32_t dw = golay_pack(nib[w][3 * k], nib[w][3 * k + 1], nib[w][3 * k + 2]);
+    uint32_t cw = dw | golay_parity12(dw) << 12;
+    if (a.inject)
+      cw ^= philox_flip_mask<NB>(key0 + (uint32_t)k * a.nbits, (uint32_t)k, a.thr, a.nb_eff);
+    c[k] = (int32_t)cw;
+  }
+}
+
+struct ShimReadArgs {
+  ShimGeom geo;
+  const void *cache[2];
+  const float *scales[2];
+  void *out[2];  // [hkv, ctx, d]
+  int64_t ctx;
+  const uint16_t *par, *cor;  // Golay tables
+  uint64_t *stats;
+};
+
+template <typename TO>
+__device__ __forceinline__ void dequant4(TO *o, uint32_t q, float s) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[k] = from_f32<TO>(((float)(q >> (8 * k) & 0xFFu) - 8.0f) * s);
+}
+
+__device__ __forceinline__ uint32_t ld_word(const uint8_t *base, int64_t slot, int64_t d, int64_t c) {
+  return *reinterpret_cast<const uint32_t *>(base + slot * d + 4 * c);
+}
+
+// byte codecs (raw INT4, H(7,4), H(8,4)): one lane per 4 codewords (d % 4 == 0)
+template <typename TO, int CODEC, bool INTERP, bool STATS>
+__global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a) {
+  const ShimGeom &geo = a.geo;
+  const int64_t c4 = geo.d / 4;
+  const int64_t per_side = geo.hkv * a.ctx * c4;
+  uint32_t n1 = 0, n2 = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < 2 * per_side;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int side = (int)(i / per_side);
+    const int64_t t = i - side * per_side;
+    const int64_t c = t % c4, hl = t / c4;
+    const int64_t l = hl % a.ctx, h = hl / a.ctx;
+    const uint8_t *base = reinterpret_cast<const uint8_t *>(a.cache[side]);
+    const int64_t slot = geo.slot(l, h);
+    const uint32_t w = ld_word(base, slot, geo.d, c);
+    uint32_t q = w, type;
+    if (CODEC == KVECC_CODEC_H84) {
+      h84_decode4(w, q, type, n1, n2);
+      if (INTERP) {  // neighbours are the decoded (not interpolated) values
+        const int64_t lp = l > 0 ? l - 1 : 0, ln = l + 1 < a.ctx ? l + 1 : a.ctx - 1;
+        uint32_t ql, qr, tt, u1 = 0, u2 = 0;
+        h84_decode4(ld_word(base, geo.slot(lp, h), geo.d, c), ql, tt, u1, u2);
+        h84_decode4(ld_word(base, geo.slot(ln, h), geo.d, c), qr, tt, u1, u2);
+        q = interp_word(q, ql, qr, type);
+      }
+    } else if (CODEC == KVECC_CODEC_H74) {
+      h74_decode4(w, q, type, n1);
+    }
+    dequant4(reinterpret_cast<TO *>(a.out[side]) + (h * a.ctx + l) * geo.d + 4 * c, q,
+             a.scales[side][slot]);
+  }
+  if (STATS) flush_stats2(a.stats, n1, n2);
+}
+
+// Golay: one lane per codeword of a token row
+template <typename TO, bool STATS>
+__global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a) {
+  const ShimGeom &geo = a.geo;
+  const int64_t per_side = geo.hkv * a.ctx * geo.g;
+  uint32_t bits = 0, unc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < 2 * per_side;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int side = (int)(i / per_side);
+    const int64_t t = i - side * per_side;
+    const int64_t k = t % geo.g, hl = t / geo.g;
+    const int64_t l = hl % a.ctx, h = hl / a.ctx;
+    const int64_t slot = geo.slot(l, h);
+    const uint32_t w = (uint32_t)reinterpret_cast<const int32_t *>(a.cache[side])[slot * geo.g + k];
+    uint32_t cnt;
+    const uint32_t dw = golay_decode1(w, a.par, a.cor, cnt);
+    bits += cnt & 3u;
+    unc += cnt >> 2;
+    const float s = a.scales[side][slot];
+    TO *o = reinterpret_cast<TO *>(a.out[side]) + (h * a.ctx + l) * geo.d + 3 * k;
+    const int64_t left = geo.d - 3 * k;
+    o[0] = from_f32<TO>(((float)(dw & 0xFu) - 8.0f) * s);
+    if (left > 1) o[1] = from_f32<TO>(((float)(dw >> 4 & 0xFu) - 8.0f) * s);
+    if (left > 2) o[2] = from_f32<TO>(((float)(dw >> 8) - 8.0f) * s);
+  }
+  if (STATS) flush_stats2(a.stats, bits, unc);
+}
+
+template <typename T, int CODEC>
+static void launch_write_nb(const ShimWriteArgs &a, unsigned grid, hipStream_t st) {
+  constexpr int NB = CODEC == KVECC_CODEC_GOLAY ? 24
+                     : CODEC == KVECC_CODEC_H84 ? 8
+                     : CODEC == KVECC_CODEC_H74 ? 7
+                                                : 4;
+  if (a.nb_eff == NB)
+    hipLaunchKernelGGL((shim_write_kernel<T, CODEC, NB>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((shim_write_kernel<T, CODEC, -1>), dim3(grid), dim3(kBlock), 0, st, a);
+}
+
+template <typename T>
+static void launch_write(int codec, const ShimWriteArgs &a, unsigned grid, hipStream_t st) {
+  switch (codec) {
+    case KVECC_CODEC_NONE: launch_write_nb<T, KVECC_CODEC_NONE>(a, grid, st); break;
+    case KVECC_CODEC_H74: launch_write_nb<T, KVECC_CODEC_H74>(a, grid, st); break;
+    case KVECC_CODEC_H84: launch_write_nb<T, KVECC_CODEC_H84>(a, grid, st); break;
+    default: launch_write_nb<T, KVECC_CODEC_GOLAY>(a, grid, st); break;
+  }
+}
+
+template <typename TO, int CODEC, bool INTERP>
+static void launch_read_bytes(const ShimReadArgs &a, unsigned grid, hipStream_t st) {
+  if (a.stats)
+    hipLaunchKernelGGL((shim_read_bytes_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((shim_read_bytes_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kBlock), 0, st, a);
+}
+
+template <typename TO>
+static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_t st) {
+  if (codec == KVECC_CODEC_GOLAY) {
+    const unsigned grid = grid_for(2 * a.geo.hkv * a.ctx * a.geo.g, kBlock);
+    if (a.stats)
+      hipLaunchKernelGGL((shim_read_golay_kernel<TO, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    else
+      hipLaunchKernelGGL((shim_read_golay_kernel<TO, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    return;
+  }
+  const unsigned grid = grid_for(2 * a.geo.hkv * a.ctx * (a.geo.d / 4), kBlock);
+  if (codec == KVECC_CODEC_H84) {
+    if (interp)
+      launch_read_bytes<TO, KVECC_CODEC_H84, true>(a, grid, st);
+    else
+      launch_read_bytes<TO, KVECC_CODEC_H84, false>(a, grid, st);
+  } else if (codec == KVECC_CODEC_H74) {
+    launch_read_bytes<TO, KVECC_CODEC_H74, false>(a, grid, st);
+  } else {
+    launch_read_bytes<TO, KVECC_CODEC_NONE, false>(a, grid, st);
+  }
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
+                               int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
+                               int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
+                               float *k_scales, float *v_scales, const int32_t *block_table,
+                               int64_t num_layers, int64_t block_size, int64_t layer,
+                               void *stream) {
+  if (batch < 0 || seq < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_write: negative size");
+  if (batch == 0 || seq == 0 || hkv == 0) return KVECC_OK;
+  if (d < 1 || d > kMaxShimD) return set_error(KVECC_EINVAL, "shim_write: head_dim %lld not in [1, %d]", (long long)d, kMaxShimD);
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+    return set_error(KVECC_EINVAL, "shim_write: bad codec %d", codec);
+  if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
+    return set_error(KVECC_EINVAL, "shim_write: bad cache geometry");
+  if (!k || !v || !k_cache || !v_cache || !k_scales || !v_scales || !block_table)
+    return set_error(KVECC_EINVAL, "shim_write: null pointer");
+  ShimWriteArgs a;
+  a.geo = {block_table, hkv, d, codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d, num_layers,
+           block_size, layer};
+  a.x[0] = k;
+  a.x[1] = v;
+  a.cache[0] = k_cache;
+  a.cache[1] = v_cache;
+  a.scales[0] = k_scales;
+  a.scales[1] = v_scales;
+  a.batch = batch;
+  a.seq = seq;
+  a.seed0 = (uint32_t)(uint64_t)seed0;
+  a.rowmul = (uint32_t)((uint64_t)a.geo.g * (uint64_t)n_bits);
+  a.nbits = (uint32_t)n_bits;
+  a.thr = kvecc_ber_threshold(ber);
+  a.inject = inject != 0 && ber > 0.0f;
+  // same bit-count clamps as the flat kernels (uint8 caches draw >= 1, <= 8 bits)
+  a.nb_eff = codec == KVECC_CODEC_GOLAY ? (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits))
+                                        : (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits));
+  const int64_t waves = 2 * seq * hkv;
+  const int64_t blocks = cdiv(waves, kWavesPerBlock);
+  if (blocks > 0x7FFFFFFF) return set_error(KVECC_EINVAL, "shim_write: too many rows");
+  hipStream_t st = as_stream(stream);
+  switch (x_dtype) {
+    case KVECC_F32: launch_write<float>(codec, a, (unsigned)blocks, st); break;
+    case KVECC_F16: launch_write<__half>(codec, a, (unsigned)blocks, st); break;
+    case KVECC_BF16: launch_write<__hip_bfloat16>(codec, a, (unsigned)blocks, st); break;
+    default: return set_error(KVECC_EINVAL, "shim_write: bad dtype %d", x_dtype);
+  }
+  return check_launch("shim_write");
+}
+
+KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,
+                              const float *v_scales, const int32_t *block_table, int64_t ctx,
+                              int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
+                              int64_t layer, int codec, int interp, void *k_out, void *v_out,
+                              int out_dtype, uint64_t *stats, void *stream) {
+  if (ctx < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_read: negative size");
+  if (ctx == 0 || hkv == 0 || d == 0) return KVECC_OK;
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+    return set_error(KVECC_EINVAL, "shim_read: bad codec %d", codec);
+  if (codec != KVECC_CODEC_GOLAY && d % 4 != 0)
+    return set_error(KVECC_EINVAL, "shim_read: head_dim %lld must be a multiple of 4", (long long)d);
+  if (interp && codec != KVECC_CODEC_H84)
+    return set_error(KVECC_EINVAL, "shim_read: interpolation needs the hamming84 codec");
+  if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
+    return set_error(KVECC_EINVAL, "shim_read: bad cache geometry");
+  if (!k_cache || !v_cache || !k_scales || !v_scales || !block_table || !k_out || !v_out)
+    return set_error(KVECC_EINVAL, "shim_read: null pointer");
+  ShimReadArgs a;
+  a.geo = {block_table, hkv, d, codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d, num_layers,
+           block_size, layer};
+  a.cache[0] = k_cache;
+  a.cache[1] = v_cache;
+  a.scales[0] = k_scales;
+  a.scales[1] = v_scales;
+  a.out[0] = k_out;
+  a.out[1] = v_out;
+  a.ctx = ctx;
+  a.stats = stats;
+  a.par = a.cor = nullptr;
+  if (codec == KVECC_CODEC_GOLAY) {
+    a.par = golay_parity_table_dev();
+    a.cor = golay_correct_table_dev();
+    if (!a.par || !a.cor) return KVECC_EHIP;
+  }
+  hipStream_t st = as_stream(stream);
+  switch (out_dtype) {
+    case KVECC_F32: launch_read<float>(codec, interp, a, st); break;
+    case KVECC_F16: launch_read<__half>(codec, interp, a, st); break;
+    case KVECC_BF16: launch_read<__hip_bfloat16>(codec, interp, a, st); break;
+    default: return set_error(KVECC_EINVAL, "shim_read: bad dtype %d", out_dtype);
+  }
+  return check_launch("shim_read");
+}
+
+}  // extern "C"

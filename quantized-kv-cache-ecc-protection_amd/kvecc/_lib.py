@@ -47,6 +47,8 @@ SIGNATURES = {
     "kvecc_any_equal_u8": [_vp, _i64, _u8, _vp, _vp],
     "kvecc_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _vp],
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
+    "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
     # host backend (threads instead of a stream)
     "kvecc_cpu_hamming74_encode": [_vp, _vp, _i64, _int],
     "kvecc_cpu_hamming84_encode": [_vp, _vp, _i64, _int],
@@ -65,6 +67,8 @@ SIGNATURES = {
     "kvecc_cpu_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _int],
     "kvecc_cpu_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _int],
     "kvecc_cpu_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _int],
+    "kvecc_cpu_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _int],
+    "kvecc_cpu_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _int],
 }
 _RESTYPE = {
     "kvecc_version": ctypes.c_char_p,
@@ -74,7 +78,7 @@ _RESTYPE = {
 
 # dtype / codec codes (include/kvecc.h)
 F32, F16, BF16 = 0, 1, 2
-CODEC_NONE, CODEC_H74, CODEC_H84 = 0, 1, 2
+CODEC_NONE, CODEC_H74, CODEC_H84, CODEC_GOLAY = 0, 1, 2, 3
 
 
 class KveccError(RuntimeError):

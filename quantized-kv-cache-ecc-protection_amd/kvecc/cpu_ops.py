@@ -426,3 +426,38 @@ def fused_decode_dequantize_hamming84(codewords, scales, output_dtype=torch.floa
     if output_dtype != dtype:
         out = out.to(output_dtype)
     return out, int(st[0])
+
+
+# ============================================================================
+# ECC shim: paged KV-cache write / read (host twins of ops.shim_write / shim_read)
+# ============================================================================
+
+SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84": _lib.CODEC_H84,
+               "golay": _lib.CODEC_GOLAY}
+
+
+def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0):
+    batch, seq, _ = k.shape
+    if k.dtype not in _DT or v.dtype != k.dtype:
+        raise TypeError(f"unsupported K/V dtype {k.dtype}/{v.dtype}")
+    _check_cpu(k)
+    k, v = k.contiguous(), v.contiguous()
+    table = manager.block_table[seq_id]
+    _lib.call("kvecc_cpu_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq,
+              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec], int(n_bits),
+              int(bool(inject)), float(ber), int(seed0), _ptr(manager.k_cache),
+              _ptr(manager.v_cache), _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table),
+              manager.num_layers, manager.block_size, int(layer), NUM_THREADS)
+
+
+def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=0):
+    shape = (manager.num_kv_heads, ctx, manager.head_dim)
+    k_out = torch.empty(shape, dtype=out_dtype)
+    v_out = torch.empty(shape, dtype=out_dtype)
+    table = manager.block_table[seq_id]
+    _lib.call("kvecc_cpu_shim_read", _ptr(manager.k_cache), _ptr(manager.v_cache),
+              _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table), int(ctx),
+              manager.num_kv_heads, manager.head_dim, manager.num_layers, manager.block_size,
+              int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
+              _DT[out_dtype], _ptr(stats), NUM_THREADS)
+    return k_out, v_out

@@ -85,13 +85,16 @@ class ECCShimConfig:
     """Codec / BER / injection settings of the shim (ecc_shim.py:134-186).
 
     ``backend`` selects the codec implementation from kvecc.backends
-    (default "hip"; unknown names raise ValueError).
+    (default "hip"; unknown names raise ValueError).  ``fused`` runs the cache
+    write and read as one launch each (kvecc_shim_write / kvecc_shim_read);
+    False composes the per-op kernels (identical bits, kept for A/B tests).
     """
 
     SUPPORTED_CODECS = {"fp16", "fp8", "int4", "hamming74", "hamming84", "golay"}
 
     def __init__(self, codec="hamming84", ber=0.0, block_size=16, num_blocks=256,
-                 inject_errors=False, seed=42, use_interpolation=False, backend="hip"):
+                 inject_errors=False, seed=42, use_interpolation=False, backend="hip",
+                 fused=True):
         if codec not in self.SUPPORTED_CODECS:
             raise ValueError(f"Unsupported codec: '{codec}'. "
                              f"Supported codecs: {sorted(self.SUPPORTED_CODECS)}")
@@ -103,6 +106,7 @@ class ECCShimConfig:
         self.seed = seed
         self.use_interpolation = use_interpolation
         self.backend = backend
+        self.fused = fused  # one-launch cache write / read (False: per-op kernels)
 
 
 class SimpleBlockManager:
@@ -205,10 +209,15 @@ class ECCBackend:
     row), last-batch-wins cache writes, statistics semantics per codec.
     """
 
-    def __init__(self, manager, config, num_heads):
+    # codecs whose write / read run as one fused launch each (shim.hip)
+    FUSED_CODECS = ("int4", "hamming74", "hamming84", "golay")
+
+    def __init__(self, manager, config, num_heads, fused=None):
         self.manager = manager
         self.config = config
         self.codec_backend = get_codec_backend(getattr(config, "backend", "hip"))
+        # fused=False composes the per-op kernels instead (same bits; A/B tests)
+        self.fused = getattr(config, "fused", True) if fused is None else fused
         self.num_heads = num_heads
         self.num_kv_heads = manager.num_kv_heads
         self.head_dim = manager.head_dim
@@ -249,6 +258,12 @@ class ECCBackend:
         rows = batch * seq_len * hk
         inject = cfg.inject_errors and cfg.ber > 0
         seed0 = cfg.seed + self._injection_count
+        if self._fused_ok(k) and k.dtype == v.dtype:
+            self.codec_backend.shim_write(k, v, mgr, layer_idx, cfg.codec, _N_BITS[cfg.codec],
+                                          inject, cfg.ber, seed0, seq_id)
+            if inject:
+                self._injection_count += rows
+            return
         kr = k.reshape(batch, seq_len, hk, d)
         vr = v.reshape(batch, seq_len, hk, d)
         codec = cfg.codec
@@ -283,6 +298,18 @@ class ECCBackend:
         if inject:
             self._injection_count += rows
 
+    def _fused_ok(self, x=None):
+        if not self.fused or self.config.codec not in self.FUSED_CODECS:
+            return False
+        if not hasattr(self.codec_backend, "shim_write"):
+            return False
+        d = self.head_dim
+        if self.config.codec != "golay" and d % 4:
+            return False
+        if d > 512:
+            return False
+        return x is None or x.dtype in (torch.float32, torch.float16, torch.bfloat16)
+
     def _gather(self, cache, blk, slot, layer_idx):
         return self.manager.view5(cache)[blk, layer_idx, :, slot, :]  # [ctx, heads, per_token]
 
@@ -316,9 +343,18 @@ class ECCBackend:
         ctx = mgr.get_context_len(seq_id)
         if ctx == 0:
             return torch.zeros_like(q)
-        blk, slot = mgr.slots(seq_id, ctx)
         q_len = q.shape[2]
         fast = cfg.codec == "hamming84" and not cfg.use_interpolation and q_len == 1
+        if self._fused_ok():
+            # the reference's seq_len==1 Triton path (ecc_shim.py:791-800) keeps no statistics
+            interp = cfg.use_interpolation and cfg.codec == "hamming84"
+            k_t, v_t = self.codec_backend.shim_read(
+                mgr, layer_idx, ctx, cfg.codec, interp, torch.float32 if fast else q.dtype,
+                None if fast else self._stats, seq_id)
+            if fast:
+                return self._decode_step_attention(q, k_t, v_t)
+            return self._run_attention_hd(q, k_t, v_t)
+        blk, slot = mgr.slots(seq_id, ctx)
         k_enc = self._gather(mgr.k_cache, blk, slot, layer_idx)
         v_enc = self._gather(mgr.v_cache, blk, slot, layer_idx)
         if cfg.codec == "fp16":
@@ -334,23 +370,31 @@ class ECCBackend:
         k_f = (k_dec.float() - 8.0) * k_sc.unsqueeze(-1)
         v_f = (v_dec.float() - 8.0) * v_sc.unsqueeze(-1)
         if fast:
-            return self._decode_step_attention(q, k_f, v_f)
+            return self._decode_step_attention(q, k_f.transpose(0, 1), v_f.transpose(0, 1))
         return self._run_attention(q, k_f, v_f)
 
     def _decode_step_attention(self, q, k_f, v_f):
         """seq_len==1 path of paged_attention_ecc (attention_ecc.py:264-427): fp32
-        softmax over the context, output in q's dtype.  Query head h reads cache
-        head h // groups (the reference indexes cache head h directly, which only
-        agrees without GQA)."""
+        softmax over the context, output in q's dtype.  K/V are head-major
+        [Hkv, ctx, D]; query head h reads cache head h // groups (the reference
+        indexes cache head h directly, which only agrees without GQA)."""
         if self.num_kv_groups > 1:
-            k_f = k_f.repeat_interleave(self.num_kv_groups, dim=1)
-            v_f = v_f.repeat_interleave(self.num_kv_groups, dim=1)
+            k_f = k_f.repeat_interleave(self.num_kv_groups, dim=0)
+            v_f = v_f.repeat_interleave(self.num_kv_groups, dim=0)
         scale = 1.0 / math.sqrt(self.head_dim)
         qf = q[:, :, 0, :].float()                                # [B, H, D]
-        scores = torch.einsum("bhd,thd->bht", qf, k_f) * scale     # [B, H, ctx]
+        scores = torch.einsum("bhd,htd->bht", qf, k_f) * scale     # [B, H, ctx]
         w = torch.softmax(scores, dim=-1)
-        out = torch.einsum("bht,thd->bhd", w, v_f)
+        out = torch.einsum("bht,htd->bhd", w, v_f)
         return out.to(q.dtype).unsqueeze(2)
+
+    def _run_attention_hd(self, q, k, v):
+        """_run_attention on head-major K/V [Hkv, ctx, D] already in q's dtype."""
+        if self.num_kv_groups > 1:
+            k = k.repeat_interleave(self.num_kv_groups, dim=0)
+            v = v.repeat_interleave(self.num_kv_groups, dim=0)
+        return F.scaled_dot_product_attention(q, k.unsqueeze(0), v.unsqueeze(0),
+                                              is_causal=q.shape[2] > 1)
 
     def _run_attention(self, q, k_float, v_float, device=None):
         """GQA expand + SDPA, causal for prefill (ecc_shim.py:1138-1164)."""

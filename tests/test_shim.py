@@ -128,3 +128,50 @@ def test_shim_cache_bits_match_oracle(gpu):
 
 def test_shim_cache_bits_match_oracle_cpu_backend():
     _cache_bits_match_oracle(torch.device("cpu"), "cpu")
+
+
+def _fused_equals_composed(device, backend):
+    """The one-launch write/read (shim.hip / its host twin) leaves the same cache
+    bits and scales, returns the same attention output and counts the same
+    statistics as the per-op composition, for every fused codec."""
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    torch.manual_seed(1)
+    cases = [("hamming84", True, 64, torch.float16), ("hamming84", False, 128, torch.float32),
+             ("hamming74", False, 64, torch.bfloat16), ("golay", False, 128, torch.float16),
+             ("golay", False, 100, torch.float32), ("int4", False, 64, torch.float16)]
+    for codec, interp, d, dt in cases:
+        b, s, hk, nh = 2, 37, 2, 4  # GQA: 2 query heads per cache head
+        res = []
+        for fused in (True, False):
+            cfg = ECCShimConfig(codec=codec, ber=0.02, inject_errors=True, seed=11,
+                                use_interpolation=interp, backend=backend)
+            mgr = SimpleBlockManager(6, 16, 3, hk, d, device=device, codec=codec)
+            be = ECCBackend(mgr, cfg, num_heads=nh, fused=fused)
+            g = torch.Generator().manual_seed(3)
+            k = torch.randn(b, s, hk * d, generator=g).to(device=device, dtype=dt)
+            v = torch.randn(b, s, hk * d, generator=g).to(device=device, dtype=dt)
+            q = torch.randn(b, nh, s, d, generator=g).to(device=device, dtype=dt)
+            be._injection_count = 9
+            be.write(k, v, layer_idx=2)
+            out = be.attend(q, layer_idx=2)
+            q1 = q[:, :, :1]
+            out1 = be.attend(q1, layer_idx=2)  # seq_len==1 path
+            res.append((mgr.k_cache.cpu(), mgr.v_cache.cpu(), mgr.k_scales.cpu(),
+                        mgr.v_scales.cpu(), out.float().cpu(), out1.float().cpu(),
+                        be._injection_count, be._errors_corrected, be._errors_detected))
+        f, c = res
+        for i in range(4):
+            assert torch.equal(f[i], c[i]), (codec, d, i)
+        assert f[6:] == c[6:], (codec, f[6:], c[6:])
+        assert codec == "int4" or f[7] > 0, codec  # errors were injected and corrected
+        assert torch.allclose(f[4], c[4], atol=1e-3, rtol=1e-3), codec
+        assert torch.allclose(f[5], c[5], atol=1e-3, rtol=1e-3), codec
+
+
+def test_fused_equals_composed_cpu_backend():
+    _fused_equals_composed(torch.device("cpu"), "cpu")
+
+
+@pytest.mark.gpu
+def test_fused_equals_composed(gpu):
+    _fused_equals_composed(gpu, "hip")

@@ -46,6 +46,10 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--composed", action="store_true",
+                    help="per-op kernels instead of the fused cache write/read")
+    ap.add_argument("--cpu-backend", action="store_true",
+                    help="also run the same forward on the host backend (fp32, CPU)")
     args = ap.parse_args()
     from transformers import GPT2Config, GPT2LMHeadModel
     from kvecc.ecc_shim import (ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention,
@@ -56,25 +60,47 @@ def main():
     ids = torch.randint(0, 50257, (1, args.seq), generator=torch.Generator().manual_seed(0)).to(dev)
     out = {"config": {"model": "gpt2 12L/12H/768 random-init fp16", "seq_len": args.seq,
                       "codec": args.codec, "use_interpolation": bool(args.interp),
-                      "block_size": 16, "seed": 42}, "runs": []}
+                      "block_size": 16, "seed": 42, "fused": not args.composed}, "runs": []}
     with torch.no_grad():
         med, mn = timed(lambda: model(ids), args.steps, args.warmup)
         out["unpatched_ms"] = med
         nblocks = (args.seq + 15) // 16
         for ber in args.bers:
             cfg = ECCShimConfig(codec=args.codec, ber=ber, inject_errors=ber > 0, seed=42,
-                                block_size=16, use_interpolation=bool(args.interp))
+                                block_size=16, use_interpolation=bool(args.interp),
+                                fused=not args.composed)
             with patch_model_with_ecc_attention(model, cfg, num_blocks=nblocks):
                 def fwd():
                     reset_ecc_cache(model)
                     return model(ids)
                 med, mn = timed(fwd, args.steps, args.warmup)
                 reset_ecc_cache(model)
-                logits = model(ids).logits
+                res = model(ids, labels=ids)
                 st = get_ecc_stats(model)
             out["runs"].append({"ber": ber, "forward_ms": med, "min_ms": mn,
                                 "tokens_per_s": args.seq / (med * 1e-3),
-                                "logits_finite": bool(torch.isfinite(logits).all()), "stats": st})
+                                "loss": float(res.loss),
+                                "logits_finite": bool(torch.isfinite(res.logits).all()),
+                                "stats": st})
+        if args.cpu_backend:
+            import time
+            cpu_model = GPT2LMHeadModel(GPT2Config(n_positions=1024)).eval()
+            cpu_model.load_state_dict({k: t.float().cpu() for k, t in model.state_dict().items()})
+            cpu_ids = ids.cpu()
+            out["cpu_backend"] = []
+            for ber in args.bers:
+                cfg = ECCShimConfig(codec=args.codec, ber=ber, inject_errors=ber > 0, seed=42,
+                                    block_size=16, use_interpolation=bool(args.interp),
+                                    backend="cpu")
+                with patch_model_with_ecc_attention(cpu_model, cfg, num_blocks=nblocks):
+                    reset_ecc_cache(cpu_model)
+                    t0 = time.perf_counter()
+                    res = cpu_model(cpu_ids, labels=cpu_ids)
+                    el = time.perf_counter() - t0
+                    st = get_ecc_stats(cpu_model)
+                out["cpu_backend"].append({"ber": ber, "forward_ms": el * 1e3, "loss": float(res.loss),
+                                           "dtype": "fp32", "threads": torch.get_num_threads(),
+                                           "stats": st})
     print(json.dumps(out))
 
 
