@@ -188,6 +188,27 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
                               int64_t layer, int codec, int interp, void *k_out, void *v_out,
                               int out_dtype, uint64_t *stats, void *stream);
 
+/* ---- Paged decode attention with inline ECC decode ---------------------------- */
+/* attention_ecc.py:620-780 (paged_attention_ecc) + :265-427 (kernel): one query
+ * token per sequence, query [batch, heads, head_dim] (q_dtype), caches as above
+ * (codec H84: uint8, double errors keep their data; GOLAY: int32, uncorrectable
+ * data kept), block_table [batch, max_blocks] int32 (-1 = no block, token
+ * skipped), context_lens [batch] int32 (<= max_context_len; <= 0 means
+ * max_blocks*block_size), out [batch, heads, head_dim] in q_dtype (0 for an empty
+ * context).  Query head h reads cache head h / (heads / kv_heads).  `workspace`:
+ * kvecc_paged_attention_workspace(...) floats.  head_dim <= 256. */
+KVECC_API int64_t kvecc_paged_attention_workspace(int64_t batch, int64_t heads, int64_t head_dim,
+                                                  int64_t max_context_len);
+KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *k_cache,
+                                    const void *v_cache, const int32_t *block_table,
+                                    const int32_t *context_lens, const float *k_scales,
+                                    const float *v_scales, void *out, int64_t batch,
+                                    int64_t heads, int64_t kv_heads, int64_t head_dim,
+                                    int64_t num_blocks, int64_t num_layers, int64_t layer, int64_t block_size,
+                                    int64_t max_blocks, int64_t max_context_len, float sm_scale,
+                                    int codec, float *workspace, int64_t workspace_floats,
+                                    void *stream);
+
 /* ---- Host ("cpu") backend ------------------------------------------------- */
 /* The reference has no CPU codec backend (every wrapper asserts x.is_cuda,
  * e.g. hamming74_triton.py:185,246, golay_triton.py:399,456); BASELINE config 1 asks
@@ -245,6 +266,14 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
                                   int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
                                   int64_t layer, int codec, int interp, void *k_out, void *v_out,
                                   int out_dtype, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const void *k_cache,
+                                        const void *v_cache, const int32_t *block_table,
+                                        const int32_t *context_lens, const float *k_scales,
+                                        const float *v_scales, void *out, int64_t batch,
+                                        int64_t heads, int64_t kv_heads, int64_t head_dim,
+                                        int64_t num_blocks, int64_t num_layers, int64_t layer, int64_t block_size,
+                                        int64_t max_blocks, int64_t max_context_len,
+                                        float sm_scale, int codec, int threads);
 
 #ifdef __cplusplus
 }

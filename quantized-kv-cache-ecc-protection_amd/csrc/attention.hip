@@ -1,0 +1,419 @@
+// attention.hip -- single-token (decode) paged attention over an ECC-protected
+// INT4 KV cache, decoding the codewords inline.
+//
+// Reference: kv_cache/attention_ecc.py:265-427 (paged_attention_ecc_kernel,
+// Hamming(8,4) with decode_hamming84_inline :56-149 -- double errors keep their
+// uncorrected data -- and dequantize_int4 :152-169) and the wrapper
+// paged_attention_ecc :620-780, which the shim calls for seq_len == 1
+// (ecc_shim.py:791-800,1091-1136).  Golay(24,12) goes through the Python
+// reference_attention_ecc there (:783-909); here it is a native kernel too.
+//
+// The reference runs one program per (batch, head) walking every context token
+// with an online softmax -- B*H programs, a few dozen on a 256-CU part.  This
+// is split-context ("flash-decoding"): workgroup (split, b*H + h) owns up to
+// 256 tokens (fewer when batch*heads is small, so the grid still fills the
+// chip), with the split's slice of the block table staged in LDS.  Lanes are
+// grouped W per token row (a lane owns 16 H(8,4) codewords via one 16-byte
+// load, or one Golay codeword); each group streams its rows in ONE pass --
+// kUnroll K and V rows loaded before any is used, the group's partial dot
+// products reduced with __shfl_xor, an online softmax per group -- and the
+// groups merge through LDS.  The split's (max, sum, acc[D]) go to a workspace
+// that a second small launch combines.  Query head h reads cache head
+// h / (H / Hkv) (the reference indexes cache head h, which only agrees without
+// GQA).  Numerics: fp32 throughout, expf; the result differs from the
+// reference's sequential online softmax only by fp32 summation order.
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+constexpr int kMaxSplit = 256;    // context tokens per workgroup (upper bound)
+constexpr int kMaxSplits = 1024;  // splits per (batch, head)
+constexpr int kAttnMaxD = 256;
+constexpr int kUnroll = 4;        // token rows in flight per lane group
+
+struct AttnArgs {
+  const void *q;  // [B, H, D]
+  const void *k_cache, *v_cache;
+  const int32_t *table;     // [B, max_blocks]
+  const int32_t *ctx_lens;  // [B]
+  const float *k_scales, *v_scales;
+  float *ws;  // [B*H, nsplit, D + 2]: m, l, acc[D]
+  void *out;  // [B, H, D]
+  int64_t heads, kv_heads, d, g;  // g = codewords per token row
+  int64_t layers, layer, bs, max_blocks, nsplit, split;
+  float sm_scale;
+  const uint16_t *par, *cor;  // Golay tables
+};
+
+// Lane chunk c of a token row: VEC 32-bit words = 4*VEC H(8,4) codewords, or
+// one Golay codeword; E values.
+template <int CODEC, int VEC>
+struct Chunk {
+  static constexpr int E = CODEC == KVECC_CODEC_H84 ? 4 * VEC : 3;
+  uint32_t w[VEC];
+  __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
+    if (CODEC == KVECC_CODEC_H84) {
+      const uint8_t *p = reinterpret_cast<const uint8_t *>(cache) + row * a.d + 4 * VEC * c;
+      if (VEC == 4) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(p);
+        w[0] = v.x;
+        w[VEC > 1 ? 1 : 0] = v.y;
+        w[VEC > 2 ? 2 : 0] = v.z;
+        w[VEC > 3 ? 3 : 0] = v.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) w[k] = reinterpret_cast<const uint32_t *>(p)[k];
+      }
+    } else {
+      w[0] = (uint32_t)reinterpret_cast<const int32_t *>(cache)[row * a.g + c];
+    }
+  }
+  // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
+  // data(byte) - 8; double errors keep their data, :144-148), Golay through the
+  // correction tables (uncorrectable words keep their data, as golay_decode)
+  __device__ __forceinline__ void decode(const AttnArgs &a, const float *lut, float *v) const {
+    if (CODEC == KVECC_CODEC_H84) {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * k + e] = lut[(w[k] >> (8 * e)) & 0xFFu];
+      }
+    } else {
+      uint32_t cnt;
+      const uint32_t dw = golay_decode1(w[0], a.par, a.cor, cnt);
+#pragma unroll
+      for (int e = 0; e < 3; ++e) v[e] = (float)(dw >> (4 * e) & 0xFu) - 8.0f;
+    }
+  }
+};
+
+template <typename T, int CODEC, int VEC, int W>
+__global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
+  using C = Chunk<CODEC, VEC>;
+  constexpr int E = C::E;
+  constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
+  // cache row of each token of the split (-1 = no block / past the split),
+  // padded so the unrolled loop reads it without bounds checks
+  __shared__ int32_t rows[kMaxSplit + (kUnroll - 1) * kBlock];
+  __shared__ float red[TP * W * E];        // per-group acc
+  __shared__ float gml[2][TP];             // per-group running max / sum
+  __shared__ float lut[256];               // H(8,4): codeword byte -> data - 8
+
+  const int64_t bh = blockIdx.y;
+  const int64_t b = bh / a.heads, h = bh % a.heads;
+  const int64_t hk = h / (a.heads / a.kv_heads);
+  const int grp = threadIdx.x / W, c = threadIdx.x % W;
+  const int64_t ctx = min<int64_t>(a.ctx_lens[b], a.max_blocks * a.bs);  // table bound
+  const int64_t t0 = (int64_t)blockIdx.x * a.split;
+  const int64_t t1 = min<int64_t>(t0 + a.split, ctx);
+  const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
+  const bool live = c < a.g / VEC;  // lanes past the row idle (Golay: g < W)
+  const int cs = live ? c : 0;
+  float *ws = a.ws + (bh * a.nsplit + blockIdx.x) * (a.d + 2);
+
+  {  // one 32-bit division per token, here; none in the streaming loop
+    const uint32_t bs = (uint32_t)a.bs;
+    const int32_t head_row0 = (int32_t)((a.layer * a.kv_heads + hk) * a.bs);
+    const int32_t blk_rows = (int32_t)(a.layers * a.kv_heads * a.bs);
+    const int32_t *tab = a.table + b * a.max_blocks;
+    for (int i = threadIdx.x; i < kMaxSplit + (kUnroll - 1) * kBlock; i += kBlock) {
+      int32_t row = -1;
+      if (i < ntok) {
+        const uint32_t pos = (uint32_t)(t0 + i);
+        const uint32_t lb = pos / bs;
+        const int32_t blk = tab[lb];
+        if (blk >= 0) row = blk * blk_rows + head_row0 + (int32_t)(pos - lb * bs);
+      }
+      rows[i] = row;
+    }
+  }
+  if (CODEC == KVECC_CODEC_H84 && threadIdx.x < 256) {
+    uint32_t q, t, n1 = 0, n2 = 0;
+    h84_decode4(threadIdx.x, q, t, n1, n2);
+    lut[threadIdx.x] = (float)(q & 0xFu) - 8.0f;
+  }
+  float qv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int64_t di = (int64_t)c * E + e;
+    qv[e] = (live && di < a.d)
+                ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h) * a.d + di]) * a.sm_scale
+                : 0.0f;
+  }
+  __syncthreads();
+
+  // ---- one pass: kUnroll K and V rows in flight per lane, online softmax per group
+  float m = -INFINITY, l = 0.0f, acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.0f;
+  for (int i0 = grp; i0 < ntok; i0 += TP * kUnroll) {
+    C kc[kUnroll], vc[kUnroll];
+    float ks[kUnroll], vs[kUnroll];
+    bool ok[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {  // branch-free: invalid rows read row 0, masked
+      const int32_t r = rows[i0 + u * TP];
+      ok[u] = r >= 0;
+      const int64_t row = ok[u] ? r : 0;
+      kc[u].load(a, a.k_cache, row, cs);
+      vc[u].load(a, a.v_cache, row, cs);
+      ks[u] = a.k_scales[row];
+      vs[u] = a.v_scales[row];
+    }
+    float sc[kUnroll];
+    float mn = m;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      float part = 0.0f;
+      if (live) {
+        float kv[E];
+        kc[u].decode(a, lut, kv);
+#pragma unroll
+        for (int e = 0; e < E; ++e) part += qv[e] * kv[e];
+        part *= ks[u];  // sum q (n - 8) s = s * sum q (n - 8)
+      }
+#pragma unroll
+      for (int off = W / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, W);
+      sc[u] = ok[u] ? part : -INFINITY;
+      mn = fmaxf(mn, sc[u]);
+    }
+    if (mn == -INFINITY) continue;  // no valid row yet (uniform per group)
+    const float alpha = expf(m - mn);  // m = -inf -> 0
+    l *= alpha;
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] *= alpha;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const float p = expf(sc[u] - mn);  // invalid rows: exp(-inf) = 0
+      l += p;
+      if (live) {
+        float vv[E];
+        vc[u].decode(a, lut, vv);
+        const float ps = p * vs[u];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] += ps * vv[e];
+      }
+    }
+    m = mn;
+  }
+
+  // ---- merge the TP groups ------------------------------------------------------
+  if (live) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) red[(grp * W + c) * E + e] = acc[e];
+  }
+  if (c == 0) {
+    gml[0][grp] = m;
+    gml[1][grp] = l;
+  }
+  __syncthreads();
+  __shared__ float gw[TP];  // e^(m_g - M) per group
+  float M = -INFINITY;
+  for (int gi = 0; gi < TP; ++gi) M = fmaxf(M, gml[0][gi]);
+  if (threadIdx.x < TP) {
+    const float mg = gml[0][threadIdx.x];
+    gw[threadIdx.x] = mg == -INFINITY ? 0.0f : expf(mg - M);
+  }
+  __syncthreads();
+  for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
+    float sum = 0.0f;
+    for (int gi = 0; gi < TP; ++gi) sum += red[gi * W * E + di] * gw[gi];
+    ws[2 + di] = sum;
+  }
+  if (threadIdx.x == 0) {
+    float L = 0.0f;
+    for (int gi = 0; gi < TP; ++gi) L += gml[1][gi] * gw[gi];
+    ws[0] = M;
+    ws[1] = L;
+  }
+}
+
+// combine the splits of one (b, h): out = sum_s acc_s e^(m_s - M) / sum_s l_s e^(m_s - M)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) {
+  __shared__ float wt[kMaxSplits];
+  __shared__ float bred[kBlock / kWave];
+  const int64_t bh = blockIdx.x;
+  const int64_t stride = a.d + 2;
+  const float *ws = a.ws + bh * a.nsplit * stride;
+  float mx = -INFINITY;
+  for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) mx = fmaxf(mx, ws[s * stride]);
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0) bred[threadIdx.x / kWave] = mx;
+  __syncthreads();
+  mx = bred[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / kWave; ++w) mx = fmaxf(mx, bred[w]);
+  __syncthreads();
+  float L = 0.0f;
+  for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) {
+    const float ms = ws[s * stride];
+    const float w = ms == -INFINITY ? 0.0f : expf(ms - mx);
+    wt[s] = w;
+    L += w * ws[s * stride + 1];
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) L += __shfl_xor(L, off, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) bred[threadIdx.x / kWave] = L;
+  __syncthreads();
+  L = 0.0f;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) L += bred[w];
+  T *out = reinterpret_cast<T *>(a.out) + bh * a.d;
+  for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int64_t s = 0; s < a.nsplit; ++s) acc += ws[s * stride + 2 + di] * wt[s];
+    out[di] = from_f32<T>(L > 0.0f ? acc / L : 0.0f);  // empty context -> 0 (:424)
+  }
+}
+
+static int pow2_at_least(int64_t x) {
+  int w = 1;
+  while (w < x) w <<= 1;
+  return w;
+}
+
+template <typename T, int CODEC, int VEC>
+static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
+  const int w = pow2_at_least(a.g / VEC);
+  switch (w) {
+#define KVECC_ATTN_CASE(WW)                                                                       \
+  case WW:                                                                                        \
+    hipLaunchKernelGGL((paged_attn_split_kernel<T, CODEC, VEC, WW>), grid, dim3(kBlock), 0, st, a); \
+    return KVECC_OK;
+    KVECC_ATTN_CASE(1)
+    KVECC_ATTN_CASE(2)
+    KVECC_ATTN_CASE(4)
+    KVECC_ATTN_CASE(8)
+    KVECC_ATTN_CASE(16)
+    KVECC_ATTN_CASE(32)
+    KVECC_ATTN_CASE(64)
+#undef KVECC_ATTN_CASE
+    default:
+      return set_error(KVECC_EINVAL, "paged_attention: %lld lane chunks per token row > 64",
+                       (long long)(a.g / VEC));
+  }
+}
+
+template <typename T, int CODEC>
+static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
+  dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads));
+  int rc;
+  if (CODEC == KVECC_CODEC_H84 && a.d % 16 == 0)
+    rc = launch_split<T, CODEC, 4>(a, grid, st);  // 16-byte loads, 16 codewords per lane
+  else
+    rc = launch_split<T, CODEC, 1>(a, grid, st);
+  if (rc != KVECC_OK) return rc;
+  hipLaunchKernelGGL(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
+  return KVECC_OK;
+}
+
+// tokens per workgroup: the largest power of two <= kMaxSplit that still gives
+// >= 4 workgroups per CU (small batch*heads decode steps split finer)
+static int64_t choose_split(int64_t bh, int64_t max_context_len) {
+  int64_t split = kMaxSplit;
+  const int64_t want = 4LL * cu_count();
+  while (split > 32 && bh * cdiv(max_context_len, split) < want) split >>= 1;
+  while (cdiv(max_context_len, split) > kMaxSplits && split < kMaxSplit) split <<= 1;
+  return split;
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int64_t kvecc_paged_attention_workspace(int64_t batch, int64_t heads, int64_t head_dim,
+                                                  int64_t max_context_len) {
+  if (batch <= 0 || heads <= 0 || head_dim <= 0 || max_context_len <= 0) return 0;
+  return batch * heads * cdiv(max_context_len, choose_split(batch * heads, max_context_len)) *
+         (head_dim + 2);
+}
+
+KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *k_cache,
+                                    const void *v_cache, const int32_t *block_table,
+                                    const int32_t *context_lens, const float *k_scales,
+                                    const float *v_scales, void *out, int64_t batch,
+                                    int64_t heads, int64_t kv_heads, int64_t head_dim,
+                                    int64_t num_blocks, int64_t num_layers, int64_t layer, int64_t block_size,
+                                    int64_t max_blocks, int64_t max_context_len, float sm_scale,
+                                    int codec, float *workspace, int64_t workspace_floats,
+                                    void *stream) {
+  if (batch < 0 || heads < 0 || kv_heads < 0 || head_dim < 0)
+    return set_error(KVECC_EINVAL, "paged_attention: negative size");
+  if (batch == 0 || heads == 0) return KVECC_OK;
+  if (kv_heads < 1 || heads % kv_heads != 0)
+    return set_error(KVECC_EINVAL, "paged_attention: %lld heads not a multiple of %lld kv heads",
+                     (long long)heads, (long long)kv_heads);
+  if (head_dim < 1 || head_dim > kAttnMaxD)
+    return set_error(KVECC_EINVAL, "paged_attention: head_dim %lld not in [1, %d]", (long long)head_dim, kAttnMaxD);
+  if (codec != KVECC_CODEC_H84 && codec != KVECC_CODEC_GOLAY)
+    return set_error(KVECC_EINVAL, "paged_attention: codec %d (hamming84 or golay only)", codec);
+  if (codec == KVECC_CODEC_H84 && head_dim % 4 != 0)
+    return set_error(KVECC_EINVAL, "paged_attention: hamming84 head_dim must be a multiple of 4");
+  if (num_layers < 1 || layer < 0 || layer >= num_layers || block_size < 1 || max_blocks < 1)
+    return set_error(KVECC_EINVAL, "paged_attention: bad cache geometry");
+  if (num_blocks < 1 || num_blocks * num_layers * kv_heads * block_size > 0x7FFFFFFFLL)
+    return set_error(KVECC_EINVAL, "paged_attention: cache rows must fit int32");
+  if (max_context_len <= 0) max_context_len = max_blocks * block_size;
+  if (!query || !k_cache || !v_cache || !block_table || !context_lens || !k_scales || !v_scales ||
+      !out || !workspace)
+    return set_error(KVECC_EINVAL, "paged_attention: null pointer");
+  const int64_t need = kvecc_paged_attention_workspace(batch, heads, head_dim, max_context_len);
+  if (workspace_floats < need)
+    return set_error(KVECC_EINVAL, "paged_attention: workspace %lld < %lld floats",
+                     (long long)workspace_floats, (long long)need);
+  AttnArgs a;
+  a.q = query;
+  a.k_cache = k_cache;
+  a.v_cache = v_cache;
+  a.table = block_table;
+  a.ctx_lens = context_lens;
+  a.k_scales = k_scales;
+  a.v_scales = v_scales;
+  a.ws = workspace;
+  a.out = out;
+  a.heads = heads;
+  a.kv_heads = kv_heads;
+  a.d = head_dim;
+  a.g = codec == KVECC_CODEC_H84 ? head_dim / 4 : (head_dim + 2) / 3;
+  a.layers = num_layers;
+  a.layer = layer;
+  a.bs = block_size;
+  a.max_blocks = max_blocks;
+  a.split = choose_split(batch * heads, max_context_len);
+  a.nsplit = cdiv(max_context_len, a.split);
+  if (a.nsplit > kMaxSplits)
+    return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
+  a.sm_scale = sm_scale;
+  a.par = a.cor = nullptr;
+  if (codec == KVECC_CODEC_GOLAY) {
+    a.par = golay_parity_table_dev();
+    a.cor = golay_correct_table_dev();
+    if (!a.par || !a.cor) return KVECC_EHIP;
+  }
+  hipStream_t st = as_stream(stream);
+  int rc;
+  switch (q_dtype) {
+    case KVECC_F32:
+      rc = codec == KVECC_CODEC_H84 ? launch_attn<float, KVECC_CODEC_H84>(a, batch, st)
+                                    : launch_attn<float, KVECC_CODEC_GOLAY>(a, batch, st);
+      break;
+    case KVECC_F16:
+      rc = codec == KVECC_CODEC_H84 ? launch_attn<__half, KVECC_CODEC_H84>(a, batch, st)
+                                    : launch_attn<__half, KVECC_CODEC_GOLAY>(a, batch, st);
+      break;
+    case KVECC_BF16:
+      rc = codec == KVECC_CODEC_H84 ? launch_attn<__hip_bfloat16, KVECC_CODEC_H84>(a, batch, st)
+                                    : launch_attn<__hip_bfloat16, KVECC_CODEC_GOLAY>(a, batch, st);
+      break;
+    default: return set_error(KVECC_EINVAL, "paged_attention: bad dtype %d", q_dtype);
+  }
+  if (rc != KVECC_OK) return rc;
+  return check_launch("paged_attention");
+}
+
+}  // extern "C"

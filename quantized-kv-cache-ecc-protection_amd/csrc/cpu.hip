@@ -617,4 +617,91 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
   return KVECC_OK;
 }
 
+// ---- paged decode attention (host twin of attention.hip) ---------------------
+// The reference's order exactly: one (b, h) at a time, tokens in order, online
+// softmax in fp32 (attention_ecc.py:355-427).
+KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const void *k_cache,
+                                        const void *v_cache, const int32_t *block_table,
+                                        const int32_t *context_lens, const float *k_scales,
+                                        const float *v_scales, void *out, int64_t batch,
+                                        int64_t heads, int64_t kv_heads, int64_t head_dim,
+                                        int64_t num_blocks, int64_t num_layers, int64_t layer, int64_t block_size,
+                                        int64_t max_blocks, int64_t max_context_len,
+                                        float sm_scale, int codec, int threads) {
+  if (batch < 0 || heads < 0 || kv_heads < 0 || head_dim < 0)
+    return set_error(KVECC_EINVAL, "cpu_paged_attention: negative size");
+  if (batch == 0 || heads == 0) return KVECC_OK;
+  if (kv_heads < 1 || heads % kv_heads != 0)
+    return set_error(KVECC_EINVAL, "cpu_paged_attention: heads not a multiple of kv heads");
+  if (head_dim < 1) return set_error(KVECC_EINVAL, "cpu_paged_attention: empty head_dim");
+  if (codec != KVECC_CODEC_H84 && codec != KVECC_CODEC_GOLAY)
+    return set_error(KVECC_EINVAL, "cpu_paged_attention: codec %d (hamming84 or golay only)", codec);
+  if (q_dtype < KVECC_F32 || q_dtype > KVECC_BF16)
+    return set_error(KVECC_EINVAL, "cpu_paged_attention: bad dtype %d", q_dtype);
+  if (num_layers < 1 || layer < 0 || layer >= num_layers || block_size < 1 || max_blocks < 1)
+    return set_error(KVECC_EINVAL, "cpu_paged_attention: bad cache geometry");
+  if (!query || !k_cache || !v_cache || !block_table || !context_lens || !k_scales || !v_scales || !out)
+    return set_error(KVECC_EINVAL, "cpu_paged_attention: null pointer");
+  if (max_context_len <= 0) max_context_len = max_blocks * block_size;
+  static uint16_t tab[8192];
+  static bool ready = [] {
+    build_golay_parity_table(tab);
+    build_golay_correct_table(tab + 4096);
+    return true;
+  }();
+  (void)ready;
+  const bool golay = codec == KVECC_CODEC_GOLAY;
+  const int64_t g = golay ? (head_dim + 2) / 3 : head_dim;
+  const int64_t groups = heads / kv_heads;
+  parallel_for(batch * heads, threads, 1, [&](int64_t b0, int64_t e0, int) {
+    std::vector<float> q(head_dim), kv(head_dim), acc(head_dim);
+    auto decode_row = [&](const void *cache, int64_t srow, float s) {
+      if (golay) {
+        const int32_t *c = reinterpret_cast<const int32_t *>(cache) + srow * g;
+        for (int64_t k = 0; k < g; ++k) {
+          uint32_t cnt;
+          const uint32_t dw = golay_decode1((uint32_t)c[k], tab, tab + 4096, cnt);
+          for (int64_t u = 0; u < 3 && 3 * k + u < head_dim; ++u)
+            kv[3 * k + u] = ((float)(dw >> (4 * u) & 0xFu) - 8.0f) * s;
+        }
+      } else {
+        const uint8_t *c = reinterpret_cast<const uint8_t *>(cache) + srow * head_dim;
+        for (int64_t j = 0; j < head_dim; ++j) {
+          uint32_t d, t, n1 = 0, n2 = 0;
+          h84_decode4(c[j], d, t, n1, n2);
+          kv[j] = ((float)d - 8.0f) * s;
+        }
+      }
+    };
+    for (int64_t bh = b0; bh < e0; ++bh) {
+      const int64_t b = bh / heads, h = bh % heads, hk = h / groups;
+      for (int64_t j = 0; j < head_dim; ++j) q[j] = load_x(query, q_dtype, bh * head_dim + j);
+      std::fill(acc.begin(), acc.end(), 0.0f);
+      float m = -INFINITY, l = 0.0f;
+      const int64_t ctx = std::min<int64_t>(std::min<int64_t>(context_lens[b], max_context_len),
+                                            max_blocks * block_size);
+      for (int64_t pos = 0; pos < ctx; ++pos) {
+        const int32_t blk = block_table[b * max_blocks + pos / block_size];
+        if (blk < 0) continue;
+        const int64_t srow = (((int64_t)blk * num_layers + layer) * kv_heads + hk) * block_size +
+                             pos % block_size;
+        decode_row(k_cache, srow, k_scales[srow]);
+        float sc = 0.0f;
+        for (int64_t j = 0; j < head_dim; ++j) sc += q[j] * kv[j];
+        sc *= sm_scale;
+        const float mn = std::max(m, sc);
+        const float alpha = m == -INFINITY ? 0.0f : std::exp(m - mn);
+        const float beta = std::exp(sc - mn);
+        decode_row(v_cache, srow, v_scales[srow]);
+        for (int64_t j = 0; j < head_dim; ++j) acc[j] = alpha * acc[j] + beta * kv[j];
+        l = alpha * l + beta;
+        m = mn;
+      }
+      for (int64_t j = 0; j < head_dim; ++j)
+        store_y(out, q_dtype, bh * head_dim + j, l > 0.0f ? acc[j] / l : 0.0f);
+    }
+  });
+  return KVECC_OK;
+}
+
 }  // extern "C"

@@ -19,11 +19,13 @@ from .ops import (fused_decode_dequantize_hamming84, fused_quantize_encode_hammi
                   hamming74_encode, hamming84_decode, hamming84_encode, inject_bit_errors,
                   inject_bit_errors_triton, inject_bit_errors_triton_batched,
                   inject_bit_errors_triton_vectorized, interpolate_double_errors,
-                  interpolate_double_errors_1d, interpolate_double_errors_autotuned)
+                  interpolate_double_errors_1d, interpolate_double_errors_autotuned,
+                  paged_attention_ecc)
 
 __version__ = "0.1.0"
 
 __all__ = [
+    "paged_attention_ecc",
     "get_physical_dtype", "get_codeword_bits", "get_data_bits",
     "HAMMING74_BLOCK_SIZE", "HAMMING84_BLOCK_SIZE", "GOLAY_BLOCK_SIZE",
     "FAULT_INJECTION_BLOCK_SIZE", "INTERPOLATION_BLOCK_SIZE",

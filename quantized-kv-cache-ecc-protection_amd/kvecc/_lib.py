@@ -49,6 +49,9 @@ SIGNATURES = {
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
     "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
+    "kvecc_paged_attention_workspace": [_i64, _i64, _i64, _i64],
+    "kvecc_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
+                              _i64, _i64, _i64, _i64, _i64, _i64, _f32, _int, _vp, _i64, _vp],
     # host backend (threads instead of a stream)
     "kvecc_cpu_hamming74_encode": [_vp, _vp, _i64, _int],
     "kvecc_cpu_hamming84_encode": [_vp, _vp, _i64, _int],
@@ -69,11 +72,14 @@ SIGNATURES = {
     "kvecc_cpu_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _int],
     "kvecc_cpu_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _int],
     "kvecc_cpu_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _int],
+    "kvecc_cpu_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
+                                  _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _int, _int],
 }
 _RESTYPE = {
     "kvecc_version": ctypes.c_char_p,
     "kvecc_last_error": ctypes.c_char_p,
     "kvecc_ber_threshold": ctypes.c_uint32,
+    "kvecc_paged_attention_workspace": ctypes.c_int64,
 }
 
 # dtype / codec codes (include/kvecc.h)

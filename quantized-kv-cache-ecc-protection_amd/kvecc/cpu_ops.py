@@ -16,6 +16,7 @@ fallback of the "hip" one; it needs libkvecc.so but no GPU.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 
 import torch
@@ -461,3 +462,49 @@ def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=
               int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
               _DT[out_dtype], _ptr(stats), NUM_THREADS)
     return k_out, v_out
+
+
+# ============================================================================
+# Paged decode attention (host twin of ops.paged_attention_ecc)
+# ============================================================================
+
+def paged_attention_into(query, k_cache, v_cache, block_table, context_lens, k_scales, v_scales,
+                         out, layer_idx, block_size, sm_scale, codec, max_context_len=0):
+    batch, heads, head_dim = query.shape
+    num_blocks, num_layers, kv_heads, _ = k_cache.shape
+    max_blocks = block_table.shape[1]
+    _lib.call("kvecc_cpu_paged_attention", _ptr(query), _DT[query.dtype], _ptr(k_cache),
+              _ptr(v_cache), _ptr(block_table), _ptr(context_lens), _ptr(k_scales),
+              _ptr(v_scales), _ptr(out), batch, heads, kv_heads, head_dim, num_blocks, num_layers,
+              int(layer_idx), int(block_size), max_blocks, int(max_context_len or 0),
+              float(sm_scale), SHIM_CODECS[codec], NUM_THREADS)
+    return out
+
+
+def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_scales, layer_idx,
+                        block_size, sm_scale=None, codec="hamming84", syndrome_table=None,
+                        use_tiled=False, block_m=4, v_scales=None):
+    """Host twin of ops.paged_attention_ecc (same arguments and quirks)."""
+    _check_cpu(query, "Query")
+    if codec not in ("hamming84", "golay"):
+        raise ValueError(f"Unknown codec: {codec}")
+    if codec == "golay":
+        v_scales = k_scales
+    if v_scales is None:
+        v_scales = k_scales
+    if sm_scale is None:
+        sm_scale = 1.0 / math.sqrt(query.shape[-1])
+    q = query.contiguous()
+    out_dtype = torch.float32 if codec == "golay" else q.dtype
+    if q.dtype not in _DT:
+        raise TypeError(f"unsupported query dtype {q.dtype}")
+    if out_dtype != q.dtype:
+        q = q.to(out_dtype)
+    out = torch.empty(q.shape, dtype=out_dtype)
+    paged_attention_into(q, k_cache.contiguous(), v_cache.contiguous(),
+                         block_table.to(torch.int32).contiguous(),
+                         context_lens.to(torch.int32).contiguous(),
+                         k_scales.to(torch.float32).contiguous(),
+                         v_scales.to(torch.float32).contiguous(), out, layer_idx, block_size,
+                         sm_scale, codec)
+    return out

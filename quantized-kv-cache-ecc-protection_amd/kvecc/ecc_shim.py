@@ -345,6 +345,8 @@ class ECCBackend:
             return torch.zeros_like(q)
         q_len = q.shape[2]
         fast = cfg.codec == "hamming84" and not cfg.use_interpolation and q_len == 1
+        if self._fused_ok() and fast:
+            return self._paged_decode_attention(q, layer_idx, seq_id, ctx)
         if self._fused_ok():
             # the reference's seq_len==1 Triton path (ecc_shim.py:791-800) keeps no statistics
             interp = cfg.use_interpolation and cfg.codec == "hamming84"
@@ -372,6 +374,22 @@ class ECCBackend:
         if fast:
             return self._decode_step_attention(q, k_f.transpose(0, 1), v_f.transpose(0, 1))
         return self._run_attention(q, k_f, v_f)
+
+    def _paged_decode_attention(self, q, layer_idx, seq_id, ctx):
+        """seq_len==1 Hamming(8,4) path: paged attention with inline decode
+        (attention_ecc.py:620-780 via ecc_shim.py:1091-1136), no statistics.
+        Every batch row attends over the same seq_id context (the reference
+        passes one block-table row, ecc_shim.py:1117-1129)."""
+        mgr = self.manager
+        b, h, _, d = q.shape
+        q1 = q[:, :, 0, :].contiguous()
+        table = mgr.block_table[seq_id].unsqueeze(0).expand(b, -1).contiguous()
+        lens = torch.full((b,), ctx, dtype=torch.int32, device=q.device)
+        out = torch.empty_like(q1)
+        self.codec_backend.paged_attention_into(
+            q1, mgr.k_cache, mgr.v_cache, table, lens, mgr.k_scales, mgr.v_scales, out,
+            layer_idx, mgr.block_size, 1.0 / math.sqrt(d), "hamming84", max_context_len=ctx)
+        return out.unsqueeze(2)
 
     def _decode_step_attention(self, q, k_f, v_f):
         """seq_len==1 path of paged_attention_ecc (attention_ecc.py:264-427): fp32

@@ -18,6 +18,7 @@ Two layers:
 from __future__ import annotations
 
 import ctypes
+import math
 
 import torch
 
@@ -517,3 +518,68 @@ def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=
               int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
               _DT[out_dtype], _ptr(stats), _stream(dev))
     return k_out, v_out
+
+
+# ============================================================================
+# Paged decode attention with inline ECC decode
+# ============================================================================
+
+def paged_attention_into(query, k_cache, v_cache, block_table, context_lens, k_scales, v_scales,
+                         out, layer_idx, block_size, sm_scale, codec, max_context_len=0):
+    """kvecc_paged_attention on [B, H, D] query / out (see include/kvecc.h)."""
+    batch, heads, head_dim = query.shape
+    num_blocks, num_layers, kv_heads, _ = k_cache.shape
+    max_blocks = block_table.shape[1]
+    mcl = int(max_context_len) if max_context_len and max_context_len > 0 else max_blocks * block_size
+    ws_n = _lib.load().kvecc_paged_attention_workspace(batch, heads, head_dim, mcl)
+    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=query.device)
+    _lib.call("kvecc_paged_attention", _ptr(query), _DT[query.dtype], _ptr(k_cache), _ptr(v_cache),
+              _ptr(block_table), _ptr(context_lens), _ptr(k_scales), _ptr(v_scales), _ptr(out),
+              batch, heads, kv_heads, head_dim, num_blocks, num_layers, int(layer_idx), int(block_size),
+              max_blocks, mcl, float(sm_scale), SHIM_CODECS[codec], _ptr(ws), ws_n,
+              _stream(query.device))
+    return out
+
+
+def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_scales, layer_idx,
+                        block_size, sm_scale=None, codec="hamming84", syndrome_table=None,
+                        use_tiled=False, block_m=4, v_scales=None):
+    """Single-token paged attention over the ECC cache; attention_ecc.py:620-780.
+
+    query [B, H, D]; caches [blocks, layers, Hkv, block_size * P]; block_table
+    [B, max_blocks] int32; context_lens [B] int32.  -> [B, H, D] in query's
+    dtype.  As in the reference: v_scales defaults to k_scales; the "golay"
+    codec reproduces reference_attention_ecc (:783-909), which dequantizes K
+    and V with k_scales and returns fp32.  syndrome_table / use_tiled / block_m
+    are accepted for signature compatibility (the table lives on the device,
+    the kernel's geometry is fixed).
+    """
+    _check_gpu(query, "Query")
+    if codec not in ("hamming84", "golay"):
+        raise ValueError(f"Unknown codec: {codec}")
+    if codec == "hamming84":
+        assert k_cache.dtype == torch.uint8, "Hamming84 K cache must be uint8"
+        assert v_cache.dtype == torch.uint8, "Hamming84 V cache must be uint8"
+    else:
+        assert k_cache.dtype == torch.int32, "Golay K cache must be int32"
+        assert v_cache.dtype == torch.int32, "Golay V cache must be int32"
+        v_scales = k_scales  # reference_attention_ecc uses one scale tensor for K and V
+    if v_scales is None:
+        v_scales = k_scales
+    head_dim = query.shape[-1]
+    if sm_scale is None:
+        sm_scale = 1.0 / math.sqrt(head_dim)
+    q = query.contiguous()
+    out_dtype = torch.float32 if codec == "golay" else q.dtype
+    if q.dtype not in _DT:
+        raise TypeError(f"unsupported query dtype {q.dtype}")
+    if out_dtype != q.dtype:
+        q = q.to(out_dtype)
+    out = torch.empty(q.shape, dtype=out_dtype, device=q.device)
+    paged_attention_into(q, k_cache.contiguous(), v_cache.contiguous(),
+                         block_table.to(torch.int32).contiguous(),
+                         context_lens.to(torch.int32).contiguous(),
+                         k_scales.to(torch.float32).contiguous(),
+                         v_scales.to(torch.float32).contiguous(), out, layer_idx, block_size,
+                         sm_scale, codec)
+    return out

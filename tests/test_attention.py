@@ -1,0 +1,131 @@
+"""Paged decode attention with inline ECC decode (attention_ecc.py:620-780)
+against a plain torch fp32 reference of the same op.
+
+The reference kernel walks tokens with an online softmax in fp32; the HIP
+kernel splits the context and combines partials, so results agree to fp32
+summation-order rounding: ATOL/RTOL below.  The host twin follows the
+reference's sequential order.  Decoding itself is bit-exact (checked through
+the oracle-pinned host backend).
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+ATOL = 2e-5
+RTOL = 2e-4
+
+
+def _cache(device, codec, batch, heads, kv_heads, d, ctx, ber, seed, layers=3, layer=1, bs=16):
+    """Random paged caches written through the host backend (oracle-pinned)."""
+    from kvecc import cpu_ops
+    g = torch.Generator().manual_seed(seed)
+    nblk_seq = (ctx + bs - 1) // bs
+    num_blocks = batch * nblk_seq + 3
+    per = d if codec == "hamming84" else (d + 2) // 3
+    cdt = torch.uint8 if codec == "hamming84" else torch.int32
+    kc = torch.zeros(num_blocks, layers, kv_heads, bs * per, dtype=cdt)
+    vc = torch.zeros_like(kc)
+    x = torch.randn(2, num_blocks, layers, kv_heads, bs, d, generator=g)
+    for cache, xi in ((kc, x[0]), (vc, x[1])):
+        q, s = cpu_ops.quantize_rows(xi)
+        if codec == "hamming84":
+            enc = cpu_ops.hamming84_encode(q)
+        else:
+            enc = cpu_ops.golay_encode_rows(q)
+        if ber > 0:
+            enc = cpu_ops.inject_bit_errors_triton(enc, ber, 8 if codec == "hamming84" else 24,
+                                                   seed=seed)
+        cache.copy_(enc.reshape(cache.shape))
+    ks = torch.rand(num_blocks, layers, kv_heads, bs, generator=g) * 0.3 + 0.05
+    vs = torch.rand(num_blocks, layers, kv_heads, bs, generator=g) * 0.3 + 0.05
+    perm = torch.randperm(num_blocks, generator=g)[: batch * nblk_seq].to(torch.int32)
+    max_blocks = nblk_seq + 2
+    table = torch.full((batch, max_blocks), -1, dtype=torch.int32)
+    table[:, :nblk_seq] = perm.view(batch, nblk_seq)
+    lens = torch.tensor([max(1, ctx - 7 * b) for b in range(batch)], dtype=torch.int32)
+    return kc, vc, table, lens, ks, vs
+
+
+def _torch_reference(query, kc, vc, table, lens, ks, vs, layer, bs, codec):
+    """fp32 torch restatement of paged_attention_ecc (per (b, h) softmax)."""
+    from kvecc import cpu_ops
+    b_, h_, d = query.shape
+    kv_heads = kc.shape[2]
+    groups = h_ // kv_heads
+    out = torch.zeros(b_, h_, d)
+    for b in range(b_):
+        n = int(lens[b])
+        pos = torch.arange(n)
+        blk = table[b, pos // bs].long()
+        slot = pos % bs
+        ok = blk >= 0
+        pos, blk, slot = pos[ok], blk[ok], slot[ok]
+        for side, cache, sc in ((0, kc, ks), (1, vc, vs)):
+            rows = cache.view(cache.shape[0], cache.shape[1], kv_heads, bs, -1)[blk, layer, :, slot]
+            if codec == "hamming84":
+                dec, _ = cpu_ops.hamming84_decode(rows.contiguous())
+            else:
+                dec = cpu_ops.golay_decode_rows(rows.contiguous(), d)
+            f = (dec.float() - 8.0) * sc[blk, layer, :, slot].unsqueeze(-1)  # [n, Hkv, d]
+            if side == 0:
+                kf = f
+            else:
+                vf = f
+        for h in range(h_):
+            hk = h // groups
+            s = (query[b, h].float() @ kf[:, hk].T) / math.sqrt(d)
+            w = torch.softmax(s, dim=0)
+            out[b, h] = w @ vf[:, hk]
+    return out
+
+
+CASES = [("hamming84", 2, 4, 4, 64, 300, 0.01), ("hamming84", 1, 12, 12, 64, 1024, 0.0),
+         ("hamming84", 3, 8, 2, 128, 700, 0.02), ("golay", 2, 4, 4, 128, 513, 0.02),
+         ("golay", 1, 6, 3, 64, 77, 0.0), ("hamming84", 1, 2, 1, 32, 5, 0.05)]
+
+
+@pytest.mark.parametrize("codec,batch,heads,kvh,d,ctx,ber", CASES)
+def test_cpu_backend_vs_torch(codec, batch, heads, kvh, d, ctx, ber):
+    from kvecc import cpu_ops
+    kc, vc, table, lens, ks, vs = _cache("cpu", codec, batch, heads, kvh, d, ctx, ber, seed=ctx)
+    q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(1))
+    ref = _torch_reference(q, kc, vc, table, lens, ks, vs if codec == "hamming84" else ks, 1, 16,
+                           codec)
+    got = cpu_ops.paged_attention_ecc(q, kc, vc, table, lens, ks, 1, 16, codec=codec, v_scales=vs)
+    assert torch.allclose(got, ref, atol=ATOL, rtol=RTOL), float((got - ref).abs().max())
+
+
+def test_empty_context_and_missing_blocks():
+    from kvecc import cpu_ops
+    kc, vc, table, lens, ks, vs = _cache("cpu", "hamming84", 2, 2, 2, 32, 40, 0.0, seed=3)
+    lens[1] = 0
+    table[0, 1] = -1  # tokens 16..31 of sequence 0 are skipped
+    q = torch.randn(2, 2, 32)
+    got = cpu_ops.paged_attention_ecc(q, kc, vc, table, lens, ks, 1, 16, v_scales=vs)
+    ref = _torch_reference(q, kc, vc, table, lens, ks, vs, 1, 16, "hamming84")
+    assert torch.equal(got[1], torch.zeros(2, 32))
+    assert torch.allclose(got, ref, atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,batch,heads,kvh,d,ctx,ber", CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_hip_vs_torch(gpu, codec, batch, heads, kvh, d, ctx, ber, dtype):
+    from kvecc import ops
+    kc, vc, table, lens, ks, vs = _cache("cpu", codec, batch, heads, kvh, d, ctx, ber, seed=ctx)
+    q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(1)).to(dtype)
+    ref = _torch_reference(q.float(), kc, vc, table, lens, ks, vs if codec == "hamming84" else ks,
+                           1, 16, codec)
+    dev = lambda t: t.to(gpu)  # noqa: E731
+    got = ops.paged_attention_ecc(dev(q), dev(kc), dev(vc), dev(table), dev(lens), dev(ks), 1, 16,
+                                  codec=codec, v_scales=dev(vs)).cpu()
+    if codec == "golay" or dtype == torch.float32:
+        assert got.dtype == torch.float32
+        assert torch.allclose(got, ref, atol=ATOL, rtol=RTOL), float((got - ref).abs().max())
+    else:  # fp16 output: within one fp16 ulp of the fp32 result
+        assert got.dtype == dtype
+        assert torch.allclose(got.float(), ref, atol=1e-3, rtol=1e-3), \
+            float((got.float() - ref).abs().max())
