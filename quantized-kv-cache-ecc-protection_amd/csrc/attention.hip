@@ -71,7 +71,7 @@ struct Chunk {
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
   // correction tables (uncorrectable words keep their data, as golay_decode)
-  __device__ __forceinline__ void decode(const AttnArgs &a, const float *lut, float *v) const {
+  __device__ __forceinline__ void decode(const float *lut, const uint16_t *gtab, float *v) const {
     if (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
@@ -80,7 +80,7 @@ struct Chunk {
       }
     } else {
       uint32_t cnt;
-      const uint32_t dw = golay_decode1(w[0], a.par, a.cor, cnt);
+      const uint32_t dw = golay_decode1(w[0], gtab, gtab + 4096, cnt);
 #pragma unroll
       for (int e = 0; e < 3; ++e) v[e] = (float)(dw >> (4 * e) & 0xFu) - 8.0f;
     }
@@ -98,6 +98,8 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   __shared__ float red[TP * W * E];        // per-group acc
   __shared__ float gml[2][TP];             // per-group running max / sum
   __shared__ float lut[256];               // H(8,4): codeword byte -> data - 8
+  // Golay: parity[4096] then correct[4096] (16 KiB) copied from the device tables
+  __shared__ __attribute__((aligned(16))) uint16_t gtab[CODEC == KVECC_CODEC_GOLAY ? 8192 : 8];
 
   const int64_t bh = blockIdx.y;
   const int64_t b = bh / a.heads, h = bh % a.heads;
@@ -125,6 +127,15 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
         if (blk >= 0) row = blk * blk_rows + head_row0 + (int32_t)(pos - lb * bs);
       }
       rows[i] = row;
+    }
+  }
+  if (CODEC == KVECC_CODEC_GOLAY) {
+    const u32x4 *src0 = reinterpret_cast<const u32x4 *>(a.par);
+    const u32x4 *src1 = reinterpret_cast<const u32x4 *>(a.cor);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
+    for (int i = threadIdx.x; i < 512; i += kBlock) {
+      dst[i] = src0[i];
+      dst[512 + i] = src1[i];
     }
   }
   if (CODEC == KVECC_CODEC_H84 && threadIdx.x < 256) {
@@ -167,7 +178,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       float part = 0.0f;
       if (live) {
         float kv[E];
-        kc[u].decode(a, lut, kv);
+        kc[u].decode(lut, gtab, kv);
 #pragma unroll
         for (int e = 0; e < E; ++e) part += qv[e] * kv[e];
         part *= ks[u];  // sum q (n - 8) s = s * sum q (n - 8)
@@ -188,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       l += p;
       if (live) {
         float vv[E];
-        vc[u].decode(a, lut, vv);
+        vc[u].decode(lut, gtab, vv);
         const float ps = p * vs[u];
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] += ps * vv[e];

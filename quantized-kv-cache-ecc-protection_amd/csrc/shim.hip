@@ -28,11 +28,14 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 
 struct ShimGeom {
   const int32_t *table;
-  int64_t hkv, d, g;  // g = codewords per token row: d, or ceil(d/3) for Golay
-  int64_t layers, bs, layer;
-  __device__ __forceinline__ int64_t slot(int64_t pos, int64_t h) const {
-    const int64_t blk = table[pos / bs];
-    return ((blk * layers + layer) * hkv + h) * bs + pos % bs;
+  // 32-bit index math (the host checks every count fits): 64-bit division is
+  // ~100 instructions on gfx950
+  uint32_t hkv, d, g;  // g = codewords per token row: d, or ceil(d/3) for Golay
+  uint32_t layers, bs, layer;
+  __device__ __forceinline__ int64_t slot(uint32_t pos, uint32_t h) const {
+    const uint32_t lb = pos / bs;
+    const int64_t blk = table[lb];
+    return ((blk * layers + layer) * hkv + h) * bs + (pos - lb * bs);
   }
 };
 
@@ -52,13 +55,13 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
   __shared__ uint8_t nib[kWavesPerBlock][kMaxShimD + 4];
   const ShimGeom &geo = a.geo;
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  const int64_t per_side = a.seq * geo.hkv;
-  const int64_t item = (int64_t)blockIdx.x * kWavesPerBlock + w;
+  const uint32_t per_side = (uint32_t)a.seq * geo.hkv;
+  const uint32_t item = blockIdx.x * kWavesPerBlock + w;
   const bool live = item < 2 * per_side;
-  const int side = live ? (int)(item / per_side) : 0;
-  const int64_t rr = live ? item - side * per_side : 0;
-  const int64_t pos = rr / geo.hkv, h = rr - pos * geo.hkv;
-  const int64_t r = (a.batch - 1) * per_side + rr;  // running row index of the write
+  const int side = live && item >= per_side ? 1 : 0;
+  const uint32_t rr = live ? item - side * per_side : 0;
+  const uint32_t pos = rr / geo.hkv, h = rr - pos * geo.hkv;
+  const int64_t r = (a.batch - 1) * (int64_t)per_side + rr;  // running row index of the write
   const uint32_t key0 = (a.seed0 + (uint32_t)r + (uint32_t)side) * a.rowmul;
   const int64_t slot = live ? geo.slot(pos, h) : 0;
 
@@ -69,7 +72,7 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
     const T *x = reinterpret_cast<const T *>(a.x[side]) + r * geo.d;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      const int64_t e = lane + (int64_t)i * kWave;
+      const uint32_t e = lane + i * kWave;
       v[i] = e < geo.d ? to_f32<T>(x[e]) : 0.0f;
       amax = fmaxf(amax, fabsf(v[i]));
     }
@@ -97,19 +100,19 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
   if (live) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      const int64_t e = lane + (int64_t)i * kWave;
+      const uint32_t e = lane + i * kWave;
       if (e < geo.d) nib[w][e] = (uint8_t)quantize_nibble(v[i], scale);
     }
-    if (lane < 3 * geo.g - geo.d) nib[w][geo.d + lane] = 0;  // per-head zero padding
+    if ((uint32_t)lane < 3 * geo.g - geo.d) nib[w][geo.d + lane] = 0;  // per-head zero padding
   }
   __syncthreads();
   if (!live) return;
   int32_t *c = reinterpret_cast<int32_t *>(a.cache[side]) + slot * geo.g;
-  for (int64_t k = lane; k < geo.g; k += kWave) {
+  for (uint32_t k = lane; k < geo.g; k += kWave) {
     const uint32_t dw = golay_pack(nib[w][3 * k], nib[w][3 * k + 1], nib[w][3 * k + 2]);
     uint32_t cw = dw | golay_parity12(dw) << 12;
     if (a.inject)
-      cw ^= philox_flip_mask<NB>(key0 + (uint32_t)k * a.nbits, (uint32_t)k, a.thr, a.nb_eff);
+      cw ^= philox_flip_mask<NB>(key0 + k * a.nbits, k, a.thr, a.nb_eff);
     c[k] = (int32_t)cw;
   }
 }
@@ -119,7 +122,7 @@ struct ShimReadArgs {
   const void *cache[2];
   const float *scales[2];
   void *out[2];  // [hkv, ctx, d]
-  int64_t ctx;
+  uint32_t ctx;
   const uint16_t *par, *cor;  // Golay tables
   uint64_t *stats;
 };
@@ -130,7 +133,7 @@ __device__ __forceinline__ void dequant4(TO *o, uint32_t q, float s) {
   for (int k = 0; k < 4; ++k) o[k] = from_f32<TO>(((float)(q >> (8 * k) & 0xFFu) - 8.0f) * s);
 }
 
-__device__ __forceinline__ uint32_t ld_word(const uint8_t *base, int64_t slot, int64_t d, int64_t c) {
+__device__ __forceinline__ uint32_t ld_word(const uint8_t *base, int64_t slot, uint32_t d, uint32_t c) {
   return *reinterpret_cast<const uint32_t *>(base + slot * d + 4 * c);
 }
 
@@ -138,15 +141,14 @@ __device__ __forceinline__ uint32_t ld_word(const uint8_t *base, int64_t slot, i
 template <typename TO, int CODEC, bool INTERP, bool STATS>
 __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a) {
   const ShimGeom &geo = a.geo;
-  const int64_t c4 = geo.d / 4;
-  const int64_t per_side = geo.hkv * a.ctx * c4;
+  const uint32_t c4 = geo.d / 4;
+  const uint32_t per_side = geo.hkv * a.ctx * c4;
   uint32_t n1 = 0, n2 = 0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < 2 * per_side;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int side = (int)(i / per_side);
-    const int64_t t = i - side * per_side;
-    const int64_t c = t % c4, hl = t / c4;
-    const int64_t l = hl % a.ctx, h = hl / a.ctx;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < 2 * per_side; i += gridDim.x * kBlock) {
+    const int side = i >= per_side ? 1 : 0;
+    const uint32_t t = i - side * per_side;
+    const uint32_t hl = t / c4, c = t - hl * c4;
+    const uint32_t h = hl / a.ctx, l = hl - h * a.ctx;
     const uint8_t *base = reinterpret_cast<const uint8_t *>(a.cache[side]);
     const int64_t slot = geo.slot(l, h);
     const uint32_t w = ld_word(base, slot, geo.d, c);
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a)
     if (CODEC == KVECC_CODEC_H84) {
       h84_decode4(w, q, type, n1, n2);
       if (INTERP) {  // neighbours are the decoded (not interpolated) values
-        const int64_t lp = l > 0 ? l - 1 : 0, ln = l + 1 < a.ctx ? l + 1 : a.ctx - 1;
+        const uint32_t lp = l > 0 ? l - 1 : 0, ln = l + 1 < a.ctx ? l + 1 : a.ctx - 1;
         uint32_t ql, qr, tt, u1 = 0, u2 = 0;
         h84_decode4(ld_word(base, geo.slot(lp, h), geo.d, c), ql, tt, u1, u2);
         h84_decode4(ld_word(base, geo.slot(ln, h), geo.d, c), qr, tt, u1, u2);
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a)
     } else if (CODEC == KVECC_CODEC_H74) {
       h74_decode4(w, q, type, n1);
     }
-    dequant4(reinterpret_cast<TO *>(a.out[side]) + (h * a.ctx + l) * geo.d + 4 * c, q,
+    dequant4(reinterpret_cast<TO *>(a.out[side]) + ((int64_t)h * a.ctx + l) * geo.d + 4 * c, q,
              a.scales[side][slot]);
   }
   if (STATS) flush_stats2(a.stats, n1, n2);
@@ -173,14 +175,13 @@ __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a)
 template <typename TO, bool STATS>
 __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a) {
   const ShimGeom &geo = a.geo;
-  const int64_t per_side = geo.hkv * a.ctx * geo.g;
+  const uint32_t per_side = geo.hkv * a.ctx * geo.g;
   uint32_t bits = 0, unc = 0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < 2 * per_side;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int side = (int)(i / per_side);
-    const int64_t t = i - side * per_side;
-    const int64_t k = t % geo.g, hl = t / geo.g;
-    const int64_t l = hl % a.ctx, h = hl / a.ctx;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < 2 * per_side; i += gridDim.x * kBlock) {
+    const int side = i >= per_side ? 1 : 0;
+    const uint32_t t = i - side * per_side;
+    const uint32_t hl = t / geo.g, k = t - hl * geo.g;
+    const uint32_t h = hl / a.ctx, l = hl - h * a.ctx;
     const int64_t slot = geo.slot(l, h);
     const uint32_t w = (uint32_t)reinterpret_cast<const int32_t *>(a.cache[side])[slot * geo.g + k];
     uint32_t cnt;
@@ -188,8 +189,8 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
     bits += cnt & 3u;
     unc += cnt >> 2;
     const float s = a.scales[side][slot];
-    TO *o = reinterpret_cast<TO *>(a.out[side]) + (h * a.ctx + l) * geo.d + 3 * k;
-    const int64_t left = geo.d - 3 * k;
+    TO *o = reinterpret_cast<TO *>(a.out[side]) + ((int64_t)h * a.ctx + l) * geo.d + 3 * k;
+    const uint32_t left = geo.d - 3 * k;
     o[0] = from_f32<TO>(((float)(dw & 0xFu) - 8.0f) * s);
     if (left > 1) o[1] = from_f32<TO>(((float)(dw >> 4 & 0xFu) - 8.0f) * s);
     if (left > 2) o[2] = from_f32<TO>(((float)(dw >> 8) - 8.0f) * s);
@@ -271,9 +272,12 @@ KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_
     return set_error(KVECC_EINVAL, "shim_write: bad cache geometry");
   if (!k || !v || !k_cache || !v_cache || !k_scales || !v_scales || !block_table)
     return set_error(KVECC_EINVAL, "shim_write: null pointer");
+  if (2 * seq * hkv > 0x7FFFFFFFLL || num_layers * hkv * block_size > 0x7FFFFFFFLL)
+    return set_error(KVECC_EINVAL, "shim_write: sizes exceed 32-bit indexing");
   ShimWriteArgs a;
-  a.geo = {block_table, hkv, d, codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d, num_layers,
-           block_size, layer};
+  a.geo = {block_table, (uint32_t)hkv, (uint32_t)d,
+           (uint32_t)(codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d), (uint32_t)num_layers,
+           (uint32_t)block_size, (uint32_t)layer};
   a.x[0] = k;
   a.x[1] = v;
   a.cache[0] = k_cache;
@@ -320,16 +324,19 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
     return set_error(KVECC_EINVAL, "shim_read: bad cache geometry");
   if (!k_cache || !v_cache || !k_scales || !v_scales || !block_table || !k_out || !v_out)
     return set_error(KVECC_EINVAL, "shim_read: null pointer");
+  if (2 * hkv * ctx * d > 0x7FFFFFFFLL || num_layers * hkv * block_size > 0x7FFFFFFFLL)
+    return set_error(KVECC_EINVAL, "shim_read: sizes exceed 32-bit indexing");
   ShimReadArgs a;
-  a.geo = {block_table, hkv, d, codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d, num_layers,
-           block_size, layer};
+  a.geo = {block_table, (uint32_t)hkv, (uint32_t)d,
+           (uint32_t)(codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d), (uint32_t)num_layers,
+           (uint32_t)block_size, (uint32_t)layer};
   a.cache[0] = k_cache;
   a.cache[1] = v_cache;
   a.scales[0] = k_scales;
   a.scales[1] = v_scales;
   a.out[0] = k_out;
   a.out[1] = v_out;
-  a.ctx = ctx;
+  a.ctx = (uint32_t)ctx;
   a.stats = stats;
   a.par = a.cor = nullptr;
   if (codec == KVECC_CODEC_GOLAY) {
