@@ -31,7 +31,10 @@ __device__ __forceinline__ u32x4 interp_vec(u32x4 q, u32x4 l, u32x4 r, u32x4 e) 
   return o;
 }
 
-// vector path: inner % 16 == 0; work item = (o, row block, column chunk)
+// vector path: inner % 16 == 0; work item = (o, row block, column chunk).  All
+// kRows + 2 q rows (with the one-row halo each side) and kRows err rows of the
+// item are loaded before any is used, non-temporally, so a lane keeps ~18
+// 16-byte loads in flight.
 __global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restrict__ q,
                                                             const u32x4 *__restrict__ err,
                                                             u32x4 *__restrict__ out, int64_t outer,
@@ -48,7 +51,23 @@ __global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restr
     const int64_t o = t / rblocks;
     const int64_t l0 = rb * kRows;
     const int64_t base = o * len * chunks + c;  // vector index of (o, l=0, c)
-    const int nrow = (int)min<int64_t>(kRows, len - l0);
+    if (l0 + kRows <= len) {  // full row block
+      u32x4 qr[kRows + 2], er[kRows];
+      qr[0] = ld_stream(q + base + (l0 > 0 ? l0 - 1 : 0) * chunks);
+#pragma unroll
+      for (int k = 0; k < kRows; ++k) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
+      qr[kRows + 1] = ld_stream(q + base + (l0 + kRows < len ? l0 + kRows : len - 1) * chunks);
+      if (!pass) {
+#pragma unroll
+        for (int k = 0; k < kRows; ++k) er[k] = ld_stream(err + base + (l0 + k) * chunks);
+      }
+#pragma unroll
+      for (int k = 0; k < kRows; ++k)
+        st_stream(out + base + (l0 + k) * chunks,
+                  pass ? qr[k + 1] : interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
+      continue;
+    }
+    const int nrow = (int)(len - l0);  // ragged last block
     if (pass) {
       for (int k = 0; k < nrow; ++k) out[base + (l0 + k) * chunks] = q[base + (l0 + k) * chunks];
       continue;
@@ -91,24 +110,37 @@ __global__ __launch_bounds__(kBlock) void interp_scalar_kernel(const uint8_t *__
   }
 }
 
+__device__ __forceinline__ bool has_byte(u32x4 v, uint32_t pat) {
+  const uint32_t w[4] = {v.x ^ pat, v.y ^ pat, v.z ^ pat, v.w ^ pat};
+  bool hit = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hit |= ((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) != 0;  // a zero byte
+  return hit;
+}
+
+// four 16-byte non-temporal loads in flight per lane
 __global__ __launch_bounds__(kBlock) void any_equal_kernel(const uint8_t *__restrict__ x, int64_t n,
                                                            uint32_t value, int32_t *__restrict__ flag) {
+  constexpr int kU = 4;
   bool hit = false;
   const int64_t nvec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) ? n / 16 : 0;
   const u32x4 *xv = reinterpret_cast<const u32x4 *>(x);
   const uint32_t pat = value * 0x01010101u;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nvec;
-       i += (int64_t)gridDim.x * kBlock) {
-    u32x4 v = xv[i];
-    uint32_t w[4] = {v.x ^ pat, v.y ^ pat, v.z ^ pat, v.w ^ pat};
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (; i + (kU - 1) * stride < nvec; i += kU * stride) {
+    u32x4 v[kU];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      hit |= ((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) != 0;  // some byte is zero
+    for (int u = 0; u < kU; ++u) v[u] = ld_stream(xv + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) hit |= has_byte(v[u], pat);
   }
-  for (int64_t i = nvec * 16 + (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kBlock)
-    hit |= x[i] == value;
-  if (__any(hit) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1);
+  for (; i < nvec; i += stride) hit |= has_byte(ld_stream(xv + i), pat);
+  for (int64_t j = nvec * 16 + (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += stride)
+    hit |= x[j] == value;
+  // one plain store per hitting workgroup: thousands of same-address atomics
+  // serialise at ~10 ns each (they cost more than the scan)
+  if (__syncthreads_or(hit) && threadIdx.x == 0) *flag = 1;
 }
 
 }  // namespace kvecc
@@ -128,7 +160,7 @@ KVECC_API int kvecc_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *o
   if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
     const int64_t chunks = inner / 16;
     const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
-    hipLaunchKernelGGL(interp_vec_kernel, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, st,
+    hipLaunchKernelGGL(interp_vec_kernel, dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0, st,
                        reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
                        reinterpret_cast<u32x4 *>(out), outer, len, chunks, gate);
   } else {
@@ -147,7 +179,7 @@ KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int
   if (e != hipSuccess) return set_error(KVECC_EHIP, "any_equal_u8: %s", hipGetErrorString(e));
   if (n == 0) return KVECC_OK;
   if (!x) return set_error(KVECC_EINVAL, "any_equal_u8: null input");
-  hipLaunchKernelGGL(any_equal_kernel, dim3(grid_for(n, (int64_t)kBlock * 16, 4)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(any_equal_kernel, dim3(grid_for(n, (int64_t)kBlock * 64, 8)), dim3(kBlock), 0,
                      st, x, n, (uint32_t)value, flag);
   return check_launch("any_equal_u8");
 }

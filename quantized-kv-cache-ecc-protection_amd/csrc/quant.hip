@@ -76,6 +76,70 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
   }
 }
 
+// Rows of at most 64 chunks (every row of the shim and the reference's tests):
+// each lane loads its one 16-byte chunk ONCE, non-temporally, and two row
+// groups are in flight per iteration.
+template <typename T, int VEC>
+__global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__restrict__ x, int codec,
+                                                                    uint8_t *__restrict__ cw,
+                                                                    float *__restrict__ scales,
+                                                                    int64_t rows, int64_t d, int lpr) {
+  static_assert(sizeof(T) * VEC == 16, "one 16-byte chunk per lane");
+  constexpr int kU = 2;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int rows_per_wave = kWave / lpr;
+  const int sub = lane / lpr, li = lane % lpr;
+  const int64_t nchunk = d / VEC;
+  const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
+  const int64_t wave_id = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  const int64_t step = waves * rows_per_wave;
+  for (int64_t r0 = wave_id * rows_per_wave; r0 < rows; r0 += kU * step) {
+    Vec<T, VEC> v[kU];
+    bool live[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t r = r0 + u * step + sub;
+      live[u] = r < rows && li < nchunk;
+      if (live[u]) {
+        const u32x4 raw = ld_stream(reinterpret_cast<const u32x4 *>(x + r * d + li * VEC));
+        __builtin_memcpy(&v[u], &raw, 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t r = r0 + u * step + sub;
+      float f[VEC];
+      float amax = 0.0f;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        f[k] = live[u] ? to_f32<T>(v[u].v[k]) : 0.0f;
+        amax = fmaxf(amax, fabsf(f[k]));
+      }
+      amax = row_max(amax, lpr);
+      const float scale = row_scale(amax);
+      if (!live[u]) continue;
+      if (li == 0) scales[r] = scale;
+      // four quantized nibbles per word, encoded SWAR (codec_math.h)
+      uint32_t wds[VEC / 4];
+#pragma unroll
+      for (int k = 0; k < VEC / 4; ++k) {
+        uint32_t wq = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) wq |= quantize_nibble(f[4 * k + e], scale) << (8 * e);
+        wds[k] = codec == KVECC_CODEC_H84 ? h84_encode4(wq)
+                 : codec == KVECC_CODEC_H74 ? h74_encode4(wq)
+                                            : wq;
+      }
+      if (VEC == 8) {
+        uint64_t bits = (uint64_t)wds[0] | (uint64_t)wds[VEC / 4 - 1] << 32;
+        st_stream(reinterpret_cast<uint64_t *>(cw + r * d + li * VEC), bits);
+      } else {
+        st_stream(reinterpret_cast<uint32_t *>(cw + r * d + li * VEC), wds[0]);
+      }
+    }
+  }
+}
+
 // Hamming(8,4) decode of one codeword byte: data, type (codec_math.h h84_decode4)
 __device__ __forceinline__ uint32_t dec84(uint32_t c, uint32_t &type) {
   uint32_t data, n1 = 0, n2 = 0;
@@ -112,6 +176,56 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_kernel(const uint8_t *_
   if (stats) flush_stats2(stats, n1, n2);
 }
 
+// 16 / sizeof(TO) codewords per lane per access (4 for fp32, 8 for fp16/bf16;
+// d must be a multiple): each lane reads 4 or 8 codeword bytes and writes one
+// contiguous 16-byte output vector, so every wave-instruction covers one
+// contiguous span; non-temporal, kU accesses in flight per lane.  Row indices
+// use 32-bit division (64-bit division is ~100 instructions).
+template <typename TO>
+__global__ __launch_bounds__(kBlock) void decode_dequant_wide_kernel(const uint32_t *__restrict__ cw,
+                                                                     const float *__restrict__ scales,
+                                                                     TO *__restrict__ out,
+                                                                     uint32_t nchunk, uint32_t total,
+                                                                     int zero_doubles,
+                                                                     uint64_t *__restrict__ stats) {
+  constexpr int kU = 4;
+  constexpr int kW = 4 / sizeof(TO);  // codeword words per access
+  using InT = typename std::conditional<kW == 1, uint32_t, u32x2>::type;
+  const uint32_t stride = gridDim.x * kBlock;
+  uint32_t n1 = 0, n2 = 0;
+  auto one = [&](InT in, uint32_t i) {
+    uint32_t w[kW];
+    __builtin_memcpy(w, &in, sizeof(in));
+    const float s = scales[i / nchunk];
+    TO o[4 * kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+      uint32_t q, t;
+      h84_decode4(w[k], q, t, n1, n2);
+      if (zero_doubles) {  // double errors -> data 0 (fused_kernels.py:344)
+        const uint32_t dbl = (t >> 1) & ~t & 0x01010101u;  // type == 2
+        q &= ~(dbl * 0xFFu);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[4 * k + e] = from_f32<TO>(((float)(q >> (8 * e) & 0xFFu) - 8.0f) * s);
+    }
+    u32x4 b;
+    __builtin_memcpy(&b, o, 16);
+    st_stream(reinterpret_cast<u32x4 *>(out) + i, b);
+  };
+  const InT *src = reinterpret_cast<const InT *>(cw);
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  for (; i + (kU - 1) * stride < total; i += kU * stride) {
+    InT w[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) w[u] = ld_stream(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) one(w[u], i + u * stride);
+  }
+  for (; i < total; i += stride) one(ld_stream(src + i), i);
+  if (stats) flush_stats2(stats, n1, n2);
+}
+
 static int lanes_per_row(int64_t chunks) {
   int l = 1;
   while (l < chunks && l < kWave) l <<= 1;
@@ -124,7 +238,12 @@ static void launch_qe(const void *x, int codec, uint8_t *cw, float *scales, int6
   constexpr int V = 16 / sizeof(T);
   const T *xt = reinterpret_cast<const T *>(x);
   bool vec = d % V == 0 && aligned(x, 16) && aligned(cw, V);
-  if (vec) {
+  if (vec && d / V <= kWave) {
+    int lpr = lanes_per_row(d / V);
+    int64_t waves = cdiv(rows, kWave / lpr);
+    hipLaunchKernelGGL((quantize_encode_1c_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave, 16)),
+                       dim3(kBlock), 0, st, xt, codec, cw, scales, rows, d, lpr);
+  } else if (vec) {
     int lpr = lanes_per_row(d / V);
     int64_t waves = cdiv(rows, kWave / lpr);
     hipLaunchKernelGGL((quantize_encode_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave)),
@@ -141,7 +260,13 @@ template <typename TO>
 static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t rows, int64_t d,
                       int zero_doubles, uint64_t *stats, hipStream_t st) {
   TO *o = reinterpret_cast<TO *>(out);
-  if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
+  constexpr int kCw = 16 / sizeof(TO);  // codewords per 16-byte output vector
+  if (d % kCw == 0 && aligned(cw, kCw) && aligned(out, 16) && rows * d < 0xFFFFFFFFLL) {
+    const uint32_t total = (uint32_t)(rows * (d / kCw));
+    hipLaunchKernelGGL((decode_dequant_wide_kernel<TO>), dim3(grid_for(total, kBlock * 4, 16)),
+                       dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o,
+                       (uint32_t)(d / kCw), total, zero_doubles, stats);
+  } else if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
     int64_t total = rows * (d / 4);
     hipLaunchKernelGGL((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),
                        0, st, cw, scales, o, rows, d, zero_doubles, stats);

@@ -284,6 +284,29 @@ def test_interp_fast_path_keeps_values(gpu):
     assert kvecc.interpolate_double_errors(q, e).tolist() == [15, 15, 3, 15]
 
 
+def test_interp_vector_gate_pass(gpu):
+    """No double errors: the vector path's device gate copies q unchanged (no clamp)."""
+    import kvecc
+    g = torch.Generator().manual_seed(4)
+    q = torch.randint(0, 256, (16, 64, 48), generator=g, dtype=torch.uint8)
+    e = torch.randint(0, 2, (16, 64, 48), generator=g, dtype=torch.uint8) * 3  # 0 or 3
+    out = kvecc.interpolate_double_errors(q.to(gpu), e.to(gpu), seq_dim=1)
+    assert torch.equal(out.cpu(), q)
+
+
+@pytest.mark.parametrize("n,offset", [(1, 0), (17, 3), ((1 << 20) + 5, 0), ((1 << 22) + 77, 1)])
+def test_any_equal(gpu, n, offset):
+    from kvecc import ops
+    g = torch.Generator().manual_seed(n)
+    base = torch.randint(0, 2, (n + offset,), generator=g, dtype=torch.uint8)  # values 0/1
+    x = base.to(gpu)[offset:]
+    assert int(ops.any_equal(x, 2)) == 0
+    for pos in (0, n // 2, n - 1):
+        y = x.clone()
+        y[pos] = 2
+        assert int(ops.any_equal(y, 2)) == 1, pos
+
+
 # ---------------------------------------------------------------------------
 # Fused quantize/encode, decode/dequantize
 # ---------------------------------------------------------------------------
@@ -320,6 +343,22 @@ def test_quantize_vs_torch_path(gpu, oracle, dtype, shape):
     out, nc = kvecc.fused_decode_dequantize_hamming84(cw, s84, output_dtype=dtype)
     ref, _ = oracle.decode_dequant_h84(oracle.hamming84_encode(oq), os_)
     assert torch.equal(out.cpu(), torch.from_numpy(ref).to(dtype)) and nc == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(4096, 128), (100, 64), (9, 48), (3, 20)])
+def test_decode_dequant_noisy_vs_cpu_backend(gpu, dtype, shape):
+    """Noisy codewords (singles corrected, doubles zeroed) equal the host backend."""
+    import kvecc
+    from kvecc import cpu_ops
+    g = torch.Generator().manual_seed(shape[0])
+    x = torch.randn(*shape, generator=g) * 2
+    cw, s = cpu_ops.fused_quantize_encode_hamming84(x)
+    noisy = cpu_ops.inject_bit_errors_triton(cw, 0.03, 8, seed=5)
+    ref, nc_ref = cpu_ops.fused_decode_dequantize_hamming84(noisy, s, output_dtype=dtype)
+    out, nc = kvecc.fused_decode_dequantize_hamming84(noisy.to(gpu), s.to(gpu), output_dtype=dtype)
+    assert nc == nc_ref and nc > 0
+    assert torch.equal(out.cpu(), ref)
 
 
 # ---------------------------------------------------------------------------

@@ -38,7 +38,7 @@ def timed(fn, flush, rounds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=10)
-    ap.add_argument("--which", default="golay,hamming,inject,copy")
+    ap.add_argument("--which", default="golay,hamming,inject,copy,interp,fused")
     args = ap.parse_args()
     which = set(args.which.split(","))
     from kvecc import ops
@@ -109,6 +109,48 @@ def main():
         out = torch.empty_like(flat)
         med, mn = timed(lambda: ops.inject_into(flat, out, 1e-3, 8, seed=42), flush, 3)
         res["inject_u8_nb8"] = {"us": med, "philox_per_s": n * 8 / med * 1e6}
+
+    if "interp" in which:
+        # H84 decode output of [8,4096,32,128] interpolated along L (seq_dim=1):
+        # q, err in and out: 3 B/element
+        q = x.clone()
+        err = (torch.rand(B, L, H, D, generator=g) < 0.01).to(torch.uint8).mul_(2).to(dev)
+        out = torch.empty_like(q)
+        n = q.numel()
+        outer, length, inner = B, L, H * D
+        flag = ops.any_equal(err.view(-1), 2)
+        variants = {
+            "interp_vec": lambda: ops.interpolate_into(q.view(-1), err.view(-1), out.view(-1),
+                                                       outer, length, inner),
+            "interp_vec_gated": lambda: ops.interpolate_into(q.view(-1), err.view(-1), out.view(-1),
+                                                             outer, length, inner, gate=flag),
+            "any_equal": lambda: ops.any_equal(err.view(-1), 2, flag),
+        }
+        for k, fn in variants.items():
+            med, mn = timed(fn, flush, args.rounds)
+            byts = n if k == "any_equal" else 3 * n
+            res[k] = {"us": med, "min_us": mn, "GBps": byts / med / 1e3}
+
+    if "fused" in which:
+        rows, d = B * L * H, D
+        xf = torch.randn(rows, d, generator=g).to(torch.float16).to(dev)
+        cw = torch.empty(rows, d, dtype=torch.uint8, device=dev)
+        sc = torch.empty(rows, dtype=torch.float32, device=dev)
+        ops.quantize_encode_rows_into(xf, 2, cw, sc)
+        out16 = torch.empty(rows, d, dtype=torch.float16, device=dev)
+        out32 = torch.empty(rows, d, dtype=torch.float32, device=dev)
+        st = ops.new_stats(dev)
+        variants = {
+            "quantize_encode_h84_fp16": (lambda: ops.quantize_encode_rows_into(xf, 2, cw, sc),
+                                         rows * (3 * d + 4)),
+            "decode_dequant_h84_fp16": (lambda: ops.decode_dequant_h84_into(cw, sc, out16, True, st),
+                                        rows * (3 * d + 4)),
+            "decode_dequant_h84_fp32": (lambda: ops.decode_dequant_h84_into(cw, sc, out32, True, st),
+                                        rows * (5 * d + 4)),
+        }
+        for k, (fn, byts) in variants.items():
+            med, mn = timed(fn, flush, args.rounds)
+            res[k] = {"us": med, "min_us": mn, "GBps": byts / med / 1e3}
 
     print(json.dumps(res, indent=1))
 
