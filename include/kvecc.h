@@ -157,6 +157,20 @@ KVECC_API int kvecc_decode_dequant_h84_rows(const uint8_t *cw, const float *scal
                                             int out_dtype, int64_t rows, int64_t d,
                                             int zero_doubles, uint64_t *stats, void *stream);
 
+/* ---- Packed Golay storage (native layout, not the reference's) -- */
+/* values as INT4 nibbles two per byte (value j in byte j/2, low nibble first),
+ * codewords as 3 little-endian bytes (data12 | parity12 << 12, as
+ * golay_triton.py:130-155), so codeword k covers values 3k..3k+2.
+ * nibbles: ceil(3m/2) bytes; codewords: 3m bytes; uncorrectable (may be NULL):
+ * ceil(m/8) bytes, bit k%8 of byte k/8 = codeword k uncorrectable (data kept);
+ * stats[0] += bits corrected, stats[1] += #uncorrectable.  Decode moves 4.625 B
+ * per codeword (reference layout: 8), encode 4.5 B (reference: 7). */
+KVECC_API int kvecc_golay_encode_packed(const uint8_t *nibbles, uint8_t *codewords, int64_t m,
+                                        void *stream);
+KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                        uint8_t *uncorrectable, int64_t m, uint64_t *stats,
+                                        void *stream);
+
 /* ---- ECC shim: KV-cache write and read -------------------------------------- */
 /* ecc_shim.py:557-721 (ECCBackend.write) for codec KVECC_CODEC_NONE (int4),
  * H74, H84, GOLAY in ONE launch: K and V [batch, seq, hkv*d] (x_dtype,
@@ -230,6 +244,11 @@ KVECC_API int kvecc_cpu_golay_encode_rows(const uint8_t *nibbles, int32_t *codew
                                           int64_t d, int threads);
 KVECC_API int kvecc_cpu_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles, int64_t rows,
                                           int64_t d, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_golay_encode_packed(const uint8_t *nibbles, uint8_t *codewords, int64_t m,
+                                            int threads);
+KVECC_API int kvecc_cpu_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                            uint8_t *uncorrectable, int64_t m, uint64_t *stats,
+                                            int threads);
 KVECC_API int kvecc_cpu_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
                                   int n_bits, int64_t seed, float ber, int64_t global_n,
                                   int64_t offset0, uint64_t *stats, int threads);

@@ -265,6 +265,76 @@ KVECC_API int kvecc_cpu_golay_decode_rows(const int32_t *cw, uint8_t *nibbles, i
   return KVECC_OK;
 }
 
+// packed Golay storage (host twins of packed.hip): one group of 8 codewords
+// (12 nibble bytes, 24 codeword bytes, 1 flag byte) per work item
+KVECC_API int kvecc_cpu_golay_encode_packed(const uint8_t *nibbles, uint8_t *codewords, int64_t m,
+                                            int threads) {
+  if (m < 0) return set_error(KVECC_EINVAL, "cpu_golay_encode_packed: negative m");
+  if (m && (!nibbles || !codewords)) return set_error(KVECC_EINVAL, "cpu_golay_encode_packed: null pointer");
+  static uint16_t par[4096];
+  static bool ready = [] { build_golay_parity_table(par); return true; }();
+  (void)ready;
+  parallel_for((m + 7) / 8, threads, 1, [&](int64_t b, int64_t e, int) {
+    for (int64_t g = b; g < e; ++g)
+      for (int64_t k = 8 * g; k < m && k < 8 * g + 8; ++k) {
+        uint32_t d = 0;
+        for (int u = 0; u < 3; ++u) {
+          const int64_t j = 3 * k + u;
+          d |= (uint32_t)(nibbles[j >> 1] >> (4 * (j & 1)) & 0xF) << (4 * u);
+        }
+        const uint32_t c = d | (uint32_t)par[d] << 12;
+        codewords[3 * k] = (uint8_t)c;
+        codewords[3 * k + 1] = (uint8_t)(c >> 8);
+        codewords[3 * k + 2] = (uint8_t)(c >> 16);
+      }
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                            uint8_t *uncorrectable, int64_t m, uint64_t *stats,
+                                            int threads) {
+  if (m < 0) return set_error(KVECC_EINVAL, "cpu_golay_decode_packed: negative m");
+  if (m && (!nibbles || !codewords)) return set_error(KVECC_EINVAL, "cpu_golay_decode_packed: null pointer");
+  static uint16_t tab[8192];
+  static bool ready = [] {
+    build_golay_parity_table(tab);
+    build_golay_correct_table(tab + 4096);
+    return true;
+  }();
+  (void)ready;
+  const int64_t groups = (m + 7) / 8;
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, groups, 1 << 10)));
+  parallel_for(groups, threads, 1, [&](int64_t b, int64_t e, int t) {
+    uint64_t bits = 0, unc = 0;
+    for (int64_t g = b; g < e; ++g) {
+      uint32_t fl = 0;
+      for (int64_t k = 8 * g; k < m && k < 8 * g + 8; ++k) {
+        const uint32_t c = codewords[3 * k] | (uint32_t)codewords[3 * k + 1] << 8 |
+                           (uint32_t)codewords[3 * k + 2] << 16;
+        uint32_t cnt;
+        const uint32_t d = golay_decode1(c, tab, tab + 4096, cnt);
+        bits += cnt & 3u;
+        unc += cnt >> 2;
+        fl |= (cnt >> 2) << (k - 8 * g);
+        for (int u = 0; u < 3; ++u) {
+          const int64_t j = 3 * k + u;
+          const uint32_t v = d >> (4 * u) & 0xFu;
+          if ((j & 1) == 0)
+            nibbles[j >> 1] = (uint8_t)v;  // high nibble: next value, or zero padding
+          else
+            nibbles[j >> 1] = (uint8_t)((nibbles[j >> 1] & 0x0Fu) | v << 4);
+        }
+      }
+      if (uncorrectable) uncorrectable[g] = (uint8_t)fl;
+    }
+    acc[t].a += bits;
+    acc[t].b += unc;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
 }  // extern "C"
 
 template <typename T>

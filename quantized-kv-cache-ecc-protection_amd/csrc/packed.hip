@@ -1,0 +1,286 @@
+// packed.hip -- Golay(24,12) over packed storage.
+//
+// The reference's layout spends 4 B on a 24-bit codeword (int32) and 1 B on a
+// 4-bit value (uint8 triplets), so its decode moves 8 B per codeword.  This is
+// an additional, native layout -- not a replacement of the reference API:
+//   * values:    INT4 nibbles two per byte, value j in byte j/2 (low nibble
+//                first), so codeword k's 12 data bits are bits 12k..12k+11 of
+//                the little-endian nibble stream;
+//   * codewords: 3 little-endian bytes each (bits 24k..24k+23 of the stream),
+//                same bit layout as the reference's data12 | parity12 << 12;
+//   * decode flags: one bit per codeword (1 = uncorrectable, data kept), eight
+//                codewords per byte.
+// Decode moves 3 + 1.5 + 0.125 = 4.625 B per codeword, encode 1.5 + 3 = 4.5 B.
+//
+// gfx950 design: a lane owns groups of 8 codewords = 12 B of nibbles + 24 B of
+// codewords (word aligned), kPkGroups groups per lane per tile.  Every
+// wave-instruction covers one contiguous span: nibbles move as 12 B per lane;
+// encode stores codewords as a 16 B + 8 B pair per lane regrouped through LDS
+// (with a plain 24 B lane stride packed encode ran at 3.4 TB/s).
+// Parity / correction tables in LDS as in golay.hip; all HBM accesses
+// non-temporal.
+#include "kvecc_internal.h"
+
+namespace kvecc {
+
+constexpr int kPkGroups = 2;
+constexpr int kPkBlock = 512;
+constexpr int kPkTile = kPkBlock * kPkGroups * 8;  // codewords per workgroup tile
+constexpr int kPkWaveCw = kWave * kPkGroups * 8;
+
+// 12 data words of a group <-> 3 nibble words (96 bits)
+__device__ __forceinline__ void nib_unpack8(const uint32_t n[3], uint32_t d[8]) {
+  d[0] = n[0] & 0xFFFu;
+  d[1] = (n[0] >> 12) & 0xFFFu;
+  d[2] = (n[0] >> 24) | (n[1] & 0xFu) << 8;
+  d[3] = (n[1] >> 4) & 0xFFFu;
+  d[4] = (n[1] >> 16) & 0xFFFu;
+  d[5] = (n[1] >> 28) | (n[2] & 0xFFu) << 4;
+  d[6] = (n[2] >> 8) & 0xFFFu;
+  d[7] = n[2] >> 20;
+}
+__device__ __forceinline__ void nib_pack8(const uint32_t d[8], uint32_t n[3]) {
+  n[0] = d[0] | d[1] << 12 | d[2] << 24;
+  n[1] = d[2] >> 8 | d[3] << 4 | d[4] << 16 | d[5] << 28;
+  n[2] = d[5] >> 4 | d[6] << 8 | d[7] << 20;
+}
+// 8 24-bit codewords <-> 6 words (192 bits)
+__device__ __forceinline__ void cw_unpack8(const uint32_t w[6], uint32_t c[8]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t a = w[3 * h], b = w[3 * h + 1], e = w[3 * h + 2];
+    c[4 * h + 0] = a & 0xFFFFFFu;
+    c[4 * h + 1] = (a >> 24) | (b & 0xFFFFu) << 8;
+    c[4 * h + 2] = (b >> 16) | (e & 0xFFu) << 16;
+    c[4 * h + 3] = e >> 8;
+  }
+}
+__device__ __forceinline__ void cw_pack8(const uint32_t c[8], uint32_t w[6]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t *x = c + 4 * h;
+    w[3 * h] = x[0] | x[1] << 24;
+    w[3 * h + 1] = x[1] >> 8 | x[2] << 16;
+    w[3 * h + 2] = x[2] >> 16 | x[3] << 8;
+  }
+}
+
+__device__ __forceinline__ void load_tables_pk(uint16_t *lds, const uint16_t *par,
+                                               const uint16_t *cor, bool need_cor) {
+  const u32x4 *p = reinterpret_cast<const u32x4 *>(par);
+  u32x4 *l = reinterpret_cast<u32x4 *>(lds);
+  for (int i = threadIdx.x; i < 512; i += kPkBlock) l[i] = p[i];
+  if (need_cor) {
+    const u32x4 *c = reinterpret_cast<const u32x4 *>(cor);
+    for (int i = threadIdx.x; i < 512; i += kPkBlock) l[512 + i] = c[i];
+  }
+  __syncthreads();
+}
+
+// A wave's 64 groups of codewords are 1536 contiguous bytes: in HBM they move as
+// one 16-byte and one 8-byte access per lane (1024 + 512 B, each contiguous
+// across the wave) and are regrouped to 24 bytes per lane through LDS.
+constexpr int kWaveCwBytes = kWave * 24;
+typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+
+__global__ __launch_bounds__(kPkBlock) void golay_encode_packed_kernel(
+    const uint32_t *__restrict__ nib, uint32_t *__restrict__ cw, int64_t ntiles,
+    const uint16_t *__restrict__ par) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[4096];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kPkBlock / kWave][kPkGroups][kWaveCwBytes];
+  load_tables_pk(lds, par, nullptr, false);
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t G0 = (t * kPkTile + wave * kPkWaveCw) / 8;  // first group of this wave
+    u32x3v n[kPkGroups];
+#pragma unroll
+    for (int g = 0; g < kPkGroups; ++g)
+      n[g] = ld_stream(reinterpret_cast<const u32x3v *>(nib + (G0 + g * kWave + lane) * 3));
+#pragma unroll
+    for (int g = 0; g < kPkGroups; ++g) {
+      const uint32_t nn[3] = {n[g].x, n[g].y, n[g].z};
+      uint32_t d[8], c[8], w[6];
+      nib_unpack8(nn, d);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c[k] = d[k] | (uint32_t)lds[d[k]] << 12;
+      cw_pack8(c, w);
+      u32x2 *dst = reinterpret_cast<u32x2 *>(&stage[wave][g][24 * lane]);
+      dst[0] = u32x2{w[0], w[1]};
+      dst[1] = u32x2{w[2], w[3]};
+      dst[2] = u32x2{w[4], w[5]};
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < kPkGroups; ++g) {
+      uint8_t *out = reinterpret_cast<uint8_t *>(cw) + (G0 + g * kWave) * 24;
+      st_stream(reinterpret_cast<u32x4 *>(out) + lane,
+                *reinterpret_cast<const u32x4 *>(&stage[wave][g][16 * lane]));
+      st_stream(reinterpret_cast<u32x2 *>(out + 1024) + lane,
+                *reinterpret_cast<const u32x2 *>(&stage[wave][g][1024 + 8 * lane]));
+    }
+    __syncthreads();
+  }
+}
+
+// decode reads its 24 B per lane directly as three 8-byte loads (the three
+// instructions of a wave together cover the wave's 1536 contiguous bytes);
+// regrouping through LDS as in encode measured slower here (48 vs 44 us)
+template <bool WITH_FLAGS, bool WITH_STATS>
+__global__ __launch_bounds__(kPkBlock) void golay_decode_packed_kernel(
+    const uint32_t *__restrict__ cw, uint32_t *__restrict__ nib, uint8_t *__restrict__ flags,
+    int64_t ntiles, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
+    uint64_t *__restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[8192];
+  load_tables_pk(lds, par, cor, true);
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  uint32_t bits = 0, unc = 0;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t G0 = (t * kPkTile + wave * kPkWaveCw) / 8;
+    u32x2 p[kPkGroups][3];
+#pragma unroll
+    for (int g = 0; g < kPkGroups; ++g) {
+      const u32x2 *src = reinterpret_cast<const u32x2 *>(cw + (G0 + g * kWave + lane) * 6);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) p[g][k] = ld_stream(src + k);
+    }
+#pragma unroll
+    for (int g = 0; g < kPkGroups; ++g) {
+      const uint32_t w[6] = {p[g][0].x, p[g][0].y, p[g][1].x, p[g][1].y, p[g][2].x, p[g][2].y};
+      uint32_t c[8], d[8], n[3], fl = 0;
+      cw_unpack8(w, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t cnt;
+        d[k] = golay_decode1(c[k], lds, lds + 4096, cnt);
+        bits += cnt & 3u;
+        unc += cnt >> 2;
+        fl |= (cnt >> 2) << k;
+      }
+      nib_pack8(d, n);
+      st_stream(reinterpret_cast<u32x3v *>(nib + (G0 + g * kWave + lane) * 3), u32x3v{n[0], n[1], n[2]});
+      if (WITH_FLAGS) st_stream(flags + G0 + g * kWave + lane, (uint8_t)fl);
+    }
+  }
+  if (WITH_STATS) flush_stats2<kPkBlock>(stats, bits, unc);
+}
+
+// ---- scalar tails (< one tile), byte accesses -----------------------------------
+
+__device__ __forceinline__ uint32_t get_nib(const uint8_t *p, int64_t j) {
+  return (p[j >> 1] >> (4 * (j & 1))) & 0xFu;
+}
+// encode: one thread per codeword (nibble bytes are only read)
+__global__ __launch_bounds__(kBlock) void golay_encode_packed_tail_kernel(
+    const uint8_t *__restrict__ nib, uint8_t *__restrict__ cw, int64_t begin, int64_t m,
+    const uint16_t *__restrict__ par) {
+  const int64_t k = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= m) return;
+  const uint32_t d = get_nib(nib, 3 * k) | get_nib(nib, 3 * k + 1) << 4 | get_nib(nib, 3 * k + 2) << 8;
+  const uint32_t c = d | (uint32_t)par[d] << 12;
+  cw[3 * k] = (uint8_t)c;
+  cw[3 * k + 1] = (uint8_t)(c >> 8);
+  cw[3 * k + 2] = (uint8_t)(c >> 16);
+}
+
+template <bool WITH_FLAGS, bool WITH_STATS>
+__global__ __launch_bounds__(kBlock) void golay_decode_packed_tail_kernel(
+    const uint8_t *__restrict__ cw, uint8_t *__restrict__ nib, uint8_t *__restrict__ flags,
+    int64_t begin, int64_t m, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
+    uint64_t *__restrict__ stats) {
+  // a single thread walks the (< one tile) tail sequentially: groups share bytes
+  uint32_t bits = 0, unc = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    for (int64_t g = begin / 8; g * 8 < m; ++g) {
+      uint32_t fl = 0;
+      for (int64_t k = g * 8; k < m && k < g * 8 + 8; ++k) {
+        const uint32_t c = cw[3 * k] | (uint32_t)cw[3 * k + 1] << 8 | (uint32_t)cw[3 * k + 2] << 16;
+        uint32_t cnt;
+        const uint32_t d = golay_decode1(c, par, cor, cnt);
+        bits += cnt & 3u;
+        unc += cnt >> 2;
+        fl |= (cnt >> 2) << (k - g * 8);
+        for (int e = 0; e < 3; ++e) {
+          const int64_t j = 3 * k + e;
+          const uint32_t v = d >> (4 * e) & 0xFu;
+          if ((j & 1) == 0)
+            nib[j >> 1] = (uint8_t)v;  // high nibble: next value, or zero padding
+          else
+            nib[j >> 1] = (uint8_t)((nib[j >> 1] & 0x0Fu) | v << 4);
+        }
+      }
+      if (WITH_FLAGS) flags[g] = (uint8_t)fl;
+    }
+  }
+  if (WITH_STATS) flush_stats2(stats, bits, unc);
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" {
+
+KVECC_API int kvecc_golay_encode_packed(const uint8_t *nibbles, uint8_t *codewords, int64_t m,
+                                        void *stream) {
+  if (m < 0) return set_error(KVECC_EINVAL, "golay_encode_packed: negative m");
+  if (m == 0) return KVECC_OK;
+  if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "golay_encode_packed: null pointer");
+  const uint16_t *par = golay_parity_table_dev();
+  if (!par) return KVECC_EHIP;
+  hipStream_t st = as_stream(stream);
+  int64_t done = 0;
+  if (aligned(nibbles, 4) && aligned(codewords, 4)) {
+    const int64_t ntiles = m / kPkTile;
+    if (ntiles > 0)
+      hipLaunchKernelGGL(golay_encode_packed_kernel, dim3(grid_for(ntiles, 1, 16)), dim3(kPkBlock), 0,
+                         st, reinterpret_cast<const uint32_t *>(nibbles),
+                         reinterpret_cast<uint32_t *>(codewords), ntiles, par);
+    done = ntiles * kPkTile;
+  }
+  if (done < m)
+    hipLaunchKernelGGL(golay_encode_packed_tail_kernel, dim3((unsigned)cdiv(m - done, kBlock)),
+                       dim3(kBlock), 0, st, nibbles, codewords, done, m, par);
+  return check_launch("golay_encode_packed");
+}
+
+KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                        uint8_t *uncorrectable, int64_t m, uint64_t *stats,
+                                        void *stream) {
+  if (m < 0) return set_error(KVECC_EINVAL, "golay_decode_packed: negative m");
+  if (m == 0) return KVECC_OK;
+  if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "golay_decode_packed: null pointer");
+  const uint16_t *par = golay_parity_table_dev(), *cor = golay_correct_table_dev();
+  if (!par || !cor) return KVECC_EHIP;
+  hipStream_t st = as_stream(stream);
+  int64_t done = 0;
+  if (aligned(nibbles, 4) && aligned(codewords, 4)) {
+    const int64_t ntiles = m / kPkTile;
+    if (ntiles > 0) {
+      const dim3 grid(grid_for(ntiles, 1, 32)), block(kPkBlock);
+      const uint32_t *c = reinterpret_cast<const uint32_t *>(codewords);
+      uint32_t *n = reinterpret_cast<uint32_t *>(nibbles);
+      if (uncorrectable && stats)
+        hipLaunchKernelGGL((golay_decode_packed_kernel<true, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+      else if (uncorrectable)
+        hipLaunchKernelGGL((golay_decode_packed_kernel<true, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+      else if (stats)
+        hipLaunchKernelGGL((golay_decode_packed_kernel<false, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+      else
+        hipLaunchKernelGGL((golay_decode_packed_kernel<false, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+    }
+    done = ntiles * kPkTile;
+  }
+  if (done < m) {
+    if (uncorrectable && stats)
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, true>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+    else if (uncorrectable)
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, false>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+    else if (stats)
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, true>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+    else
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, false>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+  }
+  return check_launch("golay_decode_packed");
+}
+
+}  // extern "C"

@@ -47,6 +47,8 @@ SIGNATURES = {
     "kvecc_any_equal_u8": [_vp, _i64, _u8, _vp, _vp],
     "kvecc_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _vp],
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
+    "kvecc_golay_encode_packed": [_vp, _vp, _i64, _vp],
+    "kvecc_golay_decode_packed": [_vp, _vp, _vp, _i64, _vp, _vp],
     "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
     "kvecc_paged_attention_workspace": [_i64, _i64, _i64, _i64],
@@ -61,6 +63,8 @@ SIGNATURES = {
     "kvecc_cpu_golay_decode": [_vp, _vp, _vp, _i64, _vp, _int],
     "kvecc_cpu_golay_encode_rows": [_vp, _vp, _i64, _i64, _int],
     "kvecc_cpu_golay_decode_rows": [_vp, _vp, _i64, _i64, _vp, _int],
+    "kvecc_cpu_golay_encode_packed": [_vp, _vp, _i64, _int],
+    "kvecc_cpu_golay_decode_packed": [_vp, _vp, _vp, _i64, _vp, _int],
     "kvecc_cpu_inject_u8_vectorized": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _vp, _int],
     "kvecc_cpu_inject_i32_vectorized": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _vp, _int],
     "kvecc_cpu_inject_rows_u8": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _int],

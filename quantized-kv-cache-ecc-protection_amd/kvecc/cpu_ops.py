@@ -508,3 +508,40 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
                          v_scales.to(torch.float32).contiguous(), out, layer_idx, block_size,
                          sm_scale, codec)
     return out
+
+
+# ============================================================================
+# Packed Golay storage (host twins of ops.golay_encode_packed / decode_packed)
+# ============================================================================
+
+from .ops import pack_nibbles, unpack_nibbles  # noqa: E402  (pure torch, device-agnostic)
+
+
+def golay_encode_packed(nibbles: torch.Tensor, m: int) -> torch.Tensor:
+    _check_cpu(nibbles)
+    nib = nibbles.reshape(-1)
+    if nib.dtype != torch.uint8 or nib.numel() < (3 * m + 1) // 2:
+        raise ValueError(f"need {(3 * m + 1) // 2} packed uint8 nibble bytes for {m} codewords")
+    nib = nib.contiguous()
+    out = torch.empty(3 * m, dtype=torch.uint8)
+    _lib.call("kvecc_cpu_golay_encode_packed", _ptr(nib), _ptr(out), int(m), NUM_THREADS)
+    return out
+
+
+def golay_decode_packed(codewords: torch.Tensor, m: int, return_uncorrectable: bool = False,
+                        stats=None):
+    _check_cpu(codewords)
+    cw = codewords.reshape(-1)
+    if cw.dtype != torch.uint8 or cw.numel() < 3 * m:
+        raise ValueError(f"need {3 * m} uint8 codeword bytes for {m} codewords")
+    cw = cw.contiguous()
+    nib = torch.empty((3 * m + 1) // 2, dtype=torch.uint8)
+    flags = torch.empty((m + 7) // 8, dtype=torch.uint8) if return_uncorrectable else None
+    st = _stats() if stats is None else stats
+    _lib.call("kvecc_cpu_golay_decode_packed", _ptr(cw), _ptr(nib), _ptr(flags), int(m), _ptr(st),
+              NUM_THREADS)
+    if stats is not None:
+        return (nib, flags) if return_uncorrectable else nib
+    if return_uncorrectable:
+        return nib, flags, (int(st[0]), int(st[1]))
+    return nib, (int(st[0]), int(st[1]))

@@ -583,3 +583,59 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
                          v_scales.to(torch.float32).contiguous(), out, layer_idx, block_size,
                          sm_scale, codec)
     return out
+
+
+# ============================================================================
+# Packed Golay storage (native layout; include/kvecc.h "Packed Golay storage")
+# ============================================================================
+
+def pack_nibbles(values: torch.Tensor) -> torch.Tensor:
+    """INT4 values (uint8, low nibble) -> bytes, two per byte, low nibble first."""
+    flat = values.reshape(-1).to(torch.uint8)
+    if flat.numel() % 2:
+        flat = torch.cat([flat, flat.new_zeros(1)])
+    pairs = flat.view(-1, 2) & 0xF
+    return (pairs[:, 0] | (pairs[:, 1] << 4)).contiguous()
+
+
+def unpack_nibbles(packed: torch.Tensor, n: int) -> torch.Tensor:
+    """Inverse of pack_nibbles: the first n values as uint8."""
+    p = packed.reshape(-1)
+    return torch.stack([p & 0xF, p >> 4], dim=1).reshape(-1)[:n].contiguous()
+
+
+def golay_encode_packed(nibbles: torch.Tensor, m: int) -> torch.Tensor:
+    """m codewords of the packed nibble stream (3 values each) -> 3m codeword bytes."""
+    _check_gpu(nibbles)
+    nib = nibbles.reshape(-1)
+    if nib.dtype != torch.uint8 or nib.numel() < (3 * m + 1) // 2:
+        raise ValueError(f"need {(3 * m + 1) // 2} packed uint8 nibble bytes for {m} codewords")
+    nib = nib.contiguous()
+    out = torch.empty(3 * m, dtype=torch.uint8, device=nib.device)
+    _ensure_device(nib.device)
+    _lib.call("kvecc_golay_encode_packed", _ptr(nib), _ptr(out), int(m), _stream(nib.device))
+    return out
+
+
+def golay_decode_packed(codewords: torch.Tensor, m: int, return_uncorrectable: bool = False,
+                        stats=None):
+    """3m codeword bytes -> packed nibbles (ceil(3m/2) bytes), (bits_corrected,
+    uncorrectable) [, uncorrectable bitmask ceil(m/8) bytes]."""
+    _check_gpu(codewords)
+    cw = codewords.reshape(-1)
+    if cw.dtype != torch.uint8 or cw.numel() < 3 * m:
+        raise ValueError(f"need {3 * m} uint8 codeword bytes for {m} codewords")
+    cw = cw.contiguous()
+    dev = cw.device
+    nib = torch.empty((3 * m + 1) // 2, dtype=torch.uint8, device=dev)
+    flags = torch.empty((m + 7) // 8, dtype=torch.uint8, device=dev) if return_uncorrectable else None
+    st = new_stats(dev) if stats is None else stats
+    _ensure_device(dev)
+    _lib.call("kvecc_golay_decode_packed", _ptr(cw), _ptr(nib), _ptr(flags), int(m), _ptr(st),
+              _stream(dev))
+    if stats is not None:
+        return (nib, flags) if return_uncorrectable else nib
+    bits, unc = read_stats(st)
+    if return_uncorrectable:
+        return nib, flags, (bits, unc)
+    return nib, (bits, unc)

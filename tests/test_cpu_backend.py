@@ -219,3 +219,34 @@ def test_golay_rows_vs_flat(cpu):
         trip, (bits, unc) = cpu.golay_decode(noisy.reshape(-1))
         assert torch.equal(dec, trip.view(7, 3, 3 * gs)[..., :d])
         assert cpu.read_stats(st) == [bits, unc]
+
+
+def _packed_reference(trip_u8):
+    """Packed layout restated from the reference-layout codec: int32 codewords ->
+    3 little-endian bytes; triplets -> nibble stream two per byte."""
+    from kvecc import cpu_ops
+    cw = cpu_ops.golay_encode(trip_u8.view(-1, 3)).to(torch.int64)
+    cw3 = torch.stack([(cw >> (8 * k)) & 0xFF for k in range(3)], 1).to(torch.uint8).reshape(-1)
+    return cpu_ops.pack_nibbles(trip_u8.reshape(-1)), cw3
+
+
+@pytest.mark.parametrize("m", [1, 2, 7, 8, 9, 100, 8192 * 2 + 5])
+def test_golay_packed_vs_reference_layout(cpu, m):
+    """Packed encode/decode carry exactly the reference layout's bits."""
+    g = torch.Generator().manual_seed(m)
+    trip = torch.randint(0, 16, (m, 3), generator=g, dtype=torch.uint8)
+    nib, cw3 = _packed_reference(trip)
+    assert torch.equal(cpu.golay_encode_packed(nib, m), cw3)
+    # corrupt through the reference-layout path, decode both ways
+    cw = cpu.golay_encode(trip)
+    noisy = cpu.inject_bit_errors_triton(cw, 0.08, 24, seed=3)
+    trip_ref, cnt_ref, (bits, unc) = cpu.golay_decode(noisy, return_error_counts=True)
+    n64 = noisy.to(torch.int64)
+    noisy3 = torch.stack([(n64 >> (8 * k)) & 0xFF for k in range(3)], 1).to(torch.uint8).reshape(-1)
+    out, flags, st = cpu.golay_decode_packed(noisy3, m, return_uncorrectable=True)
+    assert st == (bits, unc)
+    assert torch.equal(cpu.unpack_nibbles(out, 3 * m), trip_ref.reshape(-1))
+    if (3 * m) % 2:
+        assert int(out[-1]) >> 4 == 0  # padding nibble is zero
+    bitmask = torch.tensor([(int(flags[k // 8]) >> (k % 8)) & 1 for k in range(m)], dtype=torch.uint8)
+    assert torch.equal(bitmask, (cnt_ref == 4).to(torch.uint8))

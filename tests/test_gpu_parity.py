@@ -401,3 +401,27 @@ def test_config3_full_size_vs_cpu_backend(gpu):
     trip, cnt, dst = kvecc.golay_decode(noisy, return_error_counts=True)
     assert dst == dst_h
     assert torch.equal(trip.cpu(), trip_h) and torch.equal(cnt.cpu(), cnt_h)
+
+
+@pytest.mark.parametrize("m", [1, 7, 8, 9, 8192 * 2, 8192 * 2 + 5, 45_088_768])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_golay_packed_vs_cpu_backend(gpu, m, offset):
+    """Packed Golay storage: HIP == host backend (which tests pin to the reference
+    layout), including the tail path, unaligned buffers and the full config-3 M."""
+    if offset and m > 100_000:
+        pytest.skip("unaligned full size adds nothing over the small cases")
+    from kvecc import cpu_ops, ops
+    g = torch.Generator().manual_seed(m + offset)
+    nib = torch.randint(0, 256, ((3 * m + 1) // 2 + offset,), generator=g, dtype=torch.uint8)
+    nib_h = nib[offset:].contiguous() if offset == 0 else nib[offset:]
+    cw3_ref = cpu_ops.golay_encode_packed(nib_h, m)
+    nib_d = nib.to(gpu)[offset:]
+    cw3 = ops.golay_encode_packed(nib_d, m)
+    assert torch.equal(cw3.cpu(), cw3_ref)
+    noisy = cpu_ops.inject_bit_errors_triton(cw3_ref, 0.03, 8, seed=9)  # byte-level corruption
+    out_ref, fl_ref, st_ref = cpu_ops.golay_decode_packed(noisy, m, return_uncorrectable=True)
+    buf = torch.zeros(3 * m + offset, dtype=torch.uint8)
+    buf[offset:] = noisy
+    out, fl, st = ops.golay_decode_packed(buf.to(gpu)[offset:], m, return_uncorrectable=True)
+    assert st == st_ref and st_ref[0] > 0
+    assert torch.equal(out.cpu(), out_ref) and torch.equal(fl.cpu(), fl_ref)
