@@ -238,6 +238,7 @@ def main():
         noisy3 = torch.stack([(noisy >> (8 * k)) & 0xFF for k in range(3)], 1).to(torch.uint8)
         noisy3 = noisy3.reshape(-1).contiguous()
         nib_out = torch.empty_like(nib)
+        flags = torch.empty((m + 7) // 8, dtype=torch.uint8, device=dev)  # uncorrectable bits
         pst = ops.new_stats(dev)
         pe = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         for _ in range(args.warmup):
@@ -250,7 +251,7 @@ def main():
                           ops._stream(dev))
             pe[k][1].record()
             ops._lib.call("kvecc_golay_decode_packed", ops._ptr(noisy3), ops._ptr(nib_out),
-                          ops._VP(0), m, ops._ptr(pst), ops._stream(dev))
+                          ops._ptr(flags), m, ops._ptr(pst), ops._stream(dev))
             pe[k][2].record()
         torch.cuda.synchronize()
         p_enc = sum(e[0].elapsed_time(e[1]) for e in pe) / args.steps
