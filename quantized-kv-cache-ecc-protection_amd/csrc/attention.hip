@@ -26,7 +26,7 @@
 
 namespace kvecc {
 
-constexpr int kMaxSplit = 256;    // context tokens per workgroup (upper bound)
+constexpr int kMaxSplit = 1024;   // context tokens per workgroup (upper bound)
 constexpr int kMaxSplits = 1024;  // splits per (batch, head)
 constexpr int kAttnMaxD = 256;
 constexpr int kUnroll = 4;        // token rows in flight per lane group
@@ -113,17 +113,24 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   const int cs = live ? c : 0;
   float *ws = a.ws + (bh * a.nsplit + blockIdx.x) * (a.d + 2);
 
-  {  // one 32-bit division per token, here; none in the streaming loop
+  {  // block-table slice -> LDS (one load per logical block), then one 32-bit
+     // division per token; none in the streaming loop
+    __shared__ int32_t blks[kMaxSplit + 1];
     const uint32_t bs = (uint32_t)a.bs;
+    const uint32_t lb0 = (uint32_t)(t0 / a.bs);
+    const int nlb = ntok > 0 ? (int)((uint32_t)(t1 - 1) / bs - lb0 + 1) : 0;
+    const int32_t *tab = a.table + b * a.max_blocks + lb0;
+    for (int j = threadIdx.x; j < nlb; j += kBlock) blks[j] = tab[j];
+    __syncthreads();
     const int32_t head_row0 = (int32_t)((a.layer * a.kv_heads + hk) * a.bs);
     const int32_t blk_rows = (int32_t)(a.layers * a.kv_heads * a.bs);
-    const int32_t *tab = a.table + b * a.max_blocks;
-    for (int i = threadIdx.x; i < kMaxSplit + (kUnroll - 1) * kBlock; i += kBlock) {
+    const int npad = (int)a.split + (kUnroll - 1) * kBlock;
+    for (int i = threadIdx.x; i < npad; i += kBlock) {
       int32_t row = -1;
       if (i < ntok) {
         const uint32_t pos = (uint32_t)(t0 + i);
         const uint32_t lb = pos / bs;
-        const int32_t blk = tab[lb];
+        const int32_t blk = blks[lb - lb0];
         if (blk >= 0) row = blk * blk_rows + head_row0 + (int32_t)(pos - lb * bs);
       }
       rows[i] = row;
