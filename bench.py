@@ -247,11 +247,9 @@ def main():
         torch.cuda.synchronize()
         for k in range(args.steps):
             pe[k][0].record()
-            ops._lib.call("kvecc_golay_encode_packed", ops._ptr(nib), ops._ptr(cw3), m,
-                          ops._stream(dev))
+            ops.golay_encode_packed_into(nib, cw3, m)
             pe[k][1].record()
-            ops._lib.call("kvecc_golay_decode_packed", ops._ptr(noisy3), ops._ptr(nib_out),
-                          ops._ptr(flags), m, ops._ptr(pst), ops._stream(dev))
+            ops.golay_decode_packed_into(noisy3, nib_out, flags, m, pst)
             pe[k][2].record()
         torch.cuda.synchronize()
         p_enc = sum(e[0].elapsed_time(e[1]) for e in pe) / args.steps

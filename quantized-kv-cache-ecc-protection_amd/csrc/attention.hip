@@ -14,7 +14,7 @@
 // 256 tokens (fewer when batch*heads is small, so the grid still fills the
 // chip), with the split's slice of the block table staged in LDS.  Lanes are
 // grouped W per token row (a lane owns 16 H(8,4) codewords via one 16-byte
-// load, or one Golay codeword); each group streams its rows in ONE pass --
+// load, or 3 Golay codewords); each group streams its rows in ONE pass --
 // kUnroll K and V rows loaded before any is used, the group's partial dot
 // products reduced with __shfl_xor, an online softmax per group -- and the
 // groups merge through LDS.  The split's (max, sum, acc[D]) go to a workspace
@@ -46,10 +46,11 @@ struct AttnArgs {
 };
 
 // Lane chunk c of a token row: VEC 32-bit words = 4*VEC H(8,4) codewords, or
-// one Golay codeword; E values.
+// VEC Golay codewords (3*VEC values; codewords past the row's last are read
+// clamped and contribute nothing, their values fall outside [0, d)); E values.
 template <int CODEC, int VEC>
 struct Chunk {
-  static constexpr int E = CODEC == KVECC_CODEC_H84 ? 4 * VEC : 3;
+  static constexpr int E = CODEC == KVECC_CODEC_H84 ? 4 * VEC : 3 * VEC;
   uint32_t w[VEC];
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
     if (CODEC == KVECC_CODEC_H84) {
@@ -65,7 +66,9 @@ struct Chunk {
         for (int k = 0; k < VEC; ++k) w[k] = reinterpret_cast<const uint32_t *>(p)[k];
       }
     } else {
-      w[0] = (uint32_t)reinterpret_cast<const int32_t *>(cache)[row * a.g + c];
+      const int32_t *p = reinterpret_cast<const int32_t *>(cache) + row * a.g;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) w[k] = (uint32_t)p[min<int64_t>(VEC * c + k, a.g - 1)];
     }
   }
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
@@ -79,10 +82,13 @@ struct Chunk {
         for (int e = 0; e < 4; ++e) v[4 * k + e] = lut[(w[k] >> (8 * e)) & 0xFFu];
       }
     } else {
-      uint32_t cnt;
-      const uint32_t dw = golay_decode1(w[0], gtab, gtab + 4096, cnt);
 #pragma unroll
-      for (int e = 0; e < 3; ++e) v[e] = (float)(dw >> (4 * e) & 0xFu) - 8.0f;
+      for (int k = 0; k < VEC; ++k) {
+        uint32_t cnt;
+        const uint32_t dw = golay_decode1(w[k], gtab, gtab + 4096, cnt);
+#pragma unroll
+        for (int e = 0; e < 3; ++e) v[3 * k + e] = (float)(dw >> (4 * e) & 0xFu) - 8.0f;
+      }
     }
   }
 };
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   const int64_t t0 = (int64_t)blockIdx.x * a.split;
   const int64_t t1 = min<int64_t>(t0 + a.split, ctx);
   const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
-  const bool live = c < a.g / VEC;  // lanes past the row idle (Golay: g < W)
+  const bool live = c < (a.g + VEC - 1) / VEC;  // lanes past the row idle
   const int cs = live ? c : 0;
   float *ws = a.ws + (bh * a.nsplit + blockIdx.x) * (a.d + 2);
 
@@ -295,7 +301,7 @@ static int pow2_at_least(int64_t x) {
 
 template <typename T, int CODEC, int VEC>
 static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
-  const int w = pow2_at_least(a.g / VEC);
+  const int w = pow2_at_least((a.g + VEC - 1) / VEC);
   switch (w) {
 #define KVECC_ATTN_CASE(WW)                                                                       \
   case WW:                                                                                        \
@@ -311,7 +317,7 @@ static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
 #undef KVECC_ATTN_CASE
     default:
       return set_error(KVECC_EINVAL, "paged_attention: %lld lane chunks per token row > 64",
-                       (long long)(a.g / VEC));
+                       (long long)((a.g + VEC - 1) / VEC));
   }
 }
 
@@ -321,6 +327,8 @@ static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
   int rc;
   if (CODEC == KVECC_CODEC_H84 && a.d % 16 == 0)
     rc = launch_split<T, CODEC, 4>(a, grid, st);  // 16-byte loads, 16 codewords per lane
+  else if (CODEC == KVECC_CODEC_GOLAY)
+    rc = launch_split<T, CODEC, 3>(a, grid, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
   else
     rc = launch_split<T, CODEC, 1>(a, grid, st);
   if (rc != KVECC_OK) return rc;
@@ -330,11 +338,14 @@ static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
 
 // tokens per workgroup: the largest power of two <= kMaxSplit that still gives
 // >= 4 workgroups per CU (small batch*heads decode steps split finer)
-static int64_t choose_split(int64_t bh, int64_t max_context_len) {
-  int64_t split = kMaxSplit;
+static int64_t choose_split(int64_t bh, int64_t max_context_len, int codec) {
+  // Golay rows take 16 lanes per token at D=128 (3 codewords each, 4 B loads):
+  // its workgroups stream fewer bytes per pass and prefer more, shorter splits
+  const int64_t top = codec == KVECC_CODEC_GOLAY ? 256 : kMaxSplit;
+  int64_t split = top;
   const int64_t want = 4LL * cu_count();
   while (split > 32 && bh * cdiv(max_context_len, split) < want) split >>= 1;
-  while (cdiv(max_context_len, split) > kMaxSplits && split < kMaxSplit) split <<= 1;
+  while (cdiv(max_context_len, split) > kMaxSplits && split < top) split <<= 1;
   return split;
 }
 
@@ -347,7 +358,9 @@ extern "C" {
 KVECC_API int64_t kvecc_paged_attention_workspace(int64_t batch, int64_t heads, int64_t head_dim,
                                                   int64_t max_context_len) {
   if (batch <= 0 || heads <= 0 || head_dim <= 0 || max_context_len <= 0) return 0;
-  return batch * heads * cdiv(max_context_len, choose_split(batch * heads, max_context_len)) *
+  // sized for the codec with the most splits (Golay) so one size fits both
+  return batch * heads *
+         cdiv(max_context_len, choose_split(batch * heads, max_context_len, KVECC_CODEC_GOLAY)) *
          (head_dim + 2);
 }
 
@@ -402,7 +415,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.layer = layer;
   a.bs = block_size;
   a.max_blocks = max_blocks;
-  a.split = choose_split(batch * heads, max_context_len);
+  a.split = choose_split(batch * heads, max_context_len, codec);
   a.nsplit = cdiv(max_context_len, a.split);
   if (a.nsplit > kMaxSplits)
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);

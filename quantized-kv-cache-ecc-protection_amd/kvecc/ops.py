@@ -604,6 +604,21 @@ def unpack_nibbles(packed: torch.Tensor, n: int) -> torch.Tensor:
     return torch.stack([p & 0xF, p >> 4], dim=1).reshape(-1)[:n].contiguous()
 
 
+def golay_encode_packed_into(nibbles, codewords, m):
+    """Asynchronous packed encode into caller buffers (device pointers, stream)."""
+    _lib.call("kvecc_golay_encode_packed", _ptr(nibbles), _ptr(codewords), int(m),
+              _stream(nibbles.device))
+    return codewords
+
+
+def golay_decode_packed_into(codewords, nibbles, uncorrectable=None, m=None, stats=None):
+    """Asynchronous packed decode into caller buffers; statistics stay on the device."""
+    m = codewords.numel() // 3 if m is None else int(m)
+    _lib.call("kvecc_golay_decode_packed", _ptr(codewords), _ptr(nibbles), _ptr(uncorrectable), m,
+              _ptr(stats), _stream(codewords.device))
+    return nibbles
+
+
 def golay_encode_packed(nibbles: torch.Tensor, m: int) -> torch.Tensor:
     """m codewords of the packed nibble stream (3 values each) -> 3m codeword bytes."""
     _check_gpu(nibbles)
