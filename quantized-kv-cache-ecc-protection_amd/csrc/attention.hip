@@ -338,10 +338,10 @@ static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
 
 // tokens per workgroup: the largest power of two <= kMaxSplit that still gives
 // >= 4 workgroups per CU (small batch*heads decode steps split finer)
-static int64_t choose_split(int64_t bh, int64_t max_context_len, int codec) {
-  // Golay rows take 16 lanes per token at D=128 (3 codewords each, 4 B loads):
-  // its workgroups stream fewer bytes per pass and prefer more, shorter splits
-  const int64_t top = codec == KVECC_CODEC_GOLAY ? 256 : kMaxSplit;
+static int64_t choose_split(int64_t bh, int64_t max_context_len) {
+  // longer splits amortise each workgroup's fixed work (table staging, the
+  // group merge); measured best at 1024 for both codecs at [8,4096,32,128]
+  const int64_t top = kMaxSplit;
   int64_t split = top;
   const int64_t want = 4LL * cu_count();
   while (split > 32 && bh * cdiv(max_context_len, split) < want) split >>= 1;
@@ -358,9 +358,7 @@ extern "C" {
 KVECC_API int64_t kvecc_paged_attention_workspace(int64_t batch, int64_t heads, int64_t head_dim,
                                                   int64_t max_context_len) {
   if (batch <= 0 || heads <= 0 || head_dim <= 0 || max_context_len <= 0) return 0;
-  // sized for the codec with the most splits (Golay) so one size fits both
-  return batch * heads *
-         cdiv(max_context_len, choose_split(batch * heads, max_context_len, KVECC_CODEC_GOLAY)) *
+  return batch * heads * cdiv(max_context_len, choose_split(batch * heads, max_context_len)) *
          (head_dim + 2);
 }
 
@@ -415,7 +413,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.layer = layer;
   a.bs = block_size;
   a.max_blocks = max_blocks;
-  a.split = choose_split(batch * heads, max_context_len, codec);
+  a.split = choose_split(batch * heads, max_context_len);
   a.nsplit = cdiv(max_context_len, a.split);
   if (a.nsplit > kMaxSplits)
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
