@@ -106,3 +106,48 @@ def test_backend_registry():
     with pytest.raises(ValueError):
         backends.get_codec_backend("cuda-triton")
     assert "hip" in backends.available_backends()
+
+
+_SKIP_VALIDATION = {"kvecc_version", "kvecc_last_error", "kvecc_device_count", "kvecc_init_device",
+                    "kvecc_golay_syndrome_table_host", "kvecc_golay_h_row_masks_host",
+                    "kvecc_ber_threshold", "kvecc_paged_attention_workspace"}
+
+
+def _call_with(lib, name, args_t, size):
+    args = []
+    for t in args_t:
+        if t is ctypes.c_int64:
+            args.append(size)
+        elif t is ctypes.c_int:
+            args.append(1)
+        elif t is ctypes.c_float:
+            args.append(0.5)
+        elif t is ctypes.c_uint8:
+            args.append(0)
+        else:
+            args.append(None)
+    return getattr(lib, name)(*args)
+
+
+def test_every_entry_point_rejects_negative_sizes():
+    """Argument validation precedes any device work, on every status entry point:
+    negative sizes -> KVECC_EINVAL with a message naming the function."""
+    from kvecc import _lib
+    lib = _lib.load()
+    for name, args_t in _lib.SIGNATURES.items():
+        if name in _SKIP_VALIDATION or ctypes.c_int64 not in args_t:
+            continue
+        rc = _call_with(lib, name, args_t, -1)
+        msg = lib.kvecc_last_error().decode()
+        assert rc == -1, (name, rc)
+        assert name[len("kvecc_"):].split("_")[0] in msg or "negative" in msg, (name, msg)
+
+
+def test_host_twins_reject_null_buffers():
+    """Non-empty work with NULL buffers is an error, never a crash (host twins)."""
+    from kvecc import _lib
+    lib = _lib.load()
+    for name, args_t in _lib.SIGNATURES.items():
+        if not name.startswith("kvecc_cpu_") or ctypes.c_int64 not in args_t:
+            continue
+        assert _call_with(lib, name, args_t, 8) == -1, name
