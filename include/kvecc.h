@@ -171,6 +171,16 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
                                         uint8_t *uncorrectable, int64_t m, uint64_t *stats,
                                         void *stream);
 
+/* Hamming(8,4) with packed values: nibbles two per byte (as above), codewords
+ * one byte each (the reference's), error types 2 bits per value (value j at
+ * bits 2*(j%4) of byte j/4; may be NULL).  stats as kvecc_hamming84_decode.
+ * Encode moves 1.5 B/value (reference layout: 2), decode 1.75 (reference: 3). */
+KVECC_API int kvecc_hamming84_encode_packed(const uint8_t *nibbles, uint8_t *codewords, int64_t n,
+                                            void *stream);
+KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                            uint8_t *error_types, int64_t n, uint64_t *stats,
+                                            void *stream);
+
 /* ---- ECC shim: KV-cache write and read -------------------------------------- */
 /* ecc_shim.py:557-721 (ECCBackend.write) for codec KVECC_CODEC_NONE (int4),
  * H74, H84, GOLAY in ONE launch: K and V [batch, seq, hkv*d] (x_dtype,
@@ -249,6 +259,11 @@ KVECC_API int kvecc_cpu_golay_encode_packed(const uint8_t *nibbles, uint8_t *cod
 KVECC_API int kvecc_cpu_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
                                             uint8_t *uncorrectable, int64_t m, uint64_t *stats,
                                             int threads);
+KVECC_API int kvecc_cpu_hamming84_encode_packed(const uint8_t *nibbles, uint8_t *codewords,
+                                                int64_t n, int threads);
+KVECC_API int kvecc_cpu_hamming84_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                                uint8_t *error_types, int64_t n, uint64_t *stats,
+                                                int threads);
 KVECC_API int kvecc_cpu_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *counts, int64_t n,
                                   int n_bits, int64_t seed, float ber, int64_t global_n,
                                   int64_t offset0, uint64_t *stats, int threads);

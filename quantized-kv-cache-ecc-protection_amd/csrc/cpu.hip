@@ -335,6 +335,48 @@ KVECC_API int kvecc_cpu_golay_decode_packed(const uint8_t *codewords, uint8_t *n
   return KVECC_OK;
 }
 
+// packed Hamming(8,4) (host twins of packed.hip): groups of 4 values share a
+// type byte and two nibble bytes, one group per work item
+KVECC_API int kvecc_cpu_hamming84_encode_packed(const uint8_t *nibbles, uint8_t *codewords,
+                                                int64_t n, int threads) {
+  if (n < 0) return set_error(KVECC_EINVAL, "cpu_hamming84_encode_packed: negative n");
+  if (n && (!nibbles || !codewords)) return set_error(KVECC_EINVAL, "cpu_hamming84_encode_packed: null pointer");
+  parallel_for(n, threads, 64, [&](int64_t b, int64_t e, int) {
+    for (int64_t j = b; j < e; ++j)
+      codewords[j] = (uint8_t)(h84_encode4(nibbles[j >> 1] >> (4 * (j & 1)) & 0xFu) & 0xFFu);
+  });
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_cpu_hamming84_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                                uint8_t *error_types, int64_t n, uint64_t *stats,
+                                                int threads) {
+  if (n < 0) return set_error(KVECC_EINVAL, "cpu_hamming84_decode_packed: negative n");
+  if (n && (!nibbles || !codewords)) return set_error(KVECC_EINVAL, "cpu_hamming84_decode_packed: null pointer");
+  const int64_t groups = (n + 3) / 4;
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, groups, 1 << 14)));
+  parallel_for(groups, threads, 16, [&](int64_t b, int64_t e, int t) {
+    uint32_t n1 = 0, n2 = 0;
+    for (int64_t g = b; g < e; ++g) {
+      uint32_t tb = 0;
+      for (int64_t j = 4 * g; j < n && j < 4 * g + 4; ++j) {
+        uint32_t d, ty;
+        h84_decode4(codewords[j], d, ty, n1, n2);
+        if ((j & 1) == 0)
+          nibbles[j >> 1] = (uint8_t)d;  // high nibble: next value, or zero padding
+        else
+          nibbles[j >> 1] = (uint8_t)((nibbles[j >> 1] & 0x0Fu) | d << 4);
+        tb |= ty << (2 * (j & 3));
+      }
+      if (error_types) error_types[g] = (uint8_t)tb;
+    }
+    acc[t].a += n1;
+    acc[t].b += n2;
+  });
+  add_stats(stats, acc, 2);
+  return KVECC_OK;
+}
+
 }  // extern "C"
 
 template <typename T>

@@ -1,4 +1,5 @@
-// packed.hip -- Golay(24,12) over packed storage.
+// packed.hip -- Golay(24,12) and Hamming(8,4) over packed storage (SURVEY
+// §8f rank 3).
 //
 // The reference's layout spends 4 B on a 24-bit codeword (int32) and 1 B on a
 // 4-bit value (uint8 triplets), so its decode moves 8 B per codeword.  This is
@@ -11,6 +12,10 @@
 //   * decode flags: one bit per codeword (1 = uncorrectable, data kept), eight
 //                codewords per byte.
 // Decode moves 3 + 1.5 + 0.125 = 4.625 B per codeword, encode 1.5 + 3 = 4.5 B.
+// Hamming(8,4) keeps its byte codewords (already 8 bits) but packs the values
+// (nibbles) and the decode's ErrorType (2 bits per value, value j at bits
+// 2(j%4) of byte j/4): encode 0.5 + 1 = 1.5 B/value, decode 1 + 0.5 + 0.25 =
+// 1.75 B/value (reference layout: 2 and 3).
 //
 // gfx950 design: a lane owns groups of 8 codewords = 12 B of nibbles + 24 B of
 // codewords (word aligned), kPkGroups groups per lane per tile.  Every
@@ -182,38 +187,127 @@ __global__ __launch_bounds__(kBlock) void golay_encode_packed_tail_kernel(
   cw[3 * k + 2] = (uint8_t)(c >> 16);
 }
 
+// decode: one thread per group of 8 codewords (12 nibble bytes + 1 flag byte,
+// never shared between groups because `begin` is a multiple of 8)
 template <bool WITH_FLAGS, bool WITH_STATS>
 __global__ __launch_bounds__(kBlock) void golay_decode_packed_tail_kernel(
     const uint8_t *__restrict__ cw, uint8_t *__restrict__ nib, uint8_t *__restrict__ flags,
     int64_t begin, int64_t m, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
     uint64_t *__restrict__ stats) {
-  // a single thread walks the (< one tile) tail sequentially: groups share bytes
   uint32_t bits = 0, unc = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    for (int64_t g = begin / 8; g * 8 < m; ++g) {
-      uint32_t fl = 0;
-      for (int64_t k = g * 8; k < m && k < g * 8 + 8; ++k) {
-        const uint32_t c = cw[3 * k] | (uint32_t)cw[3 * k + 1] << 8 | (uint32_t)cw[3 * k + 2] << 16;
-        uint32_t cnt;
-        const uint32_t d = golay_decode1(c, par, cor, cnt);
-        bits += cnt & 3u;
-        unc += cnt >> 2;
-        fl |= (cnt >> 2) << (k - g * 8);
-        for (int e = 0; e < 3; ++e) {
-          const int64_t j = 3 * k + e;
-          const uint32_t v = d >> (4 * e) & 0xFu;
-          if ((j & 1) == 0)
-            nib[j >> 1] = (uint8_t)v;  // high nibble: next value, or zero padding
-          else
-            nib[j >> 1] = (uint8_t)((nib[j >> 1] & 0x0Fu) | v << 4);
-        }
+  for (int64_t g = begin / 8 + (int64_t)blockIdx.x * kBlock + threadIdx.x; g * 8 < m;
+       g += (int64_t)gridDim.x * kBlock) {
+    uint32_t fl = 0;
+    for (int64_t k = g * 8; k < m && k < g * 8 + 8; ++k) {
+      const uint32_t c = cw[3 * k] | (uint32_t)cw[3 * k + 1] << 8 | (uint32_t)cw[3 * k + 2] << 16;
+      uint32_t cnt;
+      const uint32_t d = golay_decode1(c, par, cor, cnt);
+      bits += cnt & 3u;
+      unc += cnt >> 2;
+      fl |= (cnt >> 2) << (k - g * 8);
+      for (int e = 0; e < 3; ++e) {
+        const int64_t j = 3 * k + e;
+        const uint32_t v = d >> (4 * e) & 0xFu;
+        if ((j & 1) == 0)
+          nib[j >> 1] = (uint8_t)v;  // high nibble: next value, or zero padding
+        else
+          nib[j >> 1] = (uint8_t)((nib[j >> 1] & 0x0Fu) | v << 4);
       }
-      if (WITH_FLAGS) flags[g] = (uint8_t)fl;
     }
+    if (WITH_FLAGS) flags[g] = (uint8_t)fl;
   }
   if (WITH_STATS) flush_stats2(stats, bits, unc);
 }
 
+// ---- Hamming(8,4) with packed values / error types ---------------------------
+
+// 4 data bytes (0x0d each) -> 16 bits d0 | d1 << 4 | d2 << 8 | d3 << 12
+__device__ __forceinline__ uint32_t nib_pack4(uint32_t w) {
+  const uint32_t x = w | (w >> 4);  // byte0 = d0|d1<<4, byte2 = d2|d3<<4
+  return (x & 0xFFu) | ((x >> 8) & 0xFF00u);
+}
+// 16 bits of 4 nibbles -> 4 bytes (0x0d each)
+__device__ __forceinline__ uint32_t nib_unpack4(uint32_t h) {
+  const uint32_t x = (h & 0xFFu) | (h & 0xFF00u) << 8;  // byte0 = d0|d1<<4, byte2 = d2|d3<<4
+  return (x & 0x000F000Fu) | (x << 4 & 0x0F000F00u);
+}
+// 4 type bytes (0..3) -> 8 bits t0 | t1 << 2 | t2 << 4 | t3 << 6
+__device__ __forceinline__ uint32_t type_pack4(uint32_t t) {
+  const uint32_t x = t | (t >> 6);          // byte0 = t0|t1<<2, byte2 = t2|t3<<2
+  return (x & 0xFu) | ((x >> 12) & 0xF0u);
+}
+
+constexpr int kHpBlock = 256;
+
+// a lane owns 16 values: one 16-byte codeword access, 8 bytes of nibbles
+__global__ __launch_bounds__(kHpBlock) void h84_encode_packed_kernel(const u32x2 *__restrict__ nib,
+                                                                     u32x4 *__restrict__ cw,
+                                                                     int64_t n16) {
+  for (int64_t i = (int64_t)blockIdx.x * kHpBlock + threadIdx.x; i < n16;
+       i += (int64_t)gridDim.x * kHpBlock) {
+    const u32x2 v = ld_stream(nib + i);
+    u32x4 o;
+    o.x = h84_encode4(nib_unpack4(v.x & 0xFFFFu));
+    o.y = h84_encode4(nib_unpack4(v.x >> 16));
+    o.z = h84_encode4(nib_unpack4(v.y & 0xFFFFu));
+    o.w = h84_encode4(nib_unpack4(v.y >> 16));
+    st_stream(cw + i, o);
+  }
+}
+
+template <bool WITH_TYPES, bool WITH_STATS>
+__global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4 *__restrict__ cw,
+                                                                     u32x2 *__restrict__ nib,
+                                                                     uint32_t *__restrict__ types,
+                                                                     int64_t n16,
+                                                                     uint64_t *__restrict__ stats) {
+  uint32_t n1 = 0, n2 = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kHpBlock + threadIdx.x; i < n16;
+       i += (int64_t)gridDim.x * kHpBlock) {
+    const u32x4 c = ld_stream(cw + i);
+    const uint32_t w[4] = {c.x, c.y, c.z, c.w};
+    uint32_t d[4], t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h84_decode4(w[k], d[k], t[k], n1, n2);
+    st_stream(nib + i, u32x2{nib_pack4(d[0]) | nib_pack4(d[1]) << 16,
+                             nib_pack4(d[2]) | nib_pack4(d[3]) << 16});
+    if (WITH_TYPES)
+      st_stream(types + i, type_pack4(t[0]) | type_pack4(t[1]) << 8 | type_pack4(t[2]) << 16 |
+                               type_pack4(t[3]) << 24);
+  }
+  if (WITH_STATS) flush_stats2<kHpBlock>(stats, n1, n2);
+}
+
+// tails and unaligned buffers, byte accesses: encode one thread per value,
+// decode one thread per group of 4 values (2 nibble bytes + 1 type byte, never
+// shared because `begin` is a multiple of 16)
+__global__ __launch_bounds__(kBlock) void h84_encode_packed_tail_kernel(const uint8_t *__restrict__ nib,
+                                                                        uint8_t *__restrict__ cw,
+                                                                        int64_t begin, int64_t n) {
+  for (int64_t j = begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * kBlock)
+    cw[j] = (uint8_t)(h84_encode4(nib[j >> 1] >> (4 * (j & 1)) & 0xFu) & 0xFFu);
+}
+
+__global__ __launch_bounds__(kBlock) void h84_decode_packed_tail_kernel(
+    const uint8_t *__restrict__ cw, uint8_t *__restrict__ nib, uint8_t *__restrict__ types,
+    int64_t begin, int64_t n, uint64_t *__restrict__ stats) {
+  uint32_t n1 = 0, n2 = 0;
+  for (int64_t g = begin / 4 + (int64_t)blockIdx.x * kBlock + threadIdx.x; g * 4 < n;
+       g += (int64_t)gridDim.x * kBlock) {
+    uint32_t tb = 0, nb[2] = {0, 0};
+    for (int64_t j = 4 * g; j < n && j < 4 * g + 4; ++j) {
+      uint32_t d, t;
+      h84_decode4(cw[j], d, t, n1, n2);
+      nb[(j >> 1) & 1] |= d << (4 * (j & 1));
+      tb |= t << (2 * (j & 3));
+    }
+    nib[2 * g] = (uint8_t)nb[0];
+    if (4 * g + 2 < n) nib[2 * g + 1] = (uint8_t)nb[1];
+    if (types) types[g] = (uint8_t)tb;
+  }
+  if (stats) flush_stats2(stats, n1, n2);
+}
 }  // namespace kvecc
 
 using namespace kvecc;
@@ -271,16 +365,70 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
     done = ntiles * kPkTile;
   }
   if (done < m) {
+    const dim3 grid(grid_for(cdiv(m - done, 8), kBlock)), block(kBlock);
     if (uncorrectable && stats)
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, true>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, true>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
     else if (uncorrectable)
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, false>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, false>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
     else if (stats)
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, true>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, true>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
     else
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, false>), dim3(1), dim3(kBlock), 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, false>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
   }
   return check_launch("golay_decode_packed");
+}
+
+KVECC_API int kvecc_hamming84_encode_packed(const uint8_t *nibbles, uint8_t *codewords, int64_t n,
+                                            void *stream) {
+  if (n < 0) return set_error(KVECC_EINVAL, "hamming84_encode_packed: negative n");
+  if (n == 0) return KVECC_OK;
+  if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "hamming84_encode_packed: null pointer");
+  hipStream_t st = as_stream(stream);
+  int64_t done = 0;
+  if (aligned(nibbles, 8) && aligned(codewords, 16)) {
+    const int64_t n16 = n / 16;
+    if (n16 > 0)
+      hipLaunchKernelGGL(h84_encode_packed_kernel, dim3(grid_for(n16, kHpBlock, 32)), dim3(kHpBlock),
+                         0, st, reinterpret_cast<const u32x2 *>(nibbles),
+                         reinterpret_cast<u32x4 *>(codewords), n16);
+    done = n16 * 16;
+  }
+  if (done < n)
+    hipLaunchKernelGGL(h84_encode_packed_tail_kernel, dim3(grid_for(n - done, kBlock)), dim3(kBlock),
+                       0, st, nibbles, codewords, done, n);
+  return check_launch("hamming84_encode_packed");
+}
+
+KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *nibbles,
+                                            uint8_t *error_types, int64_t n, uint64_t *stats,
+                                            void *stream) {
+  if (n < 0) return set_error(KVECC_EINVAL, "hamming84_decode_packed: negative n");
+  if (n == 0) return KVECC_OK;
+  if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "hamming84_decode_packed: null pointer");
+  hipStream_t st = as_stream(stream);
+  int64_t done = 0;
+  if (aligned(nibbles, 8) && aligned(codewords, 16) && (!error_types || aligned(error_types, 4))) {
+    const int64_t n16 = n / 16;
+    if (n16 > 0) {
+      const dim3 grid(grid_for(n16, kHpBlock, 32)), block(kHpBlock);
+      const u32x4 *c = reinterpret_cast<const u32x4 *>(codewords);
+      u32x2 *o = reinterpret_cast<u32x2 *>(nibbles);
+      uint32_t *t = reinterpret_cast<uint32_t *>(error_types);
+      if (error_types && stats)
+        hipLaunchKernelGGL((h84_decode_packed_kernel<true, true>), grid, block, 0, st, c, o, t, n16, stats);
+      else if (error_types)
+        hipLaunchKernelGGL((h84_decode_packed_kernel<true, false>), grid, block, 0, st, c, o, t, n16, stats);
+      else if (stats)
+        hipLaunchKernelGGL((h84_decode_packed_kernel<false, true>), grid, block, 0, st, c, o, t, n16, stats);
+      else
+        hipLaunchKernelGGL((h84_decode_packed_kernel<false, false>), grid, block, 0, st, c, o, t, n16, stats);
+    }
+    done = n16 * 16;
+  }
+  if (done < n)
+    hipLaunchKernelGGL(h84_decode_packed_tail_kernel, dim3(grid_for(cdiv(n - done, 4), kBlock)),
+                       dim3(kBlock), 0, st, codewords, nibbles, error_types, done, n, stats);
+  return check_launch("hamming84_decode_packed");
 }
 
 }  // extern "C"

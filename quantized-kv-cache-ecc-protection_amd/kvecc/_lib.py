@@ -49,6 +49,8 @@ SIGNATURES = {
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
     "kvecc_golay_encode_packed": [_vp, _vp, _i64, _vp],
     "kvecc_golay_decode_packed": [_vp, _vp, _vp, _i64, _vp, _vp],
+    "kvecc_hamming84_encode_packed": [_vp, _vp, _i64, _vp],
+    "kvecc_hamming84_decode_packed": [_vp, _vp, _vp, _i64, _vp, _vp],
     "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
     "kvecc_paged_attention_workspace": [_i64, _i64, _i64, _i64],
@@ -65,6 +67,8 @@ SIGNATURES = {
     "kvecc_cpu_golay_decode_rows": [_vp, _vp, _i64, _i64, _vp, _int],
     "kvecc_cpu_golay_encode_packed": [_vp, _vp, _i64, _int],
     "kvecc_cpu_golay_decode_packed": [_vp, _vp, _vp, _i64, _vp, _int],
+    "kvecc_cpu_hamming84_encode_packed": [_vp, _vp, _i64, _int],
+    "kvecc_cpu_hamming84_decode_packed": [_vp, _vp, _vp, _i64, _vp, _int],
     "kvecc_cpu_inject_u8_vectorized": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _vp, _int],
     "kvecc_cpu_inject_i32_vectorized": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _vp, _int],
     "kvecc_cpu_inject_rows_u8": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _int],

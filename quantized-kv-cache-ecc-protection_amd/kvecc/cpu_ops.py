@@ -545,3 +545,31 @@ def golay_decode_packed(codewords: torch.Tensor, m: int, return_uncorrectable: b
     if return_uncorrectable:
         return nib, flags, (int(st[0]), int(st[1]))
     return nib, (int(st[0]), int(st[1]))
+
+
+from .ops import pack_error_types  # noqa: E402  (pure torch, device-agnostic)
+
+
+def hamming84_encode_packed(nibbles: torch.Tensor, n: int) -> torch.Tensor:
+    _check_cpu(nibbles)
+    nib = nibbles.reshape(-1)
+    if nib.dtype != torch.uint8 or nib.numel() < (n + 1) // 2:
+        raise ValueError(f"need {(n + 1) // 2} packed uint8 nibble bytes for {n} values")
+    nib = nib.contiguous()
+    out = torch.empty(n, dtype=torch.uint8)
+    _lib.call("kvecc_cpu_hamming84_encode_packed", _ptr(nib), _ptr(out), int(n), NUM_THREADS)
+    return out
+
+
+def hamming84_decode_packed(codewords: torch.Tensor, return_error_types: bool = False):
+    _check_cpu(codewords)
+    cw = codewords.reshape(-1).to(torch.uint8).contiguous()
+    n = cw.numel()
+    nib = torch.empty((n + 1) // 2, dtype=torch.uint8)
+    et = torch.empty((n + 3) // 4, dtype=torch.uint8) if return_error_types else None
+    st = _stats()
+    _lib.call("kvecc_cpu_hamming84_decode_packed", _ptr(cw), _ptr(nib), _ptr(et), n, _ptr(st),
+              NUM_THREADS)
+    if return_error_types:
+        return nib, et, (int(st[0]), int(st[1]))
+    return nib, (int(st[0]), int(st[1]))

@@ -654,3 +654,52 @@ def golay_decode_packed(codewords: torch.Tensor, m: int, return_uncorrectable: b
     if return_uncorrectable:
         return nib, flags, (bits, unc)
     return nib, (bits, unc)
+
+
+def pack_error_types(types: torch.Tensor) -> torch.Tensor:
+    """ErrorType bytes (0..3) -> 2 bits per value, value j at bits 2*(j%4) of byte j/4."""
+    flat = types.reshape(-1).to(torch.uint8)
+    pad = (4 - flat.numel() % 4) % 4
+    if pad:
+        flat = torch.cat([flat, flat.new_zeros(pad)])
+    q = (flat.view(-1, 4) & 3).to(torch.int32)
+    return (q[:, 0] | q[:, 1] << 2 | q[:, 2] << 4 | q[:, 3] << 6).to(torch.uint8)
+
+
+def hamming84_encode_packed_into(nibbles, codewords, n):
+    _lib.call("kvecc_hamming84_encode_packed", _ptr(nibbles), _ptr(codewords), int(n),
+              _stream(nibbles.device))
+    return codewords
+
+
+def hamming84_decode_packed_into(codewords, nibbles, error_types=None, n=None, stats=None):
+    n = codewords.numel() if n is None else int(n)
+    _lib.call("kvecc_hamming84_decode_packed", _ptr(codewords), _ptr(nibbles), _ptr(error_types), n,
+              _ptr(stats), _stream(codewords.device))
+    return nibbles
+
+
+def hamming84_encode_packed(nibbles: torch.Tensor, n: int) -> torch.Tensor:
+    """n values of a packed nibble stream -> n Hamming(8,4) codeword bytes."""
+    _check_gpu(nibbles)
+    nib = nibbles.reshape(-1)
+    if nib.dtype != torch.uint8 or nib.numel() < (n + 1) // 2:
+        raise ValueError(f"need {(n + 1) // 2} packed uint8 nibble bytes for {n} values")
+    nib = nib.contiguous()
+    out = torch.empty(n, dtype=torch.uint8, device=nib.device)
+    return hamming84_encode_packed_into(nib, out, n)
+
+
+def hamming84_decode_packed(codewords: torch.Tensor, return_error_types: bool = False):
+    """Codeword bytes -> packed nibbles, (corrected, detected) [, packed 2-bit types]."""
+    _check_gpu(codewords)
+    cw = codewords.reshape(-1).to(torch.uint8).contiguous()
+    n = cw.numel()
+    nib = torch.empty((n + 1) // 2, dtype=torch.uint8, device=cw.device)
+    et = torch.empty((n + 3) // 4, dtype=torch.uint8, device=cw.device) if return_error_types else None
+    st = new_stats(cw.device)
+    hamming84_decode_packed_into(cw, nib, et, n, st)
+    corrected, detected = read_stats(st)
+    if return_error_types:
+        return nib, et, (corrected, detected)
+    return nib, (corrected, detected)

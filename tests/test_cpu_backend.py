@@ -250,3 +250,18 @@ def test_golay_packed_vs_reference_layout(cpu, m):
         assert int(out[-1]) >> 4 == 0  # padding nibble is zero
     bitmask = torch.tensor([(int(flags[k // 8]) >> (k % 8)) & 1 for k in range(m)], dtype=torch.uint8)
     assert torch.equal(bitmask, (cnt_ref == 4).to(torch.uint8))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 15, 16, 17, 100, 4096 * 16 + 7])
+def test_hamming84_packed_vs_reference_layout(cpu, n):
+    g = torch.Generator().manual_seed(n)
+    vals = torch.randint(0, 16, (n,), generator=g, dtype=torch.uint8)
+    nib = cpu.pack_nibbles(vals)
+    cw = cpu.hamming84_encode_packed(nib, n)
+    assert torch.equal(cw, cpu.hamming84_encode(vals))
+    noisy = cpu.inject_bit_errors_triton(cw, 0.05, 8, seed=4)
+    data, et, st = cpu.hamming84_decode(noisy, return_error_types=True)
+    pn, pt, pst = cpu.hamming84_decode_packed(noisy, return_error_types=True)
+    assert pst == st
+    assert torch.equal(pn, cpu.pack_nibbles(data)) and torch.equal(pt, cpu.pack_error_types(et))
+    assert torch.equal(cpu.unpack_nibbles(pn, n), data)

@@ -425,3 +425,23 @@ def test_golay_packed_vs_cpu_backend(gpu, m, offset):
     out, fl, st = ops.golay_decode_packed(buf.to(gpu)[offset:], m, return_uncorrectable=True)
     assert st == st_ref and st_ref[0] > 0
     assert torch.equal(out.cpu(), out_ref) and torch.equal(fl.cpu(), fl_ref)
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 16 * 1000 + 9, 134_217_728])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_hamming84_packed_vs_cpu_backend(gpu, n, offset):
+    if offset and n > 100_000:
+        pytest.skip("unaligned full size adds nothing over the small cases")
+    from kvecc import cpu_ops, ops
+    g = torch.Generator().manual_seed(n + offset)
+    nib = torch.randint(0, 256, ((n + 1) // 2 + offset,), generator=g, dtype=torch.uint8)
+    cw_ref = cpu_ops.hamming84_encode_packed(nib[offset:], n)
+    cw = ops.hamming84_encode_packed(nib.to(gpu)[offset:], n)
+    assert torch.equal(cw.cpu(), cw_ref)
+    noisy = cpu_ops.inject_bit_errors_triton(cw_ref, 0.02, 8, seed=6)
+    pn_ref, pt_ref, st_ref = cpu_ops.hamming84_decode_packed(noisy, return_error_types=True)
+    buf = torch.zeros(n + offset, dtype=torch.uint8)
+    buf[offset:] = noisy
+    pn, pt, st = ops.hamming84_decode_packed(buf.to(gpu)[offset:], return_error_types=True)
+    assert st == st_ref
+    assert torch.equal(pn.cpu(), pn_ref) and torch.equal(pt.cpu(), pt_ref)

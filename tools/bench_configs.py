@@ -155,6 +155,15 @@ def extended(reps):
                                        m, "codewords", 4.5)
     out["packed_golay_decode"] = entry(timed(lambda: ops.golay_decode_packed_into(
         cw3, nib2, fl, m, st), reps), m, "codewords", 4.625)
+    n = 8 * 4096 * 32 * 128
+    hn = torch.randint(0, 256, (n // 2,), dtype=torch.uint8, device=dev)
+    hcw = ops.hamming84_encode_packed(hn, n)
+    hn2 = torch.empty_like(hn)
+    ht = torch.empty(n // 4, dtype=torch.uint8, device=dev)
+    out["packed_h84_encode"] = entry(timed(lambda: ops.hamming84_encode_packed_into(hn, hcw, n), reps),
+                                     n, "values", 1.5)
+    out["packed_h84_decode"] = entry(timed(lambda: ops.hamming84_decode_packed_into(
+        hcw, hn2, ht, n, st), reps), n, "values", 1.75)
     # paged decode attention, [8 seqs x 4096 ctx, 32 heads, D=128]
     for codec in ("hamming84", "golay"):
         b, hq, d, ctx, bs = 8, 32, 128, 4096, 16
