@@ -54,6 +54,14 @@ enum { KVECC_F32 = 0, KVECC_F16 = 1, KVECC_BF16 = 2 };
 /* codec codes for fused kernels */
 enum { KVECC_CODEC_NONE = 0, KVECC_CODEC_H74 = 1, KVECC_CODEC_H84 = 2, KVECC_CODEC_GOLAY = 3 };
 
+/* Row scale rule of the INT4 quantizer.  The reference computes
+ * `abs_max / 7.0` with a Python-scalar divisor (paged_cache_ecc.py:330); torch
+ * evaluates that as IEEE division on CPU tensors but as abs_max * RN(1/7) on
+ * GPU tensors (its CPU-scalar-divisor shortcut), and the two differ in ~55% of
+ * rows.  DIV7 reproduces the reference run on the CPU (the golden fixtures),
+ * MUL_INV7 the reference run on a GPU.  q = x / scale is IEEE under both. */
+enum { KVECC_SCALE_DIV7 = 0, KVECC_SCALE_MUL_INV7 = 1 };
+
 /* ---- runtime --------------------------------------------------------------- */
 KVECC_API const char *kvecc_version(void);
 KVECC_API const char *kvecc_last_error(void);
@@ -146,10 +154,12 @@ KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int
 /* ---- Fused quantize / encode and decode / dequantize ----------------------- */
 /* fused_kernels.py:18-160 (H84), :163-269 (H74), and the shim's torch path
  * ecc_shim.py:572-580: per row of d values (dtype x_dtype), scale = absmax/7
- * (0 -> 1), q = rint(x/scale) clamped [-8,7] + 8, then encoded with `codec`
- * (KVECC_CODEC_NONE stores the raw nibble).  scales: fp32 per row. */
-KVECC_API int kvecc_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
-                                         float *scales, int64_t rows, int64_t d, void *stream);
+ * under `scale_rule` (KVECC_SCALE_*; 0 -> 1), q = rint(x/scale) clamped [-8,7]
+ * + 8, then encoded with `codec` (KVECC_CODEC_NONE stores the raw nibble).
+ * scales: fp32 per row. */
+KVECC_API int kvecc_quantize_encode_rows(const void *x, int x_dtype, int codec, int scale_rule,
+                                         uint8_t *cw, float *scales, int64_t rows, int64_t d,
+                                         void *stream);
 /* fused_kernels.py:272-437 : H84 decode + (q-8)*scale -> out (out_dtype).
  * zero_doubles = 1 reproduces :344 (double-error data -> 0).
  * stats[0] += #SINGLE_CORRECTED, stats[1] += #DOUBLE_DETECTED. */
@@ -184,7 +194,8 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
 /* ---- ECC shim: KV-cache write and read -------------------------------------- */
 /* ecc_shim.py:557-721 (ECCBackend.write) for codec KVECC_CODEC_NONE (int4),
  * H74, H84, GOLAY in ONE launch: K and V [batch, seq, hkv*d] (x_dtype,
- * contiguous) are quantized per (pos, head) row (absmax/7, round-half-even),
+ * contiguous) are quantized per (pos, head) row (absmax/7 under scale_rule,
+ * round-half-even),
  * encoded, injected with the row's own seed when `inject` and ber > 0
  * (K: seed0 + r, V: seed0 + r + 1, r = (b*seq + pos)*hkv + h; n_bits per
  * codeword as ecc_shim.py:555-560) and stored into the paged caches -- only the
@@ -194,7 +205,8 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
  * hkv, block_size]; token pos lives in physical block block_table[pos / block_size]
  * (device int32).  d <= 512. */
 KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
-                               int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
+                               int64_t seq, int64_t hkv, int64_t d, int codec, int scale_rule,
+                               int n_bits,
                                int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
                                float *k_scales, float *v_scales, const int32_t *block_table,
                                int64_t num_layers, int64_t block_size, int64_t layer,
@@ -284,13 +296,15 @@ KVECC_API int kvecc_cpu_inject_rows_i32(const int32_t *in, int32_t *out, int64_t
                                         uint64_t *stats, int threads);
 KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
                                     int64_t outer, int64_t len, int64_t inner, int threads);
-KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
-                                             float *scales, int64_t rows, int64_t d, int threads);
+KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec,
+                                             int scale_rule, uint8_t *cw, float *scales,
+                                             int64_t rows, int64_t d, int threads);
 KVECC_API int kvecc_cpu_decode_dequant_h84_rows(const uint8_t *cw, const float *scales, void *out,
                                                 int out_dtype, int64_t rows, int64_t d,
                                                 int zero_doubles, uint64_t *stats, int threads);
 KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
-                                   int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
+                                   int64_t seq, int64_t hkv, int64_t d, int codec,
+                                   int scale_rule, int n_bits,
                                    int inject, float ber, int64_t seed0, void *k_cache,
                                    void *v_cache, float *k_scales, float *v_scales,
                                    const int32_t *block_table, int64_t num_layers,

@@ -389,8 +389,11 @@ void oracle_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
 /* Quantization                                                              */
 /* ------------------------------------------------------------------------ */
 
-void oracle_quantize_rows(const float *x, int64_t rows, int64_t d, uint8_t *q,
+/* rule 0: scale = amax / 7 (IEEE), torch on CPU tensors; rule 1: amax * RN(1/7),
+ * torch's tensor / Python scalar on a GPU (paged_cache_ecc.py:330). */
+void oracle_quantize_rows(const float *x, int64_t rows, int64_t d, int rule, uint8_t *q,
                           float *scales) {
+  const volatile float inv7 = 1.0f / 7.0f;
   for (int64_t r = 0; r < rows; ++r) {
     const float *row = x + r * d;
     float amax = 0.0f;
@@ -398,7 +401,7 @@ void oracle_quantize_rows(const float *x, int64_t rows, int64_t d, uint8_t *q,
       float a = fabsf(row[j]);
       if (a > amax) amax = a;
     }
-    volatile float scale = amax / 7.0f;
+    volatile float scale = rule ? amax * inv7 : amax / 7.0f;
     if (scale == 0.0f) scale = 1.0f;
     scales[r] = scale;
     for (int64_t j = 0; j < d; ++j) {

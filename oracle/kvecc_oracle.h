@@ -81,8 +81,10 @@ void oracle_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
  * Shim quantization (kv_cache/ecc_shim.py:572-580 with
  * kv_cache/paged_cache_ecc.py:302-334): per row of d fp32 values,
  * scale = absmax/7 (0 -> 1), q = round_half_even(x/scale) clamped [-8,7] + 8.
+ * rule 0: the scale by IEEE division (torch on CPU tensors, the golden
+ * fixtures); rule 1: absmax * RN(1/7) (torch's tensor / Python scalar on a GPU).
  */
-void oracle_quantize_rows(const float *x, int64_t rows, int64_t d, uint8_t *q,
+void oracle_quantize_rows(const float *x, int64_t rows, int64_t d, int rule, uint8_t *q,
                           float *scales);
 /* fused_kernels.py:272-357 data path: H84 decode, doubles -> 0, (q-8)*scale */
 void oracle_decode_dequant_h84(const uint8_t *cw, const float *scales, int64_t rows,

@@ -58,7 +58,7 @@ def lib():
             "oracle_inject_u8_vectorized": [_u8p, _u8p, _u8p, _i64, _int, _i64, _f32, _i64p],
             "oracle_inject_i32_vectorized": [_i32p, _i32p, _u8p, _i64, _int, _i64, _f32, _i64p],
             "oracle_interpolate": [_u8p, _u8p, _u8p, _i64, _i64, _i64],
-            "oracle_quantize_rows": [_f32p, _i64, _i64, _u8p, _f32p],
+            "oracle_quantize_rows": [_f32p, _i64, _i64, _int, _u8p, _f32p],
             "oracle_decode_dequant_h84": [_u8p, _f32p, _i64, _i64, _f32p, _i64p],
         }
         for name, args in sig.items():
@@ -224,14 +224,15 @@ def interpolate_double_errors(q, err, seq_dim=-1):
     return out.reshape(q.shape)
 
 
-def quantize_rows(x):
-    """-> (q uint8 [..., D], scales f32 [...])  ecc_shim.py:572-580"""
+def quantize_rows(x, rule=0):
+    """-> (q uint8 [..., D], scales f32 [...])  ecc_shim.py:572-580
+    rule 0: scale by IEEE division (torch on CPU); 1: absmax * RN(1/7) (torch on a GPU)"""
     x = _c(x, np.float32)
     d = x.shape[-1]
     rows = x.size // d if d else 0
     q = np.empty(x.shape, np.uint8)
     s = np.empty(x.shape[:-1], np.float32)
-    lib().oracle_quantize_rows(_p(x, _f32p), rows, d, _p(q, _u8p), _p(s, _f32p))
+    lib().oracle_quantize_rows(_p(x, _f32p), rows, d, int(rule), _p(q, _u8p), _p(s, _f32p))
     return q, s
 
 

@@ -98,17 +98,35 @@ KV_HD float div_rn(float a, float b) {
 #endif
 }
 
-// scale = absmax / 7, 0 -> 1 (compute_quantization_scales, paged_cache_ecc.py:302-334)
-KV_HD float row_scale(float amax) {
-  float s = div_rn(amax, 7.0f);
+// scale = absmax / 7, 0 -> 1 (compute_quantization_scales, paged_cache_ecc.py:302-334).
+// rule 0 (KVECC_SCALE_DIV7): IEEE division, torch on CPU tensors; rule 1
+// (KVECC_SCALE_MUL_INV7): absmax * RN(1/7), torch's tensor / Python scalar on a GPU.
+KV_HD float row_scale(float amax, int rule) {
+  float s = rule ? amax * (1.0f / 7.0f) : div_rn(amax, 7.0f);
   return s == 0.0f ? 1.0f : s;
 }
 
-// round_half_even(x / scale) clamped to [-8, 7], + 8
-KV_HD uint32_t quantize_nibble(float x, float scale) {
-  float q = rintf(div_rn(x, scale));
-  q = fminf(fmaxf(q, -8.0f), 7.0f);
+// rounded quotient clamped to [-8, 7], + 8
+KV_HD uint32_t nibble_of_quotient(float quot) {
+  float q = fminf(fmaxf(rintf(quot), -8.0f), 7.0f);
   return (uint32_t)(int)(q + 8.0f);
+}
+
+// round_half_even(x / scale) clamped to [-8, 7], + 8
+KV_HD uint32_t quantize_nibble(float x, float scale) { return nibble_of_quotient(div_rn(x, scale)); }
+
+// x / scale through a per-row reciprocal (Markstein): with inv = RN(1/scale),
+// q0 = RN(x * inv) is within an ulp of x / scale, r = x - scale * q0 is exact
+// under FMA, and RN(q0 + r * inv) is the correctly rounded quotient while no
+// intermediate leaves the normal range.  Three ops instead of IEEE division's
+// ~10.  The kernels take this path only for fp16/bf16 rows whose scale passes
+// recip_ok; tests/test_quant_exhaustive.py checks it against IEEE division for
+// every finite (value, row max) pair of both dtypes.
+KV_HD bool recip_ok(float scale) { return scale >= 0x1p-64f && scale <= 0x1p64f; }
+KV_HD float div_recip(float x, float scale, float inv) {
+  const float q0 = x * inv;
+  const float r = fmaf(-scale, q0, x);
+  return fmaf(r, inv, q0);
 }
 
 // ---- Golay(24,12) ---------------------------------------------------------------

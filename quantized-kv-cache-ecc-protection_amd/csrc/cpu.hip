@@ -529,8 +529,9 @@ KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_
   return KVECC_OK;
 }
 
-KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
-                                             float *scales, int64_t rows, int64_t d, int threads) {
+KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec,
+                                             int scale_rule, uint8_t *cw, float *scales,
+                                             int64_t rows, int64_t d, int threads) {
   if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: negative size");
   if (rows == 0) return KVECC_OK;
   if (d == 0) return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: empty rows");
@@ -539,18 +540,16 @@ KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int cod
     return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: bad dtype %d", x_dtype);
   if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_H84)
     return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: bad codec %d", codec);
+  if (scale_rule != KVECC_SCALE_DIV7 && scale_rule != KVECC_SCALE_MUL_INV7)
+    return set_error(KVECC_EINVAL, "cpu_quantize_encode_rows: bad scale rule %d", scale_rule);
   parallel_for(rows, threads, 1, [&](int64_t b, int64_t e, int) {
     for (int64_t r = b; r < e; ++r) {
       float amax = 0.0f;
       for (int64_t j = 0; j < d; ++j) amax = std::max(amax, std::fabs(load_x(x, x_dtype, r * d + j)));
-      float scale = amax / 7.0f;
-      if (scale == 0.0f) scale = 1.0f;
+      const float scale = row_scale(amax, scale_rule);
       scales[r] = scale;
-      for (int64_t j = 0; j < d; ++j) {
-        float q = std::rint(load_x(x, x_dtype, r * d + j) / scale);
-        q = std::min(std::max(q, -8.0f), 7.0f);
-        cw[r * d + j] = (uint8_t)encode_nibble((uint32_t)(int)(q + 8.0f), codec);
-      }
+      for (int64_t j = 0; j < d; ++j)
+        cw[r * d + j] = (uint8_t)encode_nibble(quantize_nibble(load_x(x, x_dtype, r * d + j), scale), codec);
     }
   });
   return KVECC_OK;
@@ -584,8 +583,9 @@ KVECC_API int kvecc_cpu_decode_dequant_h84_rows(const uint8_t *cw, const float *
 // ---- shim write / read (host twins of shim.hip) ------------------------------
 
 KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
-                                   int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
-                                   int inject, float ber, int64_t seed0, void *k_cache,
+                                   int64_t seq, int64_t hkv, int64_t d, int codec,
+                                   int scale_rule, int n_bits, int inject, float ber,
+                                   int64_t seed0, void *k_cache,
                                    void *v_cache, float *k_scales, float *v_scales,
                                    const int32_t *block_table, int64_t num_layers,
                                    int64_t block_size, int64_t layer, int threads) {
@@ -594,6 +594,8 @@ KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, in
   if (d < 1) return set_error(KVECC_EINVAL, "cpu_shim_write: empty rows");
   if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
     return set_error(KVECC_EINVAL, "cpu_shim_write: bad codec %d", codec);
+  if (scale_rule != KVECC_SCALE_DIV7 && scale_rule != KVECC_SCALE_MUL_INV7)
+    return set_error(KVECC_EINVAL, "cpu_shim_write: bad scale rule %d", scale_rule);
   if (x_dtype < KVECC_F32 || x_dtype > KVECC_BF16)
     return set_error(KVECC_EINVAL, "cpu_shim_write: bad dtype %d", x_dtype);
   if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
@@ -622,7 +624,7 @@ KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, in
       const void *x = side ? v : k;
       float amax = 0.0f;
       for (int64_t j = 0; j < d; ++j) amax = std::max(amax, std::fabs(load_x(x, x_dtype, r * d + j)));
-      const float scale = row_scale(amax);
+      const float scale = row_scale(amax, scale_rule);
       (side ? v_scales : k_scales)[slot] = scale;
       if (!golay) {
         uint8_t *c = reinterpret_cast<uint8_t *>(side ? v_cache : k_cache) + slot * g;

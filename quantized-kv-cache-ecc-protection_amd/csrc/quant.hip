@@ -5,7 +5,9 @@
 // shim's torch path ecc_shim.py:572-580 with compute_quantization_scales
 // (kv_cache/paged_cache_ecc.py:302-334), which is the parity target:
 //   scale = absmax(row) / 7  (0 -> 1),  q = round_half_even(x / scale)
-//   clamped to [-8, 7] + 8,  all in IEEE fp32 (correctly rounded division).
+//   clamped to [-8, 7] + 8,  in fp32, the scale under the caller's rule
+//   (KVECC_SCALE_*: IEEE division as torch on the CPU, or absmax * RN(1/7) as
+//   torch on a GPU) and x / scale correctly rounded.
 //
 // gfx950 design: a row (one head vector, D values) is owned by LPR lanes of a
 // wave (LPR = the power of two covering D / VEC, VEC elements = 16 B per lane
@@ -35,7 +37,7 @@ struct alignas(sizeof(T) * VEC) Vec {
 // of a wave own row (wave_row0 + g).
 template <typename T, int VEC>
 __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__restrict__ x, int codec,
-                                                                 uint8_t *__restrict__ cw,
+                                                                 int rule, uint8_t *__restrict__ cw,
                                                                  float *__restrict__ scales,
                                                                  int64_t rows, int64_t d, int lpr) {
   const int lane = threadIdx.x & (kWave - 1);
@@ -57,8 +59,7 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
       }
     }
     amax = row_max(amax, lpr);
-    float scale = __fdiv_rn(amax, 7.0f);
-    if (scale == 0.0f) scale = 1.0f;
+    const float scale = row_scale(amax, rule);
     if (!live) continue;
     if (li == 0) scales[r] = scale;
     uint8_t *cr = cw + r * d;
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
 // groups are in flight per iteration.
 template <typename T, int VEC>
 __global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__restrict__ x, int codec,
-                                                                    uint8_t *__restrict__ cw,
+                                                                    int rule, uint8_t *__restrict__ cw,
                                                                     float *__restrict__ scales,
                                                                     int64_t rows, int64_t d, int lpr) {
   static_assert(sizeof(T) * VEC == 16, "one 16-byte chunk per lane");
@@ -116,16 +117,27 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__r
         amax = fmaxf(amax, fabsf(f[k]));
       }
       amax = row_max(amax, lpr);
-      const float scale = row_scale(amax);
+      const float scale = row_scale(amax, rule);
       if (!live[u]) continue;
       if (li == 0) scales[r] = scale;
+      // x / scale: reciprocal + FMA correction for 16-bit inputs (codec_math.h
+      // div_recip, exhaustively checked), IEEE division otherwise
+      uint32_t nq[VEC];
+      if (sizeof(T) == 2 && recip_ok(scale)) {
+        const float inv = div_rn(1.0f, scale);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) nq[k] = nibble_of_quotient(div_recip(f[k], scale, inv));
+      } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) nq[k] = quantize_nibble(f[k], scale);
+      }
       // four quantized nibbles per word, encoded SWAR (codec_math.h)
       uint32_t wds[VEC / 4];
 #pragma unroll
       for (int k = 0; k < VEC / 4; ++k) {
         uint32_t wq = 0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) wq |= quantize_nibble(f[4 * k + e], scale) << (8 * e);
+        for (int e = 0; e < 4; ++e) wq |= nq[4 * k + e] << (8 * e);
         wds[k] = codec == KVECC_CODEC_H84 ? h84_encode4(wq)
                  : codec == KVECC_CODEC_H74 ? h74_encode4(wq)
                                             : wq;
@@ -233,8 +245,8 @@ static int lanes_per_row(int64_t chunks) {
 }
 
 template <typename T>
-static void launch_qe(const void *x, int codec, uint8_t *cw, float *scales, int64_t rows, int64_t d,
-                      hipStream_t st) {
+static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *scales, int64_t rows,
+                      int64_t d, hipStream_t st) {
   constexpr int V = 16 / sizeof(T);
   const T *xt = reinterpret_cast<const T *>(x);
   bool vec = d % V == 0 && aligned(x, 16) && aligned(cw, V);
@@ -242,17 +254,17 @@ static void launch_qe(const void *x, int codec, uint8_t *cw, float *scales, int6
     int lpr = lanes_per_row(d / V);
     int64_t waves = cdiv(rows, kWave / lpr);
     hipLaunchKernelGGL((quantize_encode_1c_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave, 16)),
-                       dim3(kBlock), 0, st, xt, codec, cw, scales, rows, d, lpr);
+                       dim3(kBlock), 0, st, xt, codec, rule, cw, scales, rows, d, lpr);
   } else if (vec) {
     int lpr = lanes_per_row(d / V);
     int64_t waves = cdiv(rows, kWave / lpr);
     hipLaunchKernelGGL((quantize_encode_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave)),
-                       dim3(kBlock), 0, st, xt, codec, cw, scales, rows, d, lpr);
+                       dim3(kBlock), 0, st, xt, codec, rule, cw, scales, rows, d, lpr);
   } else {
     int lpr = lanes_per_row(d);
     int64_t waves = cdiv(rows, kWave / lpr);
     hipLaunchKernelGGL((quantize_encode_kernel<T, 1>), dim3(grid_for(waves, kBlock / kWave)),
-                       dim3(kBlock), 0, st, xt, codec, cw, scales, rows, d, lpr);
+                       dim3(kBlock), 0, st, xt, codec, rule, cw, scales, rows, d, lpr);
   }
 }
 
@@ -283,19 +295,22 @@ using namespace kvecc;
 
 extern "C" {
 
-KVECC_API int kvecc_quantize_encode_rows(const void *x, int x_dtype, int codec, uint8_t *cw,
-                                         float *scales, int64_t rows, int64_t d, void *stream) {
+KVECC_API int kvecc_quantize_encode_rows(const void *x, int x_dtype, int codec, int scale_rule,
+                                         uint8_t *cw, float *scales, int64_t rows, int64_t d,
+                                         void *stream) {
   if (rows < 0 || d < 0) return set_error(KVECC_EINVAL, "quantize_encode_rows: negative size");
   if (rows == 0) return KVECC_OK;
   if (d == 0) return set_error(KVECC_EINVAL, "quantize_encode_rows: empty rows");
   if (!x || !cw || !scales) return set_error(KVECC_EINVAL, "quantize_encode_rows: null pointer");
   if (codec != KVECC_CODEC_NONE && codec != KVECC_CODEC_H74 && codec != KVECC_CODEC_H84)
     return set_error(KVECC_EINVAL, "quantize_encode_rows: bad codec %d", codec);
+  if (scale_rule != KVECC_SCALE_DIV7 && scale_rule != KVECC_SCALE_MUL_INV7)
+    return set_error(KVECC_EINVAL, "quantize_encode_rows: bad scale rule %d", scale_rule);
   hipStream_t st = as_stream(stream);
   switch (x_dtype) {
-    case KVECC_F32: launch_qe<float>(x, codec, cw, scales, rows, d, st); break;
-    case KVECC_F16: launch_qe<__half>(x, codec, cw, scales, rows, d, st); break;
-    case KVECC_BF16: launch_qe<__hip_bfloat16>(x, codec, cw, scales, rows, d, st); break;
+    case KVECC_F32: launch_qe<float>(x, codec, scale_rule, cw, scales, rows, d, st); break;
+    case KVECC_F16: launch_qe<__half>(x, codec, scale_rule, cw, scales, rows, d, st); break;
+    case KVECC_BF16: launch_qe<__hip_bfloat16>(x, codec, scale_rule, cw, scales, rows, d, st); break;
     default: return set_error(KVECC_EINVAL, "quantize_encode_rows: bad dtype %d", x_dtype);
   }
   return check_launch("quantize_encode_rows");

@@ -46,7 +46,7 @@ struct ShimWriteArgs {
   float *scales[2];
   int64_t batch, seq;
   uint32_t seed0, rowmul, nbits, thr;
-  int nb_eff, inject;
+  int nb_eff, inject, scale_rule;
 };
 
 // one wave per (side, pos, head) row of the last batch
@@ -79,8 +79,14 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
   }
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) amax = fmaxf(amax, __shfl_xor(amax, off, kWave));
-  const float scale = row_scale(amax);
+  const float scale = row_scale(amax, a.scale_rule);
   if (live && lane == 0) a.scales[side][slot] = scale;
+  // x / scale: reciprocal + FMA correction for 16-bit rows (codec_math.h div_recip)
+  const bool recip = sizeof(T) == 2 && recip_ok(scale);
+  const float inv = div_rn(1.0f, scale);
+  auto quant = [&](float x) {
+    return recip ? nibble_of_quotient(div_recip(x, scale, inv)) : quantize_nibble(x, scale);
+  };
 
   if (CODEC != KVECC_CODEC_GOLAY) {
     if (!live) return;
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
     for (int i = 0; i < kPer; ++i) {
       const uint32_t e = lane + i * kWave;
       if (e < geo.d) {
-        uint32_t cw = encode_nibble(quantize_nibble(v[i], scale), CODEC);
+        uint32_t cw = encode_nibble(quant(v[i]), CODEC);
         if (a.inject) cw ^= philox_flip_mask<NB>(key0 + e * a.nbits, e, a.thr, a.nb_eff);
         c[e] = (uint8_t)cw;
       }
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const uint32_t e = lane + i * kWave;
-      if (e < geo.d) nib[w][e] = (uint8_t)quantize_nibble(v[i], scale);
+      if (e < geo.d) nib[w][e] = (uint8_t)quant(v[i]);
     }
     if ((uint32_t)lane < 3 * geo.g - geo.d) nib[w][geo.d + lane] = 0;  // per-head zero padding
   }
@@ -258,8 +264,8 @@ using namespace kvecc;
 extern "C" {
 
 KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
-                               int64_t seq, int64_t hkv, int64_t d, int codec, int n_bits,
-                               int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
+                               int64_t seq, int64_t hkv, int64_t d, int codec, int scale_rule,
+                               int n_bits, int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
                                float *k_scales, float *v_scales, const int32_t *block_table,
                                int64_t num_layers, int64_t block_size, int64_t layer,
                                void *stream) {
@@ -268,6 +274,8 @@ KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_
   if (d < 1 || d > kMaxShimD) return set_error(KVECC_EINVAL, "shim_write: head_dim %lld not in [1, %d]", (long long)d, kMaxShimD);
   if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
     return set_error(KVECC_EINVAL, "shim_write: bad codec %d", codec);
+  if (scale_rule != KVECC_SCALE_DIV7 && scale_rule != KVECC_SCALE_MUL_INV7)
+    return set_error(KVECC_EINVAL, "shim_write: bad scale rule %d", scale_rule);
   if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
     return set_error(KVECC_EINVAL, "shim_write: bad cache geometry");
   if (!k || !v || !k_cache || !v_cache || !k_scales || !v_scales || !block_table)
@@ -291,6 +299,7 @@ KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_
   a.nbits = (uint32_t)n_bits;
   a.thr = kvecc_ber_threshold(ber);
   a.inject = inject != 0 && ber > 0.0f;
+  a.scale_rule = scale_rule;
   // same bit-count clamps as the flat kernels (uint8 caches draw >= 1, <= 8 bits)
   a.nb_eff = codec == KVECC_CODEC_GOLAY ? (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits))
                                         : (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits));

@@ -45,13 +45,13 @@ SIGNATURES = {
     "kvecc_inject_rows_i32": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _vp],
     "kvecc_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "kvecc_any_equal_u8": [_vp, _i64, _u8, _vp, _vp],
-    "kvecc_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _vp],
+    "kvecc_quantize_encode_rows": [_vp, _int, _int, _int, _vp, _vp, _i64, _i64, _vp],
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
     "kvecc_golay_encode_packed": [_vp, _vp, _i64, _vp],
     "kvecc_golay_decode_packed": [_vp, _vp, _vp, _i64, _vp, _vp],
     "kvecc_hamming84_encode_packed": [_vp, _vp, _i64, _vp],
     "kvecc_hamming84_decode_packed": [_vp, _vp, _vp, _i64, _vp, _vp],
-    "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
     "kvecc_paged_attention_workspace": [_i64, _i64, _i64, _i64],
     "kvecc_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
@@ -76,9 +76,9 @@ SIGNATURES = {
     "kvecc_cpu_inject_u8": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
     "kvecc_cpu_inject_i32": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
     "kvecc_cpu_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _int],
-    "kvecc_cpu_quantize_encode_rows": [_vp, _int, _int, _vp, _vp, _i64, _i64, _int],
+    "kvecc_cpu_quantize_encode_rows": [_vp, _int, _int, _int, _vp, _vp, _i64, _i64, _int],
     "kvecc_cpu_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _int],
-    "kvecc_cpu_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _int],
+    "kvecc_cpu_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _int],
     "kvecc_cpu_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _int],
     "kvecc_cpu_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
                                   _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _int, _int],
@@ -93,6 +93,18 @@ _RESTYPE = {
 # dtype / codec codes (include/kvecc.h)
 F32, F16, BF16 = 0, 1, 2
 CODEC_NONE, CODEC_H74, CODEC_H84, CODEC_GOLAY = 0, 1, 2, 3
+SCALE_DIV7, SCALE_MUL_INV7 = 0, 1
+# INT4 row-scale rules (kvecc.h KVECC_SCALE_*): the reference's `abs_max / 7.0`
+# (paged_cache_ecc.py:330) as torch computes it on CPU tensors ("div7", IEEE
+# division) or on GPU tensors ("mul_inv7", abs_max * RN(1/7))
+SCALE_RULES = {"div7": SCALE_DIV7, "mul_inv7": SCALE_MUL_INV7}
+
+
+def scale_rule_code(rule, default):
+    rule = default if rule is None else rule
+    if rule not in SCALE_RULES:
+        raise ValueError(f"unknown scale rule {rule!r}; expected one of {sorted(SCALE_RULES)}")
+    return SCALE_RULES[rule]
 
 
 class KveccError(RuntimeError):

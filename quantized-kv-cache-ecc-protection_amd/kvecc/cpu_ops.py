@@ -364,12 +364,19 @@ def interpolate_double_errors_autotuned(q, error_type, original_shape=None, seq_
 
 _DT = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
 
+# Row-scale rule when the caller names none: the reference's `abs_max / 7.0` as
+# torch evaluates it on this backend's device (CPU tensors: IEEE division;
+# kvecc.h KVECC_SCALE_*).  Pass scale_rule="mul_inv7" to reproduce the reference run
+# on a GPU.
+DEFAULT_SCALE_RULE = "div7"
 
-def quantize_encode_rows_into(x2d, codec_code, cw, scales):
+
+def quantize_encode_rows_into(x2d, codec_code, cw, scales, scale_rule=None):
     if x2d.dtype not in _DT:
         raise TypeError(f"unsupported input dtype {x2d.dtype}")
     rows, d = x2d.shape
-    _lib.call("kvecc_cpu_quantize_encode_rows", _ptr(x2d), _DT[x2d.dtype], int(codec_code), _ptr(cw),
+    _lib.call("kvecc_cpu_quantize_encode_rows", _ptr(x2d), _DT[x2d.dtype], int(codec_code),
+              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), _ptr(cw),
               _ptr(scales), rows, d, NUM_THREADS)
     return cw, scales
 
@@ -381,7 +388,7 @@ def decode_dequant_h84_into(cw2d, scales, out, zero_doubles=True, stats=None):
     return out
 
 
-def _fused_quantize_encode(input_tensor, codec_code):
+def _fused_quantize_encode(input_tensor, codec_code, scale_rule=None):
     _check_cpu(input_tensor)
     if input_tensor.dtype not in _DT:
         raise TypeError(f"unsupported input dtype {input_tensor.dtype}")
@@ -391,23 +398,24 @@ def _fused_quantize_encode(input_tensor, codec_code):
     rows = x.shape[0]
     cw = torch.empty(rows, d, dtype=torch.uint8)
     scales = torch.empty(rows, dtype=torch.float32)
-    _lib.call("kvecc_cpu_quantize_encode_rows", _ptr(x), _DT[x.dtype], int(codec_code), _ptr(cw),
+    _lib.call("kvecc_cpu_quantize_encode_rows", _ptr(x), _DT[x.dtype], int(codec_code),
+              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), _ptr(cw),
               _ptr(scales), rows, d, NUM_THREADS)
     if input_tensor.dim() == 1:
         return cw.squeeze(0), scales
     return cw.view(shape), scales.view(shape[:-1])
 
 
-def fused_quantize_encode_hamming84(input_tensor):
-    return _fused_quantize_encode(input_tensor, _lib.CODEC_H84)
+def fused_quantize_encode_hamming84(input_tensor, scale_rule=None):
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H84, scale_rule)
 
 
-def fused_quantize_encode_hamming74(input_tensor):
-    return _fused_quantize_encode(input_tensor, _lib.CODEC_H74)
+def fused_quantize_encode_hamming74(input_tensor, scale_rule=None):
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H74, scale_rule)
 
 
-def quantize_rows(input_tensor):
-    return _fused_quantize_encode(input_tensor, _lib.CODEC_NONE)
+def quantize_rows(input_tensor, scale_rule=None):
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_NONE, scale_rule)
 
 
 def fused_decode_dequantize_hamming84(codewords, scales, output_dtype=torch.float32):
@@ -437,7 +445,8 @@ SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84"
                "golay": _lib.CODEC_GOLAY}
 
 
-def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0):
+def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0,
+               scale_rule=None):
     batch, seq, _ = k.shape
     if k.dtype not in _DT or v.dtype != k.dtype:
         raise TypeError(f"unsupported K/V dtype {k.dtype}/{v.dtype}")
@@ -445,7 +454,8 @@ def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0
     k, v = k.contiguous(), v.contiguous()
     table = manager.block_table[seq_id]
     _lib.call("kvecc_cpu_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq,
-              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec], int(n_bits),
+              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec],
+              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), int(n_bits),
               int(bool(inject)), float(ber), int(seed0), _ptr(manager.k_cache),
               _ptr(manager.v_cache), _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table),
               manager.num_layers, manager.block_size, int(layer), NUM_THREADS)

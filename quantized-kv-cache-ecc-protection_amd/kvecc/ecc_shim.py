@@ -88,13 +88,17 @@ class ECCShimConfig:
     (default "hip"; unknown names raise ValueError).  ``fused`` runs the cache
     write and read as one launch each (kvecc_shim_write / kvecc_shim_read);
     False composes the per-op kernels (identical bits, kept for A/B tests).
+    ``scale_rule`` picks how the INT4 row scale absmax / 7 is rounded:
+    "mul_inv7" (absmax * RN(1/7), what the reference computes on GPU tensors),
+    "div7" (IEEE division, the reference on CPU tensors) or None for the
+    backend's device (kvecc.h KVECC_SCALE_*).
     """
 
     SUPPORTED_CODECS = {"fp16", "fp8", "int4", "hamming74", "hamming84", "golay"}
 
     def __init__(self, codec="hamming84", ber=0.0, block_size=16, num_blocks=256,
                  inject_errors=False, seed=42, use_interpolation=False, backend="hip",
-                 fused=True):
+                 fused=True, scale_rule=None):
         if codec not in self.SUPPORTED_CODECS:
             raise ValueError(f"Unsupported codec: '{codec}'. "
                              f"Supported codecs: {sorted(self.SUPPORTED_CODECS)}")
@@ -107,6 +111,7 @@ class ECCShimConfig:
         self.use_interpolation = use_interpolation
         self.backend = backend
         self.fused = fused  # one-launch cache write / read (False: per-op kernels)
+        self.scale_rule = scale_rule
 
 
 class SimpleBlockManager:
@@ -260,7 +265,7 @@ class ECCBackend:
         seed0 = cfg.seed + self._injection_count
         if self._fused_ok(k) and k.dtype == v.dtype:
             self.codec_backend.shim_write(k, v, mgr, layer_idx, cfg.codec, _N_BITS[cfg.codec],
-                                          inject, cfg.ber, seed0, seq_id)
+                                          inject, cfg.ber, seed0, seq_id, cfg.scale_rule)
             if inject:
                 self._injection_count += rows
             return
@@ -277,7 +282,7 @@ class ECCBackend:
                 if inject:
                     self._inject_rows(enc, rows, d, seed0 + which)
             else:
-                q, sc = ops.quantize_rows(x)  # shim torch-path rounding, exact
+                q, sc = ops.quantize_rows(x, cfg.scale_rule)  # the shim's torch rounding
                 if codec == "golay":
                     enc = ops.golay_encode_rows(q)
                     row_len = enc.shape[-1]

@@ -411,17 +411,24 @@ def interpolate_double_errors_autotuned(q, error_type, original_shape=None, seq_
 
 _DT = {torch.float32: _lib.F32, torch.float16: _lib.F16, torch.bfloat16: _lib.BF16}
 
+# Row-scale rule when the caller names none: the reference's `abs_max / 7.0` as
+# torch evaluates it on this backend's device (GPU tensors: abs_max * RN(1/7);
+# kvecc.h KVECC_SCALE_*).  Pass scale_rule="div7" to reproduce the reference run
+# on the CPU.
+DEFAULT_SCALE_RULE = "mul_inv7"
 
-def quantize_encode_rows_into(x2d, codec_code, cw, scales):
+
+def quantize_encode_rows_into(x2d, codec_code, cw, scales, scale_rule=None):
     if x2d.dtype not in _DT:
         raise TypeError(f"unsupported input dtype {x2d.dtype}")
     rows, d = x2d.shape
-    _lib.call("kvecc_quantize_encode_rows", _ptr(x2d), _DT[x2d.dtype], int(codec_code), _ptr(cw),
+    _lib.call("kvecc_quantize_encode_rows", _ptr(x2d), _DT[x2d.dtype], int(codec_code),
+              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), _ptr(cw),
               _ptr(scales), rows, d, _stream(x2d.device))
     return cw, scales
 
 
-def _fused_quantize_encode(input_tensor, codec_code):
+def _fused_quantize_encode(input_tensor, codec_code, scale_rule=None):
     _check_gpu(input_tensor)
     shape = input_tensor.shape
     d = shape[-1]
@@ -429,26 +436,26 @@ def _fused_quantize_encode(input_tensor, codec_code):
     rows = x.shape[0]
     cw = torch.empty(rows, d, dtype=torch.uint8, device=input_tensor.device)
     scales = torch.empty(rows, dtype=torch.float32, device=input_tensor.device)
-    quantize_encode_rows_into(x, codec_code, cw, scales)
+    quantize_encode_rows_into(x, codec_code, cw, scales, scale_rule)
     if input_tensor.dim() == 1:
         return cw.squeeze(0), scales
     return cw.view(shape), scales.view(shape[:-1])
 
 
-def fused_quantize_encode_hamming84(input_tensor):
+def fused_quantize_encode_hamming84(input_tensor, scale_rule=None):
     """Row absmax INT4 quantization + Hamming(8,4) encode in one kernel;
     fused_kernels.py:97-160 (matches the shim's torch rounding exactly)."""
-    return _fused_quantize_encode(input_tensor, _lib.CODEC_H84)
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H84, scale_rule)
 
 
-def fused_quantize_encode_hamming74(input_tensor):
+def fused_quantize_encode_hamming74(input_tensor, scale_rule=None):
     """fused_kernels.py:222-269 with Hamming(7,4)."""
-    return _fused_quantize_encode(input_tensor, _lib.CODEC_H74)
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_H74, scale_rule)
 
 
-def quantize_rows(input_tensor):
+def quantize_rows(input_tensor, scale_rule=None):
     """INT4 quantization only (codec 'int4'): -> (nibbles uint8, scales f32)."""
-    return _fused_quantize_encode(input_tensor, _lib.CODEC_NONE)
+    return _fused_quantize_encode(input_tensor, _lib.CODEC_NONE, scale_rule)
 
 
 def decode_dequant_h84_into(cw2d, scales, out, zero_doubles=True, stats=None):
@@ -489,7 +496,8 @@ SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84"
                "golay": _lib.CODEC_GOLAY}
 
 
-def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0):
+def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0,
+               scale_rule=None):
     """ECCBackend.write for one layer (ecc_shim.py:557-721): K, V [batch, seq,
     hkv*d] -> quantize, encode, per-row inject, scatter into manager's caches."""
     batch, seq, _ = k.shape
@@ -498,7 +506,8 @@ def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0
     k, v = k.contiguous(), v.contiguous()
     table = manager.block_table[seq_id]
     _lib.call("kvecc_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq,
-              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec], int(n_bits),
+              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec],
+              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), int(n_bits),
               int(bool(inject)), float(ber), int(seed0), _ptr(manager.k_cache),
               _ptr(manager.v_cache), _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table),
               manager.num_layers, manager.block_size, int(layer), _stream(k.device))

@@ -265,3 +265,28 @@ def test_hamming84_packed_vs_reference_layout(cpu, n):
     assert pst == st
     assert torch.equal(pn, cpu.pack_nibbles(data)) and torch.equal(pt, cpu.pack_error_types(et))
     assert torch.equal(cpu.unpack_nibbles(pn, n), data)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+def test_scale_rules(cpu, oracle, dtype):
+    """Both row-scale rules against the oracle: "div7" (the reference on CPU
+    tensors, the default here) and "mul_inv7" (abs_max * RN(1/7), the
+    reference's `abs_max / 7.0` on a GPU); the rules disagree on many rows."""
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn(500, 64, generator=g) * 3).to(dtype)
+    x[0] = 0
+    inv7 = torch.tensor([1.0]) / torch.tensor([7.0])
+    amax = x.float().abs().amax(-1)
+    scales = {}
+    for rule, code in (("div7", 0), ("mul_inv7", 1)):
+        q, s = cpu.quantize_rows(x, scale_rule=rule)
+        oq, os_ = oracle.quantize_rows(x.float().numpy(), rule=code)
+        assert np.array_equal(q.numpy(), oq) and np.array_equal(s.numpy(), os_), rule
+        cw, s84 = cpu.fused_quantize_encode_hamming84(x, scale_rule=rule)
+        assert torch.equal(s84, s) and np.array_equal(cw.numpy(), oracle.hamming84_encode(oq))
+        scales[rule] = s
+    assert torch.equal(scales["mul_inv7"][1:], amax[1:] * inv7) and scales["mul_inv7"][0] == 1
+    assert torch.equal(cpu.quantize_rows(x)[1], scales["div7"])
+    assert int((scales["div7"] != scales["mul_inv7"]).sum()) > 50
+    with pytest.raises(ValueError):
+        cpu.quantize_rows(x, scale_rule="div8")

@@ -316,9 +316,10 @@ def test_fused_golden(gpu, golden, manifest):
     g = golden("fused")
     for i, c in enumerate(manifest["fused"]["params"]["cases"]):
         x = _t(g[f"c{i}_x"], gpu)
-        cw, s = kvecc.fused_quantize_encode_hamming84(x)
+        # fixtures from the reference on CPU tensors: the IEEE scale rule
+        cw, s = kvecc.fused_quantize_encode_hamming84(x, scale_rule="div7")
         assert np.array_equal(_np(cw), g[f"c{i}_cw84"]) and np.array_equal(_np(s), g[f"c{i}_s84"])
-        cw, s = kvecc.fused_quantize_encode_hamming74(x)
+        cw, s = kvecc.fused_quantize_encode_hamming74(x, scale_rule="div7")
         assert np.array_equal(_np(cw), g[f"c{i}_cw74"])
         out, nc = kvecc.fused_decode_dequantize_hamming84(_t(g[f"c{i}_cw_noisy"], gpu),
                                                           _t(g[f"c{i}_s84"], gpu))
@@ -328,15 +329,23 @@ def test_fused_golden(gpu, golden, manifest):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("shape", [(4096, 128), (333, 64), (17, 100), (5, 7), (2, 3, 256)])
 def test_quantize_vs_torch_path(gpu, oracle, dtype, shape):
-    """Exactly the shim's torch rounding (ecc_shim.py:572-580) for every dtype."""
+    """Exactly the shim's torch rounding (ecc_shim.py:572-580) for every dtype,
+    under both scale rules; the default is the reference's own expression
+    `abs_max / 7.0` (paged_cache_ecc.py:330) evaluated by torch on the GPU."""
     import kvecc
     g = torch.Generator().manual_seed(sum(shape))
     x = (torch.randn(*shape, generator=g) * 3).to(dtype)
     x.view(-1, shape[-1])[0] = 0
     xd = x.to(gpu)
+    for rule, code in (("div7", 0), ("mul_inv7", 1)):
+        q, s = kvecc.ops.quantize_rows(xd, scale_rule=rule)
+        oq, os_ = oracle.quantize_rows(x.float().numpy(), rule=code)
+        assert np.array_equal(_np(q), oq) and np.array_equal(_np(s), os_), rule
     q, s = kvecc.ops.quantize_rows(xd)
-    oq, os_ = oracle.quantize_rows(x.float().numpy())
-    assert np.array_equal(_np(q), oq) and np.array_equal(_np(s), os_)
+    ref = xd.float().abs().amax(-1) / 7.0
+    ref = torch.where(ref == 0, torch.ones_like(ref), ref)
+    ref_q = (torch.round(xd.float() / ref.unsqueeze(-1)).clamp(-8, 7) + 8).to(torch.uint8)
+    assert torch.equal(s, ref) and torch.equal(q, ref_q) and np.array_equal(_np(q), oq)
     cw, s84 = kvecc.fused_quantize_encode_hamming84(xd)
     assert np.array_equal(_np(cw), oracle.hamming84_encode(oq))
     # decode + dequant to the input dtype (== torch .to(dtype) of the fp32 result)

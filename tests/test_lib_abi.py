@@ -151,3 +151,22 @@ def test_host_twins_reject_null_buffers():
         if not name.startswith("kvecc_cpu_") or ctypes.c_int64 not in args_t:
             continue
         assert _call_with(lib, name, args_t, 8) == -1, name
+
+
+def test_quantizers_reject_unknown_scale_rule():
+    """KVECC_SCALE_* is validated on every quantizing entry point (host twins
+    run here; the device entry points validate before any launch)."""
+    from kvecc import _lib
+    lib = _lib.load()
+    x = (ctypes.c_float * 8)()
+    cw = (ctypes.c_uint8 * 8)()
+    sc = (ctypes.c_float * 2)()
+    for rule, want in ((2, -1), (-1, -1), (1, 0), (0, 0)):
+        rc = lib.kvecc_cpu_quantize_encode_rows(x, _lib.F32, _lib.CODEC_H84, rule, cw, sc, 2, 4, 1)
+        assert rc == want, (rule, rc)
+    assert lib.kvecc_cpu_quantize_encode_rows(x, _lib.F32, 0, 5, cw, sc, 2, 4, 1) == -1
+    assert "scale rule" in lib.kvecc_last_error().decode()
+    header = open(HEADER).read()
+    for fn in ("kvecc_quantize_encode_rows", "kvecc_shim_write", "kvecc_cpu_quantize_encode_rows",
+               "kvecc_cpu_shim_write"):
+        assert "scale_rule" in header.split(fn + "(")[1].split(";")[0], fn

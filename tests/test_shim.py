@@ -57,9 +57,10 @@ def _shim_matches_reference(device, backend, golden, manifest):
                                 reset_ecc_cache)
     model, ids, g = _model(golden, manifest, device)
     for i, run in enumerate(manifest["shim_gpt2"]["params"]["runs"]):
+        # the fixtures come from the reference run on CPU tensors: IEEE scale division
         cfg = ECCShimConfig(codec=run["codec"], ber=run["ber"], inject_errors=run["ber"] > 0,
                             seed=42, block_size=16, use_interpolation=run["use_interpolation"],
-                            backend=backend)
+                            backend=backend, scale_rule="div7")
         with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=16):
             reset_ecc_cache(model)
             out = model(ids)
@@ -96,7 +97,9 @@ def _cache_bits_match_oracle(gpu, backend):
         be.write(k, v, layer_idx=1)
         assert be._injection_count == 5 + b * s * hk
         for which, x, cache in ((0, k, mgr.k_cache), (1, v, mgr.v_cache)):
-            q, _ = oracle.quantize_rows(x.float().cpu().numpy().reshape(b, s, hk, d))
+            # default scale rule: the reference on this backend's device
+            q, _ = oracle.quantize_rows(x.float().cpu().numpy().reshape(b, s, hk, d),
+                                        rule=1 if backend == "hip" else 0)
             last = q[-1]  # last batch wins
             for pos in range(s):
                 for h in range(hk):
