@@ -1,5 +1,8 @@
 // codec_math.h -- the codec algebra, shared by the gfx950 kernels and the
 // host ("cpu" backend) implementation: one definition of every bit operation.
+// The Hamming codecs have two forms of the same function -- v_perm byte tables
+// on the device, shifts/XORs on the host -- which tests/native/codec_math_check.cpp
+// proves equal on every byte value in every byte lane.
 //
 // References (ecc_codecs/triton_kernels/): hamming74_triton.py:48-162,
 // hamming84_triton.py:50-209, golay_triton.py:99-295,
@@ -30,21 +33,64 @@ KV_HD uint32_t byte_parity4(uint32_t y) {
 
 // ---- Hamming(7,4) / Hamming(8,4), four codewords per word (SWAR) -------------
 
-KV_HD uint32_t h74_encode4(uint32_t w) {
-  uint32_t x = w & 0x0F0F0F0Fu;
-  uint32_t d0 = x & 0x01010101u, d1 = (x >> 1) & 0x01010101u;
-  uint32_t d2 = (x >> 2) & 0x01010101u, d3 = (x >> 3) & 0x01010101u;
-  return x | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6;
+// v_perm_b32 for selectors 0..7: byte i = byte sel.byte[i] of (hi:lo)
+KV_HD uint32_t byte_perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+  const uint64_t t = (uint64_t)hi << 32 | lo;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) r |= (uint32_t)(t >> (8 * ((sel >> (8 * i)) & 7)) & 0xFFu) << (8 * i);
+  return r;
+#endif
 }
 
-KV_HD uint32_t h84_encode4(uint32_t w) {
-  uint32_t x = w & 0x0F0F0F0Fu;
+// Encoders.  Parity is linear in the data bits: the device looks the parity
+// byte of (d0,d1,d2) up in an 8-entry v_perm table and XORs in d3's (it flips
+// p0, p1 and p2; the H84 overall parity P reduces to d0^d1^d2).
+constexpr uint64_t h_enc_table(bool overall) {
+  uint64_t t = 0;
+  for (uint32_t v = 0; v < 8; ++v) {
+    const uint32_t d0 = v & 1, d1 = v >> 1 & 1, d2 = v >> 2 & 1;
+    const uint32_t e = (d0 ^ d1) << 4 | (d0 ^ d2) << 5 | (d1 ^ d2) << 6 |
+                       (overall ? (d0 ^ d1 ^ d2) << 7 : 0u);
+    t |= (uint64_t)e << (8 * v);
+  }
+  return t;
+}
+constexpr uint64_t kH74Enc = h_enc_table(false), kH84Enc = h_enc_table(true);
+
+template <bool OVERALL>
+KV_HD uint32_t h_encode4_tables(uint32_t w) {
+  const uint32_t x = w & 0x0F0F0F0Fu;
+  constexpr uint64_t t = OVERALL ? kH84Enc : kH74Enc;
+  const uint32_t p012 = byte_perm((uint32_t)(t >> 32), (uint32_t)t, x & 0x07070707u);
+  const uint32_t p3 = byte_perm(0u, 0x7000u, (x >> 3) & 0x01010101u);  // d3 -> 0x70
+  return x | (p012 ^ p3);
+}
+
+template <bool OVERALL>
+KV_HD uint32_t h_encode4_shifts(uint32_t w) {
+  const uint32_t x = w & 0x0F0F0F0Fu;
   uint32_t d0 = x & 0x01010101u, d1 = (x >> 1) & 0x01010101u;
   uint32_t d2 = (x >> 2) & 0x01010101u, d3 = (x >> 3) & 0x01010101u;
   // parity of the 7-bit word reduces to d0^d1^d2 (p0^p1^p2 = d3)
   return x | (d0 ^ d1 ^ d3) << 4 | (d0 ^ d2 ^ d3) << 5 | (d1 ^ d2 ^ d3) << 6 |
-         (d0 ^ d1 ^ d2) << 7;
+         (OVERALL ? (d0 ^ d1 ^ d2) << 7 : 0u);
 }
+
+// the device uses the tables, the host the shift form (tests/native checks they agree)
+template <bool OVERALL>
+KV_HD uint32_t h_encode4(uint32_t w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return h_encode4_tables<OVERALL>(w);
+#else
+  return h_encode4_shifts<OVERALL>(w);
+#endif
+}
+
+KV_HD uint32_t h74_encode4(uint32_t w) { return h_encode4<false>(w); }
+KV_HD uint32_t h84_encode4(uint32_t w) { return h_encode4<true>(w); }
 
 // Syndrome bits (bit 0 of each byte) of four packed codewords, rows of H
 // (config.py:296-304): s0 over bits {0,1,3,4}, s1 {0,2,3,5}, s2 {1,2,3,6}.
@@ -61,23 +107,94 @@ struct HammingSyndrome {
   }
 };
 
+// ---- the same syndromes through byte-permute tables (device) -----------------
+//
+// v_perm_b32 looks up four bytes at once in an 8-byte table held in two
+// registers.  The syndrome is linear, so the bit fields {0,1,2}, {3,4,5} and
+// {6,7} of each codeword byte index three tables whose entries are the XOR of
+// the H columns of the set bits (d0 -> 3, d1 -> 5, d2 -> 6, d3 -> 7, p0 -> 1,
+// p1 -> 2, p2 -> 4, P -> 0) in bits 0..2 and the field's parity replicated in
+// bits 4..7; XORing the three lookups gives syndrome | overall-parity x 0xF.
+// A fourth table maps the syndrome to the data-bit correction | nz << 4.
+// About half the VALU work of the shift/XOR form; the host keeps that form.
+
+// table entry for field value v whose bits carry H columns c0, c1, c2
+constexpr uint32_t h_field_entry(uint32_t v, uint32_t c0, uint32_t c1, uint32_t c2) {
+  return ((v & 1 ? c0 : 0) ^ (v & 2 ? c1 : 0) ^ (v & 4 ? c2 : 0)) |
+         (((v ^ (v >> 1) ^ (v >> 2)) & 1) ? 0xF0u : 0u);
+}
+constexpr uint64_t h_field_table(uint32_t c0, uint32_t c1, uint32_t c2) {
+  uint64_t t = 0;
+  for (uint32_t v = 0; v < 8; ++v) t |= (uint64_t)h_field_entry(v, c0, c1, c2) << (8 * v);
+  return t;
+}
+constexpr uint64_t kHField0 = h_field_table(3, 5, 6);  // d0 d1 d2
+constexpr uint64_t kHField1 = h_field_table(7, 1, 2);  // d3 p0 p1
+constexpr uint64_t kHField2 = h_field_table(4, 0, 0);  // p2 P (2-bit field)
+// syndrome -> data correction (one-hot d0..d3 when the syndrome is a data
+// column 3/5/6/7) | (syndrome != 0) << 4
+constexpr uint64_t h_fix_table() {
+  uint64_t t = 0;
+  for (uint32_t s = 1; s < 8; ++s) {
+    const uint32_t fix = s == 3 ? 1u : s == 5 ? 2u : s == 6 ? 4u : s == 7 ? 8u : 0u;
+    t |= (uint64_t)(fix | 0x10u) << (8 * s);
+  }
+  return t;
+}
+constexpr uint64_t kHFix = h_fix_table();
+
+// syndrome (bits 0..2) | overall parity x 0xF0 (bits 4..7), per byte
+KV_HD uint32_t h_code4(uint32_t w) {
+  const uint32_t a = byte_perm((uint32_t)(kHField0 >> 32), (uint32_t)kHField0, w & 0x07070707u);
+  const uint32_t b = byte_perm((uint32_t)(kHField1 >> 32), (uint32_t)kHField1, (w >> 3) & 0x07070707u);
+  const uint32_t c = byte_perm((uint32_t)(kHField2 >> 32), (uint32_t)kHField2, (w >> 6) & 0x03030303u);
+  return a ^ b ^ c;
+}
+
+// Table form of the syndrome of four codewords: fx = correction (bits 0..3) |
+// nz << 4 per byte; pe_rep = parity error replicated in bits 0..3 of each byte
+// (bits 4..7 carry the next byte's syndrome: mask before use).
+struct HammingTables {
+  uint32_t fx, pe_rep;
+  KV_HD explicit HammingTables(uint32_t w) {
+    const uint32_t code = h_code4(w);
+    fx = byte_perm((uint32_t)(kHFix >> 32), (uint32_t)kHFix, code & 0x07070707u);
+    pe_rep = code >> 4;
+  }
+  KV_HD uint32_t nz() const { return (fx >> 4) & 0x01010101u; }
+  KV_HD uint32_t pe() const { return pe_rep & 0x01010101u; }
+};
+
 // SECDED decode of four packed codewords: data nibbles, ErrorType bytes
 KV_HD void h84_decode4(uint32_t w, uint32_t &data, uint32_t &type, uint32_t &n_single,
                        uint32_t &n_double) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const HammingTables t(w);
+  data = (w ^ (t.fx & t.pe_rep)) & 0x0F0F0F0Fu;  // correct only SINGLE (pe && nz)
+  const uint32_t pe = t.pe(), nz = t.nz();
+#else
   HammingSyndrome s(w);
-  uint32_t pe = byte_parity4(w);  // stored overall parity != parity(bits 0..6)
+  const uint32_t pe = byte_parity4(w);  // stored overall parity != parity(bits 0..6)
   data = (w ^ (s.fix & (pe * 0x0Fu))) & 0x0F0F0F0Fu;  // correct only SINGLE (pe && nz)
+  const uint32_t nz = s.nz;
+#endif
   // (nz,pe) = (0,0)->0, (1,1)->1, (1,0)->2, (0,1)->3 (hamming84_triton.py:185-187)
-  type = pe | (pe ^ s.nz) << 1;
-  n_single += __builtin_popcount(pe & s.nz);
-  n_double += __builtin_popcount(~pe & s.nz);
+  type = pe | (pe ^ nz) << 1;
+  n_single += __builtin_popcount(pe & nz);
+  n_double += __builtin_popcount(~pe & nz);
 }
 
 KV_HD void h74_decode4(uint32_t w, uint32_t &data, uint32_t &flag, uint32_t &n_flag) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const HammingTables t(w);  // bit 7 only moves the parity lane, unused here
+  data = (w ^ t.fx) & 0x0F0F0F0Fu;  // doubles are miscorrected, as in the reference
+  flag = t.nz();
+#else
   HammingSyndrome s(w);
   data = (w ^ s.fix) & 0x0F0F0F0Fu;  // doubles are miscorrected, as in the reference
   flag = s.nz;
-  n_flag += __builtin_popcount(s.nz);
+#endif
+  n_flag += __builtin_popcount(flag);
 }
 
 // single nibble -> codeword (codec: 0 raw, 1 H74, 2 H84 -- KVECC_CODEC_*)

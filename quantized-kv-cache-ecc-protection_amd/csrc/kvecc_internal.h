@@ -75,6 +75,30 @@ __device__ __forceinline__ __hip_bfloat16 from_f32<__hip_bfloat16>(float v) {
 }
 
 
+// DPP move inside a 16-lane row (CTRL: quad_perm 0x00-0xFF, row_mirror 0x140,
+// row_half_mirror 0x141); no LDS round trip, unlike __shfl_xor's ds_bpermute
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
+}
+
+// max over each aligned group of G lanes (G a power of two <= 64) of
+// NON-NEGATIVE floats, result in every lane of the group.  Non-negative floats
+// order like their bit patterns, so this is an unsigned max, which lets the
+// DPP move fold into v_max_u32 (no canonicalize).  DPP for the steps inside a
+// row, ds_bpermute across rows.
+template <int G>
+__device__ __forceinline__ float group_max_nonneg(float v) {
+  uint32_t u = __float_as_uint(v);
+  if (G >= 2) u = max(u, dpp_u32<0xB1>(u));    // quad_perm [1,0,3,2]: lane ^ 1
+  if (G >= 4) u = max(u, dpp_u32<0x4E>(u));    // quad_perm [2,3,0,1]: lane ^ 2
+  if (G >= 8) u = max(u, dpp_u32<0x141>(u));   // row_half_mirror: quad 0 <-> quad 1
+  if (G >= 16) u = max(u, dpp_u32<0x140>(u));  // row_mirror: half 0 <-> half 1
+  if (G >= 32) u = max(u, (uint32_t)__shfl_xor((int)u, 16, kWave));
+  if (G >= 64) u = max(u, (uint32_t)__shfl_xor((int)u, 32, kWave));
+  return __uint_as_float(u);
+}
+
 // wave-wide sum (all 64 lanes participate)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll

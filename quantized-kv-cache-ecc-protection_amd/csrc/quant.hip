@@ -80,16 +80,16 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
 // Rows of at most 64 chunks (every row of the shim and the reference's tests):
 // each lane loads its one 16-byte chunk ONCE, non-temporally, and two row
 // groups are in flight per iteration.
-template <typename T, int VEC>
+template <typename T, int VEC, int LPR>
 __global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__restrict__ x, int codec,
                                                                     int rule, uint8_t *__restrict__ cw,
                                                                     float *__restrict__ scales,
-                                                                    int64_t rows, int64_t d, int lpr) {
+                                                                    int64_t rows, int64_t d) {
   static_assert(sizeof(T) * VEC == 16, "one 16-byte chunk per lane");
   constexpr int kU = 2;
+  constexpr int rows_per_wave = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
-  const int rows_per_wave = kWave / lpr;
-  const int sub = lane / lpr, li = lane % lpr;
+  const int sub = lane / LPR, li = lane % LPR;
   const int64_t nchunk = d / VEC;
   const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
   const int64_t wave_id = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__r
         f[k] = live[u] ? to_f32<T>(v[u].v[k]) : 0.0f;
         amax = fmaxf(amax, fabsf(f[k]));
       }
-      amax = row_max(amax, lpr);
+      amax = group_max_nonneg<LPR>(amax);
       const float scale = row_scale(amax, rule);
       if (!live[u]) continue;
       if (li == 0) scales[r] = scale;
@@ -192,13 +192,14 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_kernel(const uint8_t *_
 // d must be a multiple): each lane reads 4 or 8 codeword bytes and writes one
 // contiguous 16-byte output vector, so every wave-instruction covers one
 // contiguous span; non-temporal, kU accesses in flight per lane.  Row indices
-// use 32-bit division (64-bit division is ~100 instructions).
+// are a shift when the chunks per row are a power of two (shift >= 0), else a
+// 32-bit division (64-bit division is ~100 instructions).
 template <typename TO>
 __global__ __launch_bounds__(kBlock) void decode_dequant_wide_kernel(const uint32_t *__restrict__ cw,
                                                                      const float *__restrict__ scales,
                                                                      TO *__restrict__ out,
-                                                                     uint32_t nchunk, uint32_t total,
-                                                                     int zero_doubles,
+                                                                     uint32_t nchunk, int shift,
+                                                                     uint32_t total, int zero_doubles,
                                                                      uint64_t *__restrict__ stats) {
   constexpr int kU = 4;
   constexpr int kW = 4 / sizeof(TO);  // codeword words per access
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_wide_kernel(const uint3
   auto one = [&](InT in, uint32_t i) {
     uint32_t w[kW];
     __builtin_memcpy(w, &in, sizeof(in));
-    const float s = scales[i / nchunk];
+    const float s = scales[shift >= 0 ? i >> shift : i / nchunk];
     TO o[4 * kW];
 #pragma unroll
     for (int k = 0; k < kW; ++k) {
@@ -251,10 +252,18 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
   const T *xt = reinterpret_cast<const T *>(x);
   bool vec = d % V == 0 && aligned(x, 16) && aligned(cw, V);
   if (vec && d / V <= kWave) {
-    int lpr = lanes_per_row(d / V);
-    int64_t waves = cdiv(rows, kWave / lpr);
-    hipLaunchKernelGGL((quantize_encode_1c_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave, 16)),
-                       dim3(kBlock), 0, st, xt, codec, rule, cw, scales, rows, d, lpr);
+    const int lpr = lanes_per_row(d / V);
+    const unsigned grid = grid_for(cdiv(rows, kWave / lpr), kBlock / kWave, 16);
+#define KVECC_QE1C(L)                                                                         \
+  case L:                                                                                     \
+    hipLaunchKernelGGL((quantize_encode_1c_kernel<T, V, L>), dim3(grid), dim3(kBlock), 0, st, xt, \
+                       codec, rule, cw, scales, rows, d);                                     \
+    break;
+    switch (lpr) {
+      KVECC_QE1C(1) KVECC_QE1C(2) KVECC_QE1C(4) KVECC_QE1C(8) KVECC_QE1C(16) KVECC_QE1C(32)
+      KVECC_QE1C(64)
+    }
+#undef KVECC_QE1C
   } else if (vec) {
     int lpr = lanes_per_row(d / V);
     int64_t waves = cdiv(rows, kWave / lpr);
@@ -275,9 +284,11 @@ static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t
   constexpr int kCw = 16 / sizeof(TO);  // codewords per 16-byte output vector
   if (d % kCw == 0 && aligned(cw, kCw) && aligned(out, 16) && rows * d < 0xFFFFFFFFLL) {
     const uint32_t total = (uint32_t)(rows * (d / kCw));
+    const uint32_t nchunk = (uint32_t)(d / kCw);
+    const int shift = (nchunk & (nchunk - 1)) == 0 ? __builtin_ctz(nchunk) : -1;
     hipLaunchKernelGGL((decode_dequant_wide_kernel<TO>), dim3(grid_for(total, kBlock * 4, 16)),
                        dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o,
-                       (uint32_t)(d / kCw), total, zero_doubles, stats);
+                       nchunk, shift, total, zero_doubles, stats);
   } else if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
     int64_t total = rows * (d / 4);
     hipLaunchKernelGGL((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),
