@@ -98,16 +98,33 @@ def cpu_baseline(budget_s, threads):
             if el >= budget_s:
                 break
     return {"value": done / el, "unit": "codewords/s", "cores": threads, "kind": "port",
+            "host": host_info(),
             "sample": f"{done} codewords of Golay encode+decode (BER 1e-2 on a slice) in {el:.1f} s, "
                       f"oracle/kvecc_oracle.c on {threads} host threads"}
+
+
+def host_info():
+    """CPU model, visible cores and OMP_NUM_THREADS of the host."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
+                         None)
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_backend_baseline(budget_s, threads):
     """The product's host backend (kvecc.cpu_ops, backend="cpu": the kernels'
     codec algebra on std::threads) on the FULL per-GPU workload: Golay encode +
-    decode of M = 45,088,768 codewords, repeated for ~budget_s."""
+    decode of M = 45,088,768 codewords.  One warm-up pass, then the median of
+    the passes that fit in ~budget_s (at least 5) on `threads` threads, and the
+    median of 3 passes on 1 thread."""
+    import statistics
+
     from kvecc import cpu_ops
-    cpu_ops.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     x = torch.randint(0, 16, (B, L, H, D), generator=g, dtype=torch.uint8)
     gsz = (D + 2) // 3
@@ -116,21 +133,31 @@ def cpu_backend_baseline(budget_s, threads):
     trip = trip.view(-1, 3)
     del x
     m = trip.shape[0]
+    cpu_ops.set_num_threads(threads)
     cw = cpu_ops.golay_encode(trip)
     noisy = cpu_ops.inject_bit_errors_triton(cw, BER, 24, SEED)
-    done, reps = 0, 0
-    t0 = time.perf_counter()
-    while True:
-        cpu_ops.golay_encode(trip)
+
+    def passes(n_threads, min_reps, budget):
+        cpu_ops.set_num_threads(n_threads)
+        cpu_ops.golay_encode(trip)  # warm-up
         cpu_ops.golay_decode(noisy)
-        done += m
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    return {"value": done / el, "unit": "codewords/s", "cores": threads, "kind": "host-backend",
-            "sample": f"{reps} x full [8,4096,32,128] Golay encode+decode ({m} codewords, BER 1e-2) "
-                      f"in {el:.1f} s, kvecc.cpu_ops on {threads} host threads"}
+        times, t_start = [], time.perf_counter()
+        while len(times) < min_reps or time.perf_counter() - t_start < budget:
+            t0 = time.perf_counter()
+            cpu_ops.golay_encode(trip)
+            cpu_ops.golay_decode(noisy)
+            times.append(time.perf_counter() - t0)
+        return statistics.median(times), len(times)
+
+    med, reps = passes(threads, 5, budget_s)
+    med1, reps1 = passes(1, 3, 0.0)
+    cpu_ops.set_num_threads(threads)
+    return {"value": m / med, "unit": "codewords/s", "cores": threads, "kind": "host-backend",
+            "one_thread": {"value": m / med1, "passes": reps1},
+            "host": host_info(),
+            "sample": f"median of {reps} passes of full [8,4096,32,128] Golay encode+decode "
+                      f"({m} codewords, BER 1e-2) after a warm-up, kvecc.cpu_ops on {threads} "
+                      f"host threads; one_thread: median of {reps1} passes on 1 thread"}
 
 
 def main():
