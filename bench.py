@@ -136,16 +136,24 @@ def cpu_backend_baseline(budget_s, threads):
     cpu_ops.set_num_threads(threads)
     cw = cpu_ops.golay_encode(trip)
     noisy = cpu_ops.inject_bit_errors_triton(cw, BER, 24, SEED)
+    # outputs allocated once, as on the GPU side (fresh tensors per pass would
+    # time the kernel's page faults on first touch, not the codec)
+    flat = trip.view(-1)
+    out_trip = torch.empty(m * 3, dtype=torch.uint8)
+    counts = torch.empty(m, dtype=torch.uint8)
+    st = cpu_ops.new_stats()
+
+    def one_pass():
+        cpu_ops.golay_encode_into(flat, cw, m)
+        cpu_ops.golay_decode_into(noisy, out_trip, counts, st)
 
     def passes(n_threads, min_reps, budget):
         cpu_ops.set_num_threads(n_threads)
-        cpu_ops.golay_encode(trip)  # warm-up
-        cpu_ops.golay_decode(noisy)
+        one_pass()  # warm-up
         times, t_start = [], time.perf_counter()
         while len(times) < min_reps or time.perf_counter() - t_start < budget:
             t0 = time.perf_counter()
-            cpu_ops.golay_encode(trip)
-            cpu_ops.golay_decode(noisy)
+            one_pass()
             times.append(time.perf_counter() - t0)
         return statistics.median(times), len(times)
 
