@@ -16,9 +16,13 @@ own [8,4096,32,128] shard (global codeword offset rank*M, so the fault pattern
 equals a single-device run over the concatenated tensor); no collective in the
 data path, one RCCL all_reduce of the decode statistics after timing.
 
-Roofline: HIP events on the launching stream around encode and decode of
-every --event-every'th timed step (sampled, because each event record costs
-~2 us of stream time); achieved = 8 B/codeword * M / mean decode time.
+Roofline: on every --event-every'th timed step the encode and decode kernels
+carry a pair of HIP events in their own dispatch (kvecc_time_next_launch ->
+hipExtLaunchKernel), so the stamps are the kernels' own start and end (they
+agree with rocprofv3's kernel durations); achieved = 8 B/codeword * M / mean
+decode time.  Such a dispatch costs the step ~8 us, hence the sampling.
+--timing markers brackets the launches with hipEventRecord instead (each record
+adds ~2-4 us to the bracketed kernel's time).
 
 Prints ONE JSON line on rank 0.
 """
@@ -57,9 +61,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-inject", action="store_true")
     ap.add_argument("--no-packed", action="store_true")
+    ap.add_argument("--timing", choices=("kernel", "markers"), default="kernel",
+                    help="kernel: events carried by each timed launch (hipExtLaunchKernel); "
+                         "markers: hipEventRecord around the launches of sampled steps")
     ap.add_argument("--event-every", type=int, default=10,
-                    help="record the per-kernel HIP events on every k-th timed step (each event "
-                         "record adds ~2 us of stream time; every step cost 9%% of throughput)")
+                    help="time the kernels of every k-th timed step (a timed dispatch costs the "
+                         "step ~8 us; timing every step cost 7-9%% of throughput)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -206,20 +213,31 @@ def main():
     stats = ops.new_stats(dev)
     torch.cuda.synchronize()
 
+    kernel_timing = args.timing == "kernel"
+
     def step(ev=None):
-        if ev is not None:
+        if ev is not None and kernel_timing:
+            ops.time_next_launch(ev[0], ev[1])
+        elif ev is not None:
             ev[0].record()
         ops.golay_encode_into(trip.view(-1), cw, m)
-        if ev is not None:
+        if ev is not None and kernel_timing:
+            ops.time_next_launch(ev[2], ev[3])
+        elif ev is not None:
             ev[1].record()
         ops.golay_decode_into(noisy, out_trip, counts, stats)
-        if ev is not None:
+        if ev is not None and not kernel_timing:
             ev[2].record()
 
     for _ in range(args.warmup):
         step()
     stats.zero_()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if kernel_timing:  # (enc start, enc end, dec start, dec end) per step, handles created
+        events = [ops.kernel_timer(dev) + ops.kernel_timer(dev) for _ in range(args.steps)]
+    else:
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                  for _ in range(args.steps)]
+    torch.cuda.synchronize()
 
     def barrier():
         if dist is not None:
@@ -228,7 +246,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # sampled steps every-1, 2*every-1, ... (not step 0, right behind the sync)
+    # steps every-1, 2*every-1, ... (not step 0, right behind the sync): a
+    # timed dispatch also costs the step ~8 us (kernel) or ~4 us (markers)
     sampled = list(range(args.event_every - 1, args.steps, args.event_every)) or [args.steps - 1]
     for k in range(args.steps):
         step(events[k] if k in sampled else None)
@@ -238,8 +257,12 @@ def main():
 
     elapsed = t1 - t0
     timed = [events[k] for k in sampled]
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in timed) / len(timed)
-    dec_ms = sum(e[1].elapsed_time(e[2]) for e in timed) / len(timed)
+    if kernel_timing:
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in timed) / len(timed)
+        dec_ms = sum(e[2].elapsed_time(e[3]) for e in timed) / len(timed)
+    else:
+        enc_ms = sum(e[0].elapsed_time(e[1]) for e in timed) / len(timed)
+        dec_ms = sum(e[1].elapsed_time(e[2]) for e in timed) / len(timed)
     tt = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
     st = ops.stats_totals(stats)
     if dist is not None:
@@ -346,7 +369,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": dec_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": dec_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "golay_decode_kernel", "bytes_per_launch": DECODE_BYTES_PER_CW * m,
-                     "timing": f"HIP events on every {args.event_every}th timed step"},
+                     "timing": (f"HIP events carried by the kernel dispatches (hipExtLaunchKernel) "
+                                f"of every {args.event_every}th timed step" if kernel_timing else
+                                f"hipEventRecord markers on every {args.event_every}th timed step")},
         "decode_stats": {"bits_corrected": bits, "uncorrectable": unc, "steps": args.steps},
         "inject": inject,
         "packed": packed,

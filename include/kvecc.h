@@ -66,6 +66,13 @@ enum { KVECC_SCALE_DIV7 = 0, KVECC_SCALE_MUL_INV7 = 1 };
 KVECC_API const char *kvecc_version(void);
 KVECC_API const char *kvecc_last_error(void);
 KVECC_API int kvecc_device_count(void);
+/* Kernel timing without marker packets: the NEXT kernel this thread launches
+ * through any kvecc_* device entry point records its own start and end into
+ * the given hipEvent_t's (either may be NULL) via hipExtLaunchKernel, then the
+ * hook disarms.  Entry points that launch a main kernel and a tail kernel time
+ * the first one.  The reference has no counterpart (benchmark_harness.py:42-57
+ * brackets launches with events); bench.py uses this to time every step. */
+KVECC_API int kvecc_time_next_launch(void *start_event, void *stop_event);
 /* Upload the Golay tables to `device` (done lazily otherwise; call before graph
  * capture).  Replaces golay_triton.py:304-330 (_build_syndrome_table cache). */
 KVECC_API int kvecc_init_device(int device);

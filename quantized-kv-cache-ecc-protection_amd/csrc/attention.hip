@@ -305,7 +305,7 @@ static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
   switch (w) {
 #define KVECC_ATTN_CASE(WW)                                                                       \
   case WW:                                                                                        \
-    hipLaunchKernelGGL((paged_attn_split_kernel<T, CODEC, VEC, WW>), grid, dim3(kBlock), 0, st, a); \
+    KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, WW>), grid, dim3(kBlock), 0, st, a); \
     return KVECC_OK;
     KVECC_ATTN_CASE(1)
     KVECC_ATTN_CASE(2)
@@ -332,7 +332,7 @@ static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
   else
     rc = launch_split<T, CODEC, 1>(a, grid, st);
   if (rc != KVECC_OK) return rc;
-  hipLaunchKernelGGL(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
+  KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
   return KVECC_OK;
 }
 

@@ -232,7 +232,7 @@ KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, in
     int64_t ntiles = m / kEncTile;
     if (ntiles > 0) {
       unsigned g = grid_for(ntiles, 1, 16);  // <= 16 workgroups per CU, grid-strided
-      hipLaunchKernelGGL(golay_encode_kernel, dim3(g), dim3(kEncBlock), 0, st,
+      KVECC_LAUNCH(golay_encode_kernel, dim3(g), dim3(kEncBlock), 0, st,
                          reinterpret_cast<const uint32_t *>(triplets),
                          reinterpret_cast<u32x4 *>(codewords), ntiles, par);
     }
@@ -240,7 +240,7 @@ KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, in
   }
   if (done < m) {
     unsigned g = grid_for(m - done, kBlock);
-    hipLaunchKernelGGL(golay_encode_tail_kernel, dim3(g), dim3(kBlock), 0, st, triplets, codewords,
+    KVECC_LAUNCH(golay_encode_tail_kernel, dim3(g), dim3(kBlock), 0, st, triplets, codewords,
                        done, m, par);
   }
   return check_launch("golay_encode");
@@ -265,19 +265,19 @@ KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, ui
       auto n = reinterpret_cast<uint32_t *>(counts);
       const dim3 b(kDecBlock);
       if (counts && stats)
-        hipLaunchKernelGGL((golay_decode_kernel<true, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<true, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
       else if (counts)
-        hipLaunchKernelGGL((golay_decode_kernel<true, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<true, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
       else if (stats)
-        hipLaunchKernelGGL((golay_decode_kernel<false, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<false, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
       else
-        hipLaunchKernelGGL((golay_decode_kernel<false, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<false, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
     }
     done = ntiles * kDecTile;
   }
   if (done < m) {
     unsigned g = grid_for(m - done, kBlock);
-    hipLaunchKernelGGL(golay_decode_tail_kernel, dim3(g), dim3(kBlock), 0, st, codewords, triplets,
+    KVECC_LAUNCH(golay_decode_tail_kernel, dim3(g), dim3(kBlock), 0, st, codewords, triplets,
                        counts, done, m, par, cor, stats);
   }
   return check_launch("golay_decode");
@@ -292,7 +292,7 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
   if (!par) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
   unsigned grid = grid_for(rows * g, kBlock);
-  hipLaunchKernelGGL(golay_encode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
+  KVECC_LAUNCH(golay_encode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
                      nibbles, codewords, rows, d, g, par);
   return check_launch("golay_encode_rows");
 }
@@ -307,7 +307,7 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
   if (!par || !cor) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
   unsigned grid = grid_for(rows * g, kBlock);
-  hipLaunchKernelGGL(golay_decode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
+  KVECC_LAUNCH(golay_decode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
                      codewords, nibbles, rows, d, g, par, cor, stats);
   return check_launch("golay_decode_rows");
 }

@@ -142,14 +142,14 @@ static int launch_encode(const uint8_t *in, uint8_t *out, int64_t n, void *strea
     int64_t nvec = n / 16;
     if (nvec > 0) {
       unsigned g = grid_for(nvec, (int64_t)kBlock * kUnroll, kPerCu);
-      hipLaunchKernelGGL(encode_kernel<Op>, dim3(g), dim3(kBlock), 0, st,
+      KVECC_LAUNCH(encode_kernel<Op>, dim3(g), dim3(kBlock), 0, st,
                          reinterpret_cast<const u32x4 *>(in), reinterpret_cast<u32x4 *>(out), nvec);
     }
     done = nvec * 16;
   }
   if (done < n) {
     unsigned g = grid_for(n - done, kBlock);
-    hipLaunchKernelGGL(encode_bytes_kernel<Op>, dim3(g), dim3(kBlock), 0, st, in, out, done, n);
+    KVECC_LAUNCH(encode_bytes_kernel<Op>, dim3(g), dim3(kBlock), 0, st, in, out, done, n);
   }
   return check_launch(name);
 }
@@ -170,19 +170,19 @@ static int launch_decode(const uint8_t *cw, uint8_t *data, uint8_t *aux, int64_t
       auto d = reinterpret_cast<u32x4 *>(data);
       auto a = reinterpret_cast<u32x4 *>(aux);
       if (aux && stats)
-        hipLaunchKernelGGL((decode_kernel<H84, true, true>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
+        KVECC_LAUNCH((decode_kernel<H84, true, true>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
       else if (aux)
-        hipLaunchKernelGGL((decode_kernel<H84, true, false>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
+        KVECC_LAUNCH((decode_kernel<H84, true, false>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
       else if (stats)
-        hipLaunchKernelGGL((decode_kernel<H84, false, true>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
+        KVECC_LAUNCH((decode_kernel<H84, false, true>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
       else
-        hipLaunchKernelGGL((decode_kernel<H84, false, false>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
+        KVECC_LAUNCH((decode_kernel<H84, false, false>), dim3(g), dim3(kBlock), 0, st, c, d, a, nvec, stats);
     }
     done = nvec * 16;
   }
   if (done < n) {
     unsigned g = grid_for(n - done, kBlock);
-    hipLaunchKernelGGL(decode_bytes_kernel<H84>, dim3(g), dim3(kBlock), 0, st, cw, data, aux, done, n, stats);
+    KVECC_LAUNCH(decode_bytes_kernel<H84>, dim3(g), dim3(kBlock), 0, st, cw, data, aux, done, n, stats);
   }
   return check_launch(name);
 }

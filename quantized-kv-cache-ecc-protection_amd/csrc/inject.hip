@@ -179,16 +179,16 @@ static void launch_flat(const T *in, T *out, uint8_t *counts, const InjectArgs &
   if (vec_ok) {
     unsigned g = grid_for((a.n + 3) / 4, kBlock, 16);
     if (counts && stats)
-      hipLaunchKernelGGL((inject_kernel<T, NB, true, true>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
+      KVECC_LAUNCH((inject_kernel<T, NB, true, true>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
     else if (counts)
-      hipLaunchKernelGGL((inject_kernel<T, NB, true, false>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
+      KVECC_LAUNCH((inject_kernel<T, NB, true, false>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
     else if (stats)
-      hipLaunchKernelGGL((inject_kernel<T, NB, false, true>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
+      KVECC_LAUNCH((inject_kernel<T, NB, false, true>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
     else
-      hipLaunchKernelGGL((inject_kernel<T, NB, false, false>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
+      KVECC_LAUNCH((inject_kernel<T, NB, false, false>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
   } else {
     unsigned g = grid_for(a.n, kBlock, 16);
-    hipLaunchKernelGGL((inject_scalar_kernel<T, NB>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
+    KVECC_LAUNCH((inject_scalar_kernel<T, NB>), dim3(g), dim3(kBlock), 0, st, in, out, counts, a, stats);
   }
 }
 
@@ -253,11 +253,11 @@ static int inject_rows(const T *in, T *out, int64_t rows, int64_t row_len, int n
   hipStream_t st = as_stream(stream);
   unsigned g = grid_for(rows * row_len, kBlock, 16);
   switch (sizeof(T) == 1 ? a.nb_eff : (a.nb_eff == 24 ? 24 : -1)) {
-    case 4: hipLaunchKernelGGL((inject_rows_kernel<T, 4>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
-    case 7: hipLaunchKernelGGL((inject_rows_kernel<T, 7>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
-    case 8: hipLaunchKernelGGL((inject_rows_kernel<T, 8>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
-    case 24: hipLaunchKernelGGL((inject_rows_kernel<T, 24>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
-    default: hipLaunchKernelGGL((inject_rows_kernel<T, -1>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
+    case 4: KVECC_LAUNCH((inject_rows_kernel<T, 4>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
+    case 7: KVECC_LAUNCH((inject_rows_kernel<T, 7>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
+    case 8: KVECC_LAUNCH((inject_rows_kernel<T, 8>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
+    case 24: KVECC_LAUNCH((inject_rows_kernel<T, 24>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
+    default: KVECC_LAUNCH((inject_rows_kernel<T, -1>), dim3(g), dim3(kBlock), 0, st, in, out, a, stats); break;
   }
   return check_launch(name);
 }
@@ -271,7 +271,7 @@ static int inject_vec(const T *in, T *out, uint8_t *counts, int64_t n, int n_bit
   int nb = sizeof(T) == 1 ? (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits))
                           : (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits));
   unsigned g = grid_for(n, kBlock, 16);
-  hipLaunchKernelGGL(inject_vec_kernel<T>, dim3(g), dim3(kBlock), 0, as_stream(stream), in, out,
+  KVECC_LAUNCH(inject_vec_kernel<T>, dim3(g), dim3(kBlock), 0, as_stream(stream), in, out,
                      counts, n, mul_wrap(seed, n), (uint32_t)n, kvecc_ber_threshold(ber), nb, stats);
   return check_launch(name);
 }

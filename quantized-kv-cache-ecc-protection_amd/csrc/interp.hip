@@ -160,11 +160,11 @@ KVECC_API int kvecc_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *o
   if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
     const int64_t chunks = inner / 16;
     const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
-    hipLaunchKernelGGL(interp_vec_kernel, dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0, st,
+    KVECC_LAUNCH(interp_vec_kernel, dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0, st,
                        reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
                        reinterpret_cast<u32x4 *>(out), outer, len, chunks, gate);
   } else {
-    hipLaunchKernelGGL(interp_scalar_kernel, dim3(grid_for(total, kBlock)), dim3(kBlock), 0, st, q,
+    KVECC_LAUNCH(interp_scalar_kernel, dim3(grid_for(total, kBlock)), dim3(kBlock), 0, st, q,
                        err, out, outer, len, inner, gate);
   }
   return check_launch("interpolate");
@@ -179,7 +179,7 @@ KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int
   if (e != hipSuccess) return set_error(KVECC_EHIP, "any_equal_u8: %s", hipGetErrorString(e));
   if (n == 0) return KVECC_OK;
   if (!x) return set_error(KVECC_EINVAL, "any_equal_u8: null input");
-  hipLaunchKernelGGL(any_equal_kernel, dim3(grid_for(n, (int64_t)kBlock * 64, 8)), dim3(kBlock), 0,
+  KVECC_LAUNCH(any_equal_kernel, dim3(grid_for(n, (int64_t)kBlock * 64, 8)), dim3(kBlock), 0,
                      st, x, n, (uint32_t)value, flag);
   return check_launch("any_equal_u8");
 }

@@ -3,6 +3,7 @@
 
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,6 +35,26 @@ void build_golay_parity_table(uint16_t *out4096);
 void build_golay_correct_table(uint16_t *out4096);
 
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- launch timing (kvecc_time_next_launch) -----------------------------------
+// When armed, the next kernel launched by this thread carries the events in its
+// own dispatch (hipExtLaunchKernel): start/end stamps with no marker packets
+// between kernels.  Every launch site goes through KVECC_LAUNCH.
+struct LaunchTiming {
+  hipEvent_t start, stop;
+};
+extern thread_local LaunchTiming g_launch_timing;
+
+#define KVECC_LAUNCH(KERNEL, GRID, BLOCK, SHMEM, STREAM, ...)                                 \
+  do {                                                                                        \
+    if (::kvecc::g_launch_timing.start || ::kvecc::g_launch_timing.stop) {                    \
+      const ::kvecc::LaunchTiming t_ = ::kvecc::g_launch_timing;                              \
+      ::kvecc::g_launch_timing = {nullptr, nullptr};                                          \
+      hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, SHMEM, STREAM, t_.start, t_.stop, 0u, __VA_ARGS__); \
+    } else {                                                                                  \
+      hipLaunchKernelGGL(KERNEL, GRID, BLOCK, SHMEM, STREAM, __VA_ARGS__);                    \
+    }                                                                                         \
+  } while (0)
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 

@@ -326,13 +326,13 @@ KVECC_API int kvecc_golay_encode_packed(const uint8_t *nibbles, uint8_t *codewor
   if (aligned(nibbles, 4) && aligned(codewords, 4)) {
     const int64_t ntiles = m / kPkTile;
     if (ntiles > 0)
-      hipLaunchKernelGGL(golay_encode_packed_kernel, dim3(grid_for(ntiles, 1, 16)), dim3(kPkBlock), 0,
+      KVECC_LAUNCH(golay_encode_packed_kernel, dim3(grid_for(ntiles, 1, 16)), dim3(kPkBlock), 0,
                          st, reinterpret_cast<const uint32_t *>(nibbles),
                          reinterpret_cast<uint32_t *>(codewords), ntiles, par);
     done = ntiles * kPkTile;
   }
   if (done < m)
-    hipLaunchKernelGGL(golay_encode_packed_tail_kernel, dim3((unsigned)cdiv(m - done, kBlock)),
+    KVECC_LAUNCH(golay_encode_packed_tail_kernel, dim3((unsigned)cdiv(m - done, kBlock)),
                        dim3(kBlock), 0, st, nibbles, codewords, done, m, par);
   return check_launch("golay_encode_packed");
 }
@@ -354,26 +354,26 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
       const uint32_t *c = reinterpret_cast<const uint32_t *>(codewords);
       uint32_t *n = reinterpret_cast<uint32_t *>(nibbles);
       if (uncorrectable && stats)
-        hipLaunchKernelGGL((golay_decode_packed_kernel<true, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_packed_kernel<true, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
       else if (uncorrectable)
-        hipLaunchKernelGGL((golay_decode_packed_kernel<true, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_packed_kernel<true, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
       else if (stats)
-        hipLaunchKernelGGL((golay_decode_packed_kernel<false, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_packed_kernel<false, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
       else
-        hipLaunchKernelGGL((golay_decode_packed_kernel<false, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_packed_kernel<false, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
     }
     done = ntiles * kPkTile;
   }
   if (done < m) {
     const dim3 grid(grid_for(cdiv(m - done, 8), kBlock)), block(kBlock);
     if (uncorrectable && stats)
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, true>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      KVECC_LAUNCH((golay_decode_packed_tail_kernel<true, true>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
     else if (uncorrectable)
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<true, false>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      KVECC_LAUNCH((golay_decode_packed_tail_kernel<true, false>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
     else if (stats)
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, true>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      KVECC_LAUNCH((golay_decode_packed_tail_kernel<false, true>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
     else
-      hipLaunchKernelGGL((golay_decode_packed_tail_kernel<false, false>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
+      KVECC_LAUNCH((golay_decode_packed_tail_kernel<false, false>), grid, block, 0, st, codewords, nibbles, uncorrectable, done, m, par, cor, stats);
   }
   return check_launch("golay_decode_packed");
 }
@@ -388,13 +388,13 @@ KVECC_API int kvecc_hamming84_encode_packed(const uint8_t *nibbles, uint8_t *cod
   if (aligned(nibbles, 8) && aligned(codewords, 16)) {
     const int64_t n16 = n / 16;
     if (n16 > 0)
-      hipLaunchKernelGGL(h84_encode_packed_kernel, dim3(grid_for(n16, kHpBlock, 32)), dim3(kHpBlock),
+      KVECC_LAUNCH(h84_encode_packed_kernel, dim3(grid_for(n16, kHpBlock, 32)), dim3(kHpBlock),
                          0, st, reinterpret_cast<const u32x2 *>(nibbles),
                          reinterpret_cast<u32x4 *>(codewords), n16);
     done = n16 * 16;
   }
   if (done < n)
-    hipLaunchKernelGGL(h84_encode_packed_tail_kernel, dim3(grid_for(n - done, kBlock)), dim3(kBlock),
+    KVECC_LAUNCH(h84_encode_packed_tail_kernel, dim3(grid_for(n - done, kBlock)), dim3(kBlock),
                        0, st, nibbles, codewords, done, n);
   return check_launch("hamming84_encode_packed");
 }
@@ -415,18 +415,18 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
       u32x2 *o = reinterpret_cast<u32x2 *>(nibbles);
       uint32_t *t = reinterpret_cast<uint32_t *>(error_types);
       if (error_types && stats)
-        hipLaunchKernelGGL((h84_decode_packed_kernel<true, true>), grid, block, 0, st, c, o, t, n16, stats);
+        KVECC_LAUNCH((h84_decode_packed_kernel<true, true>), grid, block, 0, st, c, o, t, n16, stats);
       else if (error_types)
-        hipLaunchKernelGGL((h84_decode_packed_kernel<true, false>), grid, block, 0, st, c, o, t, n16, stats);
+        KVECC_LAUNCH((h84_decode_packed_kernel<true, false>), grid, block, 0, st, c, o, t, n16, stats);
       else if (stats)
-        hipLaunchKernelGGL((h84_decode_packed_kernel<false, true>), grid, block, 0, st, c, o, t, n16, stats);
+        KVECC_LAUNCH((h84_decode_packed_kernel<false, true>), grid, block, 0, st, c, o, t, n16, stats);
       else
-        hipLaunchKernelGGL((h84_decode_packed_kernel<false, false>), grid, block, 0, st, c, o, t, n16, stats);
+        KVECC_LAUNCH((h84_decode_packed_kernel<false, false>), grid, block, 0, st, c, o, t, n16, stats);
     }
     done = n16 * 16;
   }
   if (done < n)
-    hipLaunchKernelGGL(h84_decode_packed_tail_kernel, dim3(grid_for(cdiv(n - done, 4), kBlock)),
+    KVECC_LAUNCH(h84_decode_packed_tail_kernel, dim3(grid_for(cdiv(n - done, 4), kBlock)),
                        dim3(kBlock), 0, st, codewords, nibbles, error_types, done, n, stats);
   return check_launch("hamming84_decode_packed");
 }

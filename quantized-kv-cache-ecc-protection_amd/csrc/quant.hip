@@ -256,7 +256,7 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
     const unsigned grid = grid_for(cdiv(rows, kWave / lpr), kBlock / kWave, 16);
 #define KVECC_QE1C(L)                                                                         \
   case L:                                                                                     \
-    hipLaunchKernelGGL((quantize_encode_1c_kernel<T, V, L>), dim3(grid), dim3(kBlock), 0, st, xt, \
+    KVECC_LAUNCH((quantize_encode_1c_kernel<T, V, L>), dim3(grid), dim3(kBlock), 0, st, xt, \
                        codec, rule, cw, scales, rows, d);                                     \
     break;
     switch (lpr) {
@@ -267,12 +267,12 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
   } else if (vec) {
     int lpr = lanes_per_row(d / V);
     int64_t waves = cdiv(rows, kWave / lpr);
-    hipLaunchKernelGGL((quantize_encode_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave)),
+    KVECC_LAUNCH((quantize_encode_kernel<T, V>), dim3(grid_for(waves, kBlock / kWave)),
                        dim3(kBlock), 0, st, xt, codec, rule, cw, scales, rows, d, lpr);
   } else {
     int lpr = lanes_per_row(d);
     int64_t waves = cdiv(rows, kWave / lpr);
-    hipLaunchKernelGGL((quantize_encode_kernel<T, 1>), dim3(grid_for(waves, kBlock / kWave)),
+    KVECC_LAUNCH((quantize_encode_kernel<T, 1>), dim3(grid_for(waves, kBlock / kWave)),
                        dim3(kBlock), 0, st, xt, codec, rule, cw, scales, rows, d, lpr);
   }
 }
@@ -286,16 +286,16 @@ static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t
     const uint32_t total = (uint32_t)(rows * (d / kCw));
     const uint32_t nchunk = (uint32_t)(d / kCw);
     const int shift = (nchunk & (nchunk - 1)) == 0 ? __builtin_ctz(nchunk) : -1;
-    hipLaunchKernelGGL((decode_dequant_wide_kernel<TO>), dim3(grid_for(total, kBlock * 4, 16)),
+    KVECC_LAUNCH((decode_dequant_wide_kernel<TO>), dim3(grid_for(total, kBlock * 4, 16)),
                        dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o,
                        nchunk, shift, total, zero_doubles, stats);
   } else if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
     int64_t total = rows * (d / 4);
-    hipLaunchKernelGGL((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),
+    KVECC_LAUNCH((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),
                        0, st, cw, scales, o, rows, d, zero_doubles, stats);
   } else {
     int64_t total = rows * d;
-    hipLaunchKernelGGL((decode_dequant_kernel<TO, 1>), dim3(grid_for(total, kBlock)), dim3(kBlock),
+    KVECC_LAUNCH((decode_dequant_kernel<TO, 1>), dim3(grid_for(total, kBlock)), dim3(kBlock),
                        0, st, cw, scales, o, rows, d, zero_doubles, stats);
   }
 }

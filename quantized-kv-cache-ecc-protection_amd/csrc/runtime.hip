@@ -14,6 +14,7 @@
 namespace kvecc {
 
 static thread_local char g_err[512] = "";
+thread_local LaunchTiming g_launch_timing = {nullptr, nullptr};
 
 int set_error(int code, const char *fmt, ...) {
   va_list ap;
@@ -151,6 +152,12 @@ extern "C" {
 KVECC_API const char *kvecc_version(void) { return "kvecc 0.1.0 (gfx950)"; }
 
 KVECC_API const char *kvecc_last_error(void) { return g_err; }
+
+KVECC_API int kvecc_time_next_launch(void *start_event, void *stop_event) {
+  g_launch_timing = {reinterpret_cast<hipEvent_t>(start_event),
+                     reinterpret_cast<hipEvent_t>(stop_event)};
+  return KVECC_OK;
+}
 
 KVECC_API int kvecc_device_count(void) {
   int n = 0;

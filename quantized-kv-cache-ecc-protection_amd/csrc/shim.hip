@@ -211,9 +211,9 @@ static void launch_write_nb(const ShimWriteArgs &a, unsigned grid, hipStream_t s
                      : CODEC == KVECC_CODEC_H74 ? 7
                                                 : 4;
   if (a.nb_eff == NB)
-    hipLaunchKernelGGL((shim_write_kernel<T, CODEC, NB>), dim3(grid), dim3(kBlock), 0, st, a);
+    KVECC_LAUNCH((shim_write_kernel<T, CODEC, NB>), dim3(grid), dim3(kBlock), 0, st, a);
   else
-    hipLaunchKernelGGL((shim_write_kernel<T, CODEC, -1>), dim3(grid), dim3(kBlock), 0, st, a);
+    KVECC_LAUNCH((shim_write_kernel<T, CODEC, -1>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
 template <typename T>
@@ -229,9 +229,9 @@ static void launch_write(int codec, const ShimWriteArgs &a, unsigned grid, hipSt
 template <typename TO, int CODEC, bool INTERP>
 static void launch_read_bytes(const ShimReadArgs &a, unsigned grid, hipStream_t st) {
   if (a.stats)
-    hipLaunchKernelGGL((shim_read_bytes_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_bytes_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kBlock), 0, st, a);
   else
-    hipLaunchKernelGGL((shim_read_bytes_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_bytes_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
 template <typename TO>
@@ -239,9 +239,9 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
   if (codec == KVECC_CODEC_GOLAY) {
     const unsigned grid = grid_for(2 * a.geo.hkv * a.ctx * a.geo.g, kBlock);
     if (a.stats)
-      hipLaunchKernelGGL((shim_read_golay_kernel<TO, true>), dim3(grid), dim3(kBlock), 0, st, a);
+      KVECC_LAUNCH((shim_read_golay_kernel<TO, true>), dim3(grid), dim3(kBlock), 0, st, a);
     else
-      hipLaunchKernelGGL((shim_read_golay_kernel<TO, false>), dim3(grid), dim3(kBlock), 0, st, a);
+      KVECC_LAUNCH((shim_read_golay_kernel<TO, false>), dim3(grid), dim3(kBlock), 0, st, a);
     return;
   }
   const unsigned grid = grid_for(2 * a.geo.hkv * a.ctx * (a.geo.d / 4), kBlock);

@@ -25,6 +25,7 @@ SIGNATURES = {
     "kvecc_version": [],
     "kvecc_last_error": [],
     "kvecc_device_count": [],
+    "kvecc_time_next_launch": [_vp, _vp],
     "kvecc_init_device": [_int],
     "kvecc_golay_syndrome_table_host": [_vp],
     "kvecc_golay_h_row_masks_host": [_vp],

@@ -70,6 +70,22 @@ def read_stats(stats, n=2):
     return [int(v) for v in stats_totals(stats, n).tolist()]
 
 
+def kernel_timer(device=None):
+    """A (start, stop) pair of timing events whose handles exist, for time_next_launch."""
+    evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for e in evs:
+        e.record(torch.cuda.current_stream(device))  # creates the underlying hipEvent_t
+    return evs
+
+
+def time_next_launch(start, stop):
+    """Arm kvecc_time_next_launch: the next kvecc kernel launched from this thread
+    stamps its own start / end into the torch.cuda.Event pair (kernel_timer());
+    read them with start.elapsed_time(stop) after a sync.  No marker packets."""
+    _lib.call("kvecc_time_next_launch", ctypes.c_void_p(start.cuda_event),
+              ctypes.c_void_p(stop.cuda_event))
+
+
 def _flat(t, dtype):
     f = t.reshape(-1)
     if f.dtype != dtype:

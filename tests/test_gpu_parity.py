@@ -454,3 +454,21 @@ def test_hamming84_packed_vs_cpu_backend(gpu, n, offset):
     pn, pt, st = ops.hamming84_decode_packed(buf.to(gpu)[offset:], return_error_types=True)
     assert st == st_ref
     assert torch.equal(pn.cpu(), pn_ref) and torch.equal(pt.cpu(), pt_ref)
+
+
+def test_time_next_launch_stamps_one_kernel(gpu):
+    """kvecc_time_next_launch: the next launch carries the events (its own start
+    and end), the hook then disarms, and results are unchanged."""
+    from kvecc import ops
+    x = torch.randint(0, 16, (1 << 24,), dtype=torch.uint8, device=gpu)
+    ref = ops.hamming84_encode(x)
+    out = torch.empty_like(x)
+    start, stop = ops.kernel_timer(gpu)
+    ops.time_next_launch(start, stop)
+    ops.hamming84_encode_into(x, out)
+    torch.cuda.synchronize()
+    t1 = start.elapsed_time(stop)
+    assert torch.equal(out, ref) and 0.0 < t1 < 50.0
+    ops.hamming84_encode_into(x, out)  # disarmed: the events keep their stamps
+    torch.cuda.synchronize()
+    assert start.elapsed_time(stop) == t1
