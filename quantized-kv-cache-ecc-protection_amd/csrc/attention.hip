@@ -51,6 +51,9 @@ struct AttnArgs {
 template <int CODEC, int VEC>
 struct Chunk {
   static constexpr int E = CODEC == KVECC_CODEC_H84 ? 4 * VEC : 3 * VEC;
+  // decode() returns (n - 8) + kOffset: the Golay path skips the subtraction
+  // per element and the kernel folds -8 * kOffset into the sums instead
+  static constexpr float kOffset = CODEC == KVECC_CODEC_GOLAY ? 8.0f : 0.0f;
   uint32_t w[VEC];
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
     if (CODEC == KVECC_CODEC_H84) {
@@ -87,11 +90,35 @@ struct Chunk {
         uint32_t cnt;
         const uint32_t dw = golay_decode1(w[k], gtab, gtab + 4096, cnt);
 #pragma unroll
-        for (int e = 0; e < 3; ++e) v[3 * k + e] = (float)(dw >> (4 * e) & 0xFu) - 8.0f;
+        for (int e = 0; e < 3; ++e) v[3 * k + e] = (float)__builtin_amdgcn_ubfe(dw, 4 * e, 4);  // n, see kOffset
       }
     }
   }
 };
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// sum_e q[e] * v[e] as packed FMAs (v_pk_fma_f32) into two independent lanes
+template <int E>
+__device__ __forceinline__ float dot(const float *q, const float *v) {
+  f32x2 s = {0.0f, 0.0f};
+#pragma unroll
+  for (int e = 0; e + 1 < E; e += 2) s = __builtin_elementwise_fma(f32x2{q[e], q[e + 1]}, f32x2{v[e], v[e + 1]}, s);
+  if (E % 2) s.x = fmaf(q[E - 1], v[E - 1], s.x);
+  return s.x + s.y;
+}
+
+// acc[e] += p * v[e] as packed FMAs
+template <int E>
+__device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
+#pragma unroll
+  for (int e = 0; e + 1 < E; e += 2) {
+    const f32x2 r = __builtin_elementwise_fma(f32x2{p, p}, f32x2{v[e], v[e + 1]}, f32x2{acc[e], acc[e + 1]});
+    acc[e] = r.x;
+    acc[e + 1] = r.y;
+  }
+  if (E % 2) acc[E - 1] = fmaf(p, v[E - 1], acc[E - 1]);
+}
 
 template <typename T, int CODEC, int VEC, int W>
 __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
@@ -157,17 +184,20 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
     lut[threadIdx.x] = (float)(q & 0xFu) - 8.0f;
   }
   float qv[E];
+  float qsum = 0.0f;  // sum of this lane's q (folds the decode's kOffset out of the K sums)
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int64_t di = (int64_t)c * E + e;
     qv[e] = (live && di < a.d)
                 ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h) * a.d + di]) * a.sm_scale
                 : 0.0f;
+    qsum += qv[e];
   }
   __syncthreads();
 
   // ---- one pass: kUnroll K and V rows in flight per lane, online softmax per group
   float m = -INFINITY, l = 0.0f, acc[E];
+  float psum = 0.0f;  // sum of p * v_scale, for the kOffset fold of the V sums
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = 0.0f;
   for (int i0 = grp; i0 < ntok; i0 += TP * kUnroll) {
@@ -192,18 +222,18 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       if (live) {
         float kv[E];
         kc[u].decode(lut, gtab, kv);
-#pragma unroll
-        for (int e = 0; e < E; ++e) part += qv[e] * kv[e];
+        part = dot<E>(qv, kv);
+        if (C::kOffset != 0.0f) part -= C::kOffset * qsum;
         part *= ks[u];  // sum q (n - 8) s = s * sum q (n - 8)
       }
-#pragma unroll
-      for (int off = W / 2; off > 0; off >>= 1) part += __shfl_xor(part, off, W);
+      part = group_sum<W>(part);
       sc[u] = ok[u] ? part : -INFINITY;
       mn = fmaxf(mn, sc[u]);
     }
     if (mn == -INFINITY) continue;  // no valid row yet (uniform per group)
     const float alpha = expf(m - mn);  // m = -inf -> 0
     l *= alpha;
+    psum *= alpha;
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] *= alpha;
 #pragma unroll
@@ -214,8 +244,8 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
         float vv[E];
         vc[u].decode(lut, gtab, vv);
         const float ps = p * vs[u];
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] += ps * vv[e];
+        psum += ps;
+        axpy<E>(acc, ps, vv);
       }
     }
     m = mn;
@@ -224,7 +254,8 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   // ---- merge the TP groups ------------------------------------------------------
   if (live) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) red[(grp * W + c) * E + e] = acc[e];
+    for (int e = 0; e < E; ++e)
+      red[(grp * W + c) * E + e] = C::kOffset != 0.0f ? acc[e] - C::kOffset * psum : acc[e];
   }
   if (c == 0) {
     gml[0][grp] = m;

@@ -120,6 +120,20 @@ __device__ __forceinline__ float group_max_nonneg(float v) {
   return __uint_as_float(u);
 }
 
+// sum over each aligned group of G lanes (G a power of two <= 64), the same
+// bits in every lane of the group (each step adds two equal partial sums in
+// either order); DPP inside a row, ds_bpermute across rows
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+  if (G >= 2) v += __uint_as_float(dpp_u32<0xB1>(__float_as_uint(v)));    // lane ^ 1
+  if (G >= 4) v += __uint_as_float(dpp_u32<0x4E>(__float_as_uint(v)));    // lane ^ 2
+  if (G >= 8) v += __uint_as_float(dpp_u32<0x141>(__float_as_uint(v)));   // row_half_mirror
+  if (G >= 16) v += __uint_as_float(dpp_u32<0x140>(__float_as_uint(v)));  // row_mirror
+  if (G >= 32) v += __shfl_xor(v, 16, kWave);
+  if (G >= 64) v += __shfl_xor(v, 32, kWave);
+  return v;
+}
+
 // wave-wide sum (all 64 lanes participate)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
