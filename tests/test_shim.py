@@ -178,3 +178,35 @@ def test_fused_equals_composed_cpu_backend():
 @pytest.mark.gpu
 def test_fused_equals_composed(gpu):
     _fused_equals_composed(gpu, "hip")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rule", ["div7", "mul_inv7"])
+def test_hip_and_cpu_backends_write_identical_caches(gpu, rule):
+    """Under either scale rule the two backends write the same cache bytes and
+    scales and read back the same dequantized K/V and statistics (fp16, fp32
+    and bf16 models; every fused codec; injection on)."""
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    cases = [("hamming84", True, 64, torch.float16), ("hamming74", False, 128, torch.float32),
+             ("golay", False, 128, torch.bfloat16), ("golay", False, 100, torch.float16),
+             ("int4", False, 64, torch.float32)]
+    for codec, interp, d, dt in cases:
+        b, s, hk = 2, 29, 3
+        g = torch.Generator().manual_seed(d)
+        k = (torch.randn(b, s, hk * d, generator=g) * 2).to(dt)
+        v = (torch.randn(b, s, hk * d, generator=g) * 2).to(dt)
+        res = []
+        for backend, dev in (("hip", gpu), ("cpu", torch.device("cpu"))):
+            cfg = ECCShimConfig(codec=codec, ber=0.02, inject_errors=True, seed=5,
+                                use_interpolation=interp, backend=backend, scale_rule=rule)
+            mgr = SimpleBlockManager(4, 16, 2, hk, d, device=dev, codec=codec)
+            be = ECCBackend(mgr, cfg, num_heads=hk)
+            be.write(k.to(dev), v.to(dev), layer_idx=1)
+            k_t, v_t = be.codec_backend.shim_read(mgr, 1, s, codec, interp, torch.float32, be._stats)
+            res.append((mgr.k_cache.cpu(), mgr.v_cache.cpu(), mgr.k_scales.cpu(),
+                        mgr.v_scales.cpu(), k_t.cpu(), v_t.cpu(),
+                        be.codec_backend.read_stats(be._stats, 2)))
+        hip, cpu = res
+        for i in range(6):
+            assert torch.equal(hip[i], cpu[i]), (codec, rule, i)
+        assert hip[6] == cpu[6], (codec, rule)
