@@ -31,6 +31,15 @@ KV_HD uint32_t byte_parity4(uint32_t y) {
   return y & 0x01010101u;
 }
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); gfx9 has no v_xor3
+KV_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 // ---- Hamming(7,4) / Hamming(8,4), four codewords per word (SWAR) -------------
 
 // v_perm_b32 for selectors 0..7: byte i = byte sel.byte[i] of (hi:lo)
@@ -303,8 +312,8 @@ KV_HD void philox_rounds(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
   for (int r = 0; r < 10; ++r) {
     uint32_t hb = mulhi32(kPhiloxB, c2), lb = kPhiloxB * c2;
     uint32_t ha = mulhi32(kPhiloxA, c0), la = kPhiloxA * c0;
-    c0 = hb ^ c1 ^ k0;
-    c2 = ha ^ c3 ^ k1;
+    c0 = xor3(hb, c1, k0);
+    c2 = xor3(ha, c3, k1);
     c1 = lb;
     c3 = la;
     k0 += kKeyA;
@@ -314,10 +323,14 @@ KV_HD void philox_rounds(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
 
 // tl.rand(key, ctr): first Philox output word for counter (ctr,0,0,0), key
 // sign-extended to 64 bits (random.py:46-110)
-KV_HD uint32_t philox_word0(uint32_t ctr, uint32_t key) {
+KV_HD uint32_t philox_word0_k(uint32_t ctr, uint32_t k0, uint32_t k1) {
   uint32_t c0 = ctr, c1 = 0, c2 = 0, c3 = 0;
-  philox_rounds(c0, c1, c2, c3, key, (uint32_t)((int32_t)key >> 31));
+  philox_rounds(c0, c1, c2, c3, k0, k1);
   return c0;
+}
+
+KV_HD uint32_t philox_word0(uint32_t ctr, uint32_t key) {
+  return philox_word0_k(ctr, key, (uint32_t)((int32_t)key >> 31));
 }
 
 // `uint_to_uniform_float(x) < ber` as an integer test against kvecc_ber_threshold
@@ -326,16 +339,39 @@ KV_HD bool philox_below(uint32_t x, uint32_t thr) {
   return f < thr;
 }
 
-// flip mask of one element for the per-bit scheme; key_base = key of bit 0
+// The same test as one add and one compare: fold(x) < thr <=> x in [0, thr) or
+// x in [2^32 - thr, 2^32) <=> (x + thr) mod 2^32 < 2 thr, valid for thr < 2^31.
+// thr == 2^31 (ber >= ~1: every draw is below) is handled by the caller.
+KV_HD uint32_t philox_below2(uint32_t x, uint32_t thr, uint32_t thr2) {
+  return (uint32_t)(x + thr < thr2);
+}
+
+// flip mask of one element for the per-bit scheme; key_base = key of bit 0.
+// The bits' keys are consecutive, so their sign-extension words k1 agree unless
+// the run crosses 2^31 or 2^32; then k1 and its round offsets are shared
+// across the bits (one add per round per element instead of per bit).
 template <int NB>
 KV_HD uint32_t philox_flip_mask(uint32_t key_base, uint32_t ctr, uint32_t thr, int nb_rt) {
+  const int nb = NB >= 0 ? NB : nb_rt;
+  if (nb <= 0) return 0;
+  if (thr > 0x7FFFFFFFu) return nb >= 32 ? ~0u : (1u << nb) - 1;
+  const uint32_t thr2 = 2 * thr;
+  const uint32_t k1 = (uint32_t)((int32_t)key_base >> 31);
+  const bool same_sign = k1 == (uint32_t)((int32_t)(key_base + (uint32_t)(nb - 1)) >> 31);
   uint32_t m = 0;
   if (NB >= 0) {
+    if (same_sign) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) m |= (uint32_t)philox_below(philox_word0(ctr, key_base + b), thr) << b;
+      for (int b = NB - 1; b >= 0; --b)
+        m = m << 1 | philox_below2(philox_word0_k(ctr, key_base + b, k1), thr, thr2);
+    } else {
+#pragma unroll
+      for (int b = NB - 1; b >= 0; --b)
+        m = m << 1 | philox_below2(philox_word0(ctr, key_base + b), thr, thr2);
+    }
   } else {
-    for (int b = 0; b < nb_rt; ++b)
-      m |= (uint32_t)philox_below(philox_word0(ctr, key_base + b), thr) << b;
+    for (int b = nb - 1; b >= 0; --b)
+      m = m << 1 | philox_below2(philox_word0(ctr, key_base + b), thr, thr2);
   }
   return m;
 }
