@@ -154,6 +154,18 @@ KVECC_API int kvecc_inject_rows_i32(const int32_t *in, int32_t *out, int64_t row
 KVECC_API int kvecc_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
                                 int64_t outer, int64_t len, int64_t inner, const int32_t *gate,
                                 void *stream);
+/* The reference wrapper in full (interpolation_triton.py:162-265) in one pass:
+ * out = the interpolated, clamped result when any err == 2, else out = q (its
+ * `q.clone()` fast path, :199-201).  No host sync, no separate scan of err and
+ * no zeroing pass: the kernel sets flags[0] = epoch if any err == 2 and
+ * flags[1] = epoch if any q > 15 (device int32[2]); a trailing copy kernel
+ * restores out = q only when flags[0] != epoch and flags[1] == epoch (without
+ * doubles, clamping is visible only where q > 15).  `epoch` must be non-zero
+ * and differ from both words of `flags` on entry (e.g. a per-buffer call
+ * counter); afterwards "flags[k] == epoch" reads as "condition k was seen". */
+KVECC_API int kvecc_interpolate_auto(const uint8_t *q, const uint8_t *err, uint8_t *out,
+                                     int64_t outer, int64_t len, int64_t inner, int32_t *flags,
+                                     int32_t epoch, void *stream);
 /* *flag = (any x[i] == value) ? 1 : 0 (device int32, overwritten). */
 KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int32_t *flag,
                                  void *stream);

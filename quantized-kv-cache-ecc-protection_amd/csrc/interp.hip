@@ -13,8 +13,12 @@
 // reference permutes + copies to make it the last axis).  When inner is a
 // multiple of 16 each lane owns a 16-byte column chunk and walks kRows
 // consecutive sequence positions, so every q row is loaded once per lane
-// (plus a one-row halo) with 16-byte loads.  A device-side gate implements the
-// reference's no-double fast path (:199-201) without a host sync.
+// (plus a one-row halo) with 16-byte loads.  The reference's no-double fast
+// path (:199-201: return q.clone() when no err == 2) is resolved without a host
+// sync and without a separate scan of err: kvecc_interpolate_auto writes the
+// interpolated (clamped) result in one pass while recording whether any double
+// and any q > 15 was seen; the two differ only when there is no double and some
+// q > 15, which a trailing copy kernel (a no-op otherwise) then handles.
 #include "kvecc_internal.h"
 
 namespace kvecc {
@@ -35,12 +39,26 @@ __device__ __forceinline__ u32x4 interp_vec(u32x4 q, u32x4 l, u32x4 r, u32x4 e) 
 // kRows + 2 q rows (with the one-row halo each side) and kRows err rows of the
 // item are loaded before any is used, non-temporally, so a lane keeps ~18
 // 16-byte loads in flight.
+// any byte of the word == 2 / > 15
+__device__ __forceinline__ uint32_t seen_double(u32x4 e) {
+  return is_double(e.x) | is_double(e.y) | is_double(e.z) | is_double(e.w);
+}
+__device__ __forceinline__ uint32_t seen_over15(u32x4 q) {
+  return (q.x | q.y | q.z | q.w) & 0xF0F0F0F0u;
+}
+
+// RECORD: no gate; flags[0] = epoch if any err == 2, flags[1] = epoch if any
+// q > 15 (one plain store per workgroup that saw one; no zeroing pass)
+template <bool RECORD>
 __global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restrict__ q,
                                                             const u32x4 *__restrict__ err,
                                                             u32x4 *__restrict__ out, int64_t outer,
                                                             int64_t len, int64_t chunks,
-                                                            const int32_t *__restrict__ gate) {
-  const bool pass = gate != nullptr && *gate == 0;
+                                                            const int32_t *__restrict__ gate,
+                                                            int32_t *__restrict__ flags,
+                                                            int32_t epoch) {
+  const bool pass = !RECORD && gate != nullptr && *gate == 0;
+  uint32_t dbl = 0, over = 0;
   const int64_t rblocks = (len + kRows - 1) / kRows;
   const int64_t items = outer * rblocks * chunks;
   for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < items;
@@ -62,9 +80,14 @@ __global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restr
         for (int k = 0; k < kRows; ++k) er[k] = ld_stream(err + base + (l0 + k) * chunks);
       }
 #pragma unroll
-      for (int k = 0; k < kRows; ++k)
+      for (int k = 0; k < kRows; ++k) {
         st_stream(out + base + (l0 + k) * chunks,
                   pass ? qr[k + 1] : interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
+        if (RECORD) {
+          dbl |= seen_double(er[k]);
+          over |= seen_over15(qr[k + 1]);
+        }
+      }
       continue;
     }
     const int nrow = (int)(len - l0);  // ragged last block
@@ -79,20 +102,35 @@ __global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restr
       u32x4 next = q[base + (l + 1 < len ? l + 1 : len - 1) * chunks];
       u32x4 e = err[base + l * chunks];
       out[base + l * chunks] = interp_vec(cur, prev, next, e);
+      if (RECORD) {
+        dbl |= seen_double(e);
+        over |= seen_over15(cur);
+      }
       prev = cur;
       cur = next;
+    }
+  }
+  if (RECORD) {
+    const bool d = __syncthreads_or(dbl != 0), o = __syncthreads_or(over != 0);
+    if (threadIdx.x == 0) {
+      if (d) flags[0] = epoch;
+      if (o) flags[1] = epoch;
     }
   }
 }
 
 // scalar path: one element per lane
+template <bool RECORD>
 __global__ __launch_bounds__(kBlock) void interp_scalar_kernel(const uint8_t *__restrict__ q,
                                                                const uint8_t *__restrict__ err,
                                                                uint8_t *__restrict__ out,
                                                                int64_t outer, int64_t len,
                                                                int64_t inner,
-                                                               const int32_t *__restrict__ gate) {
-  const bool pass = gate != nullptr && *gate == 0;
+                                                               const int32_t *__restrict__ gate,
+                                                               int32_t *__restrict__ flags,
+                                                               int32_t epoch) {
+  const bool pass = !RECORD && gate != nullptr && *gate == 0;
+  bool dbl = false, over = false;
   const int64_t total = outer * len * inner;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * kBlock) {
@@ -107,7 +145,38 @@ __global__ __launch_bounds__(kBlock) void interp_scalar_kernel(const uint8_t *__
     const uint32_t right = q[rowbase + (l + 1 < len ? l + 1 : len - 1) * inner];
     (void)c;
     out[i] = (uint8_t)interp_word(q[i], left, right, err[i]);
+    if (RECORD) {
+      dbl |= err[i] == 2;
+      over |= q[i] > 15;
+    }
   }
+  if (RECORD) {
+    const bool d = __syncthreads_or(dbl), o = __syncthreads_or(over);
+    if (threadIdx.x == 0) {
+      if (d) flags[0] = epoch;
+      if (o) flags[1] = epoch;
+    }
+  }
+}
+
+// after a RECORD pass: no double anywhere but some q > 15 -> out = q (the
+// reference returns an unclamped clone); otherwise every workgroup exits at
+// once.  A small grid: the copy is the rare branch, the exit is the common one.
+__global__ __launch_bounds__(kBlock) void interp_fixup_kernel(const uint8_t *__restrict__ q,
+                                                              uint8_t *__restrict__ out, int64_t n,
+                                                              const int32_t *__restrict__ flags,
+                                                              int32_t epoch, bool vec) {
+  if (flags[0] == epoch || flags[1] != epoch) return;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t tid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int64_t done = 0;
+  if (vec) {
+    const int64_t nv = n / 16;
+    for (int64_t i = tid; i < nv; i += stride)
+      reinterpret_cast<u32x4 *>(out)[i] = reinterpret_cast<const u32x4 *>(q)[i];
+    done = nv * 16;
+  }
+  for (int64_t i = done + tid; i < n; i += stride) out[i] = q[i];
 }
 
 __device__ __forceinline__ bool has_byte(u32x4 v, uint32_t pat) {
@@ -143,6 +212,22 @@ __global__ __launch_bounds__(kBlock) void any_equal_kernel(const uint8_t *__rest
   if (__syncthreads_or(hit) && threadIdx.x == 0) *flag = 1;
 }
 
+template <bool RECORD>
+static void launch_interp(const uint8_t *q, const uint8_t *err, uint8_t *out, int64_t outer,
+                          int64_t len, int64_t inner, const int32_t *gate, int32_t *flags,
+                          int32_t epoch, hipStream_t st) {
+  if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
+    const int64_t chunks = inner / 16;
+    const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
+    KVECC_LAUNCH((interp_vec_kernel<RECORD>), dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0,
+                 st, reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
+                 reinterpret_cast<u32x4 *>(out), outer, len, chunks, gate, flags, epoch);
+  } else {
+    KVECC_LAUNCH((interp_scalar_kernel<RECORD>), dim3(grid_for(outer * len * inner, kBlock)),
+                 dim3(kBlock), 0, st, q, err, out, outer, len, inner, gate, flags, epoch);
+  }
+}
+
 }  // namespace kvecc
 
 using namespace kvecc;
@@ -156,18 +241,25 @@ KVECC_API int kvecc_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *o
   const int64_t total = outer * len * inner;
   if (total == 0) return KVECC_OK;
   if (!q || !err || !out) return set_error(KVECC_EINVAL, "interpolate: null pointer");
-  hipStream_t st = as_stream(stream);
-  if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
-    const int64_t chunks = inner / 16;
-    const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
-    KVECC_LAUNCH(interp_vec_kernel, dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0, st,
-                       reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
-                       reinterpret_cast<u32x4 *>(out), outer, len, chunks, gate);
-  } else {
-    KVECC_LAUNCH(interp_scalar_kernel, dim3(grid_for(total, kBlock)), dim3(kBlock), 0, st, q,
-                       err, out, outer, len, inner, gate);
-  }
+  launch_interp<false>(q, err, out, outer, len, inner, gate, nullptr, 0, as_stream(stream));
   return check_launch("interpolate");
+}
+
+KVECC_API int kvecc_interpolate_auto(const uint8_t *q, const uint8_t *err, uint8_t *out,
+                                     int64_t outer, int64_t len, int64_t inner, int32_t *flags,
+                                     int32_t epoch, void *stream) {
+  if (outer < 0 || len < 0 || inner < 0)
+    return set_error(KVECC_EINVAL, "interpolate_auto: negative size");
+  if (!flags) return set_error(KVECC_EINVAL, "interpolate_auto: null flags");
+  if (epoch == 0) return set_error(KVECC_EINVAL, "interpolate_auto: epoch must be non-zero");
+  const int64_t total = outer * len * inner;
+  if (total == 0) return KVECC_OK;
+  if (!q || !err || !out) return set_error(KVECC_EINVAL, "interpolate_auto: null pointer");
+  hipStream_t st = as_stream(stream);
+  launch_interp<true>(q, err, out, outer, len, inner, nullptr, flags, epoch, st);
+  KVECC_LAUNCH(interp_fixup_kernel, dim3(64), dim3(kBlock), 0, st, q, out, total, flags, epoch,
+               aligned(q, 16) && aligned(out, 16));
+  return check_launch("interpolate_auto");
 }
 
 KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int32_t *flag,

@@ -20,6 +20,8 @@ from __future__ import annotations
 import ctypes
 import math
 
+import threading
+
 import torch
 
 from . import _lib
@@ -392,8 +394,10 @@ def interpolate_double_errors(q, error_type, original_shape=None, seq_dim=-1):
     """Replace DOUBLE_DETECTED values by the rounded mean of their sequence
     neighbours; interpolation_triton.py:162-265.
 
-    The no-double fast path (return q unchanged) is decided on the device: no
-    host sync unless q is not uint8 (its dtype would depend on the branch).
+    The no-double fast path (return q unchanged) is decided on the device: for
+    uint8 q one pass (kvecc_interpolate_auto) with no host sync and no separate
+    scan of error_type; other dtypes sync once (the result dtype depends on the
+    branch).
     """
     _check_gpu(q)
     _check_gpu(error_type, "Error type")
@@ -401,14 +405,51 @@ def interpolate_double_errors(q, error_type, original_shape=None, seq_dim=-1):
     if q.numel() == 0:
         return q.clone()
     err = _flat(error_type, torch.uint8)
+    outer, length, inner = _seq_layout(tuple(q.shape), seq_dim)
+    if q.dtype == torch.uint8:
+        qf = _flat(q, torch.uint8)
+        out = torch.empty_like(qf)
+        interpolate_auto_into(qf, err, out, outer, length, inner)
+        return out.view(q.shape)
     flag = any_equal(err, ErrorType.DOUBLE_DETECTED)
-    if q.dtype != torch.uint8 and int(flag.item()) == 0:
+    if int(flag.item()) == 0:
         return q.clone()
     qf = _flat(q, torch.uint8)
-    outer, length, inner = _seq_layout(tuple(q.shape), seq_dim)
     out = torch.empty_like(qf)
-    interpolate_into(qf, err, out, outer, length, inner, gate=flag if q.dtype == torch.uint8 else None)
+    interpolate_into(qf, err, out, outer, length, inner)
     return out.view(q.shape)
+
+
+class _EpochFlags:
+    """Per-(device, stream) int32[2] flag words for kvecc_interpolate_auto and
+    their call counter: each call stamps a fresh epoch, so the words never need
+    zeroing (a stream orders its calls, so reuse on one stream is safe)."""
+
+    def __init__(self):
+        self._bufs = {}
+        self._lock = threading.Lock()
+
+    def next(self, device):
+        key = (device, torch.cuda.current_stream(device).cuda_stream)
+        with self._lock:
+            buf, epoch = self._bufs.get(key, (None, 0))
+            if buf is None or epoch >= 0x7FFFFFFF:
+                buf, epoch = torch.zeros(2, dtype=torch.int32, device=device), 0
+            epoch += 1
+            self._bufs[key] = (buf, epoch)
+        return buf, epoch
+
+
+_EPOCH_FLAGS = _EpochFlags()
+
+
+def interpolate_auto_into(q, err, out, outer, length, inner):
+    """kvecc_interpolate_auto: interpolation and the no-double fast path in one
+    pass.  Returns (flags, epoch): flags[k] == epoch <=> (any err == 2, any q > 15)."""
+    flags, epoch = _EPOCH_FLAGS.next(q.device)
+    _lib.call("kvecc_interpolate_auto", _ptr(q), _ptr(err), _ptr(out), outer, length, inner,
+              _ptr(flags), epoch, _stream(q.device))
+    return flags, epoch
 
 
 def interpolate_double_errors_1d(q, error_type):

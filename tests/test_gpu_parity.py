@@ -294,6 +294,45 @@ def test_interp_vector_gate_pass(gpu):
     assert torch.equal(out.cpu(), q)
 
 
+@pytest.mark.parametrize("shape,seq_dim", [((64, 32, 128), 0), ((8, 40, 48), 1), ((999,), -1),
+                                           ((5, 33, 7), 1)])
+@pytest.mark.parametrize("case", ["none", "none_over15", "one_double_far", "double_and_over15"])
+def test_interp_auto_flags_and_fixup(gpu, oracle, shape, seq_dim, case):
+    """kvecc_interpolate_auto: one pass + the trailing copy give the reference's
+    result in every branch (vector and scalar layouts); flags = (any double, any q > 15)."""
+    from kvecc import ops
+    rng = np.random.default_rng(sum(shape))
+    q = rng.integers(0, 16, size=shape, dtype=np.int64).astype(np.uint8)
+    e = rng.choice(np.array([0, 1, 3], np.uint8), size=shape)
+    flat_q, flat_e = q.reshape(-1), e.reshape(-1)
+    if case in ("none_over15", "double_and_over15"):
+        flat_q[rng.integers(0, flat_q.size, 5)] = 200
+    if case in ("one_double_far", "double_and_over15"):
+        flat_e[flat_e.size - 1] = 2
+    qd, ed = _t(q, gpu), _t(e, gpu)
+    outer, length, inner = ops._seq_layout(shape, seq_dim)
+    out = torch.empty(q.size, dtype=torch.uint8, device=gpu)
+    flags, epoch = ops.interpolate_auto_into(qd.view(-1), ed.view(-1), out, outer, length, inner)
+    want_flags = [int((e == 2).any()), int((q > 15).any())]
+    assert (flags == epoch).int().tolist() == want_flags
+    assert np.array_equal(_np(out).reshape(shape), oracle.interpolate_double_errors(q, e, seq_dim=seq_dim))
+    if not want_flags[0]:
+        assert np.array_equal(_np(out).reshape(shape), q)
+
+
+def test_interp_auto_epochs_do_not_leak(gpu):
+    """Consecutive calls share the flag words: a double seen by one call must not
+    gate the next (each call stamps a fresh epoch instead of zeroing)."""
+    import kvecc
+    q = torch.full((64, 48), 200, dtype=torch.uint8, device=gpu)
+    e_dbl = torch.zeros_like(q)
+    e_dbl[5, 7] = 2
+    e_none = torch.zeros_like(q)
+    for _ in range(3):
+        assert int(kvecc.interpolate_double_errors(q, e_dbl, seq_dim=0).max()) == 15
+        assert torch.equal(kvecc.interpolate_double_errors(q, e_none, seq_dim=0), q)
+
+
 @pytest.mark.parametrize("n,offset", [(1, 0), (17, 3), ((1 << 20) + 5, 0), ((1 << 22) + 77, 1)])
 def test_any_equal(gpu, n, offset):
     from kvecc import ops

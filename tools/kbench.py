@@ -125,6 +125,9 @@ def main():
             "interp_vec_gated": lambda: ops.interpolate_into(q.view(-1), err.view(-1), out.view(-1),
                                                              outer, length, inner, gate=flag),
             "any_equal": lambda: ops.any_equal(err.view(-1), 2, flag),
+            "interp_auto": lambda: ops.interpolate_auto_into(q.view(-1), err.view(-1), out.view(-1),
+                                                             outer, length, inner),
+            "interpolate_double_errors": lambda: ops.interpolate_double_errors(q, err, seq_dim=1),
         }
         for k, fn in variants.items():
             med, mn = timed(fn, flush, args.rounds)
