@@ -230,6 +230,23 @@ KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_
                                float *k_scales, float *v_scales, const int32_t *block_table,
                                int64_t num_layers, int64_t block_size, int64_t layer,
                                void *stream);
+/* kvecc_shim_write on strided K/V: element (b, pos, h, e) of K lives at
+ * k[b*k_batch_stride + pos*k_seq_stride + h*k_head_stride + e] (same for V;
+ * each head's d values contiguous), so the projections' views are read in
+ * place -- a slice of GPT-2's fused c_attn output, or Llama's post-RoPE
+ * [b, h, s, d] tensor transposed -- where the reference first copies them
+ * with .transpose(1, 2).contiguous() (ecc_shim.py:1290-1291, :1351-1352).
+ * Strides are >= 0 and head strides >= d. */
+KVECC_API int kvecc_shim_write_strided(const void *k, const void *v, int64_t k_batch_stride,
+                                       int64_t k_seq_stride, int64_t k_head_stride,
+                                       int64_t v_batch_stride, int64_t v_seq_stride,
+                                       int64_t v_head_stride, int x_dtype, int64_t batch,
+                                       int64_t seq, int64_t hkv, int64_t d, int codec,
+                                       int scale_rule, int n_bits, int inject, float ber,
+                                       int64_t seed0, void *k_cache, void *v_cache,
+                                       float *k_scales, float *v_scales,
+                                       const int32_t *block_table, int64_t num_layers,
+                                       int64_t block_size, int64_t layer, void *stream);
 /* ecc_shim.py:990-1071 (ECCBackend.attend, decode side) in ONE launch: gather
  * the first ctx tokens of layer `layer`, decode (H74: stats[0] += #flagged;
  * H84: stats[0] += #SINGLE_CORRECTED, stats[1] += #DOUBLE_DETECTED; Golay:

@@ -41,7 +41,8 @@ struct ShimGeom {
 
 struct ShimWriteArgs {
   ShimGeom geo;
-  const void *x[2];  // K, V: [batch, seq, hkv * d], contiguous
+  const void *x[2];  // K, V: [batch, seq, hkv, d], each head's d values contiguous
+  int64_t xb[2], xs[2], xh[2];  // element strides of the batch, seq and head dims
   void *cache[2];
   float *scales[2];
   int64_t batch, seq;
@@ -69,7 +70,8 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
   float v[kPer];
   float amax = 0.0f;
   if (live) {
-    const T *x = reinterpret_cast<const T *>(a.x[side]) + r * geo.d;
+    const T *x = reinterpret_cast<const T *>(a.x[side]) + (a.batch - 1) * a.xb[side] +
+                 (int64_t)pos * a.xs[side] + (int64_t)h * a.xh[side];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const uint32_t e = lane + i * kWave;
@@ -263,12 +265,12 @@ using namespace kvecc;
 
 extern "C" {
 
-KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
-                               int64_t seq, int64_t hkv, int64_t d, int codec, int scale_rule,
-                               int n_bits, int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
-                               float *k_scales, float *v_scales, const int32_t *block_table,
-                               int64_t num_layers, int64_t block_size, int64_t layer,
-                               void *stream) {
+static int shim_write_impl(const void *k, const void *v, const int64_t xb[2], const int64_t xs[2],
+                           const int64_t xh[2], int x_dtype, int64_t batch, int64_t seq, int64_t hkv, int64_t d,
+                           int codec, int scale_rule, int n_bits, int inject, float ber,
+                           int64_t seed0, void *k_cache, void *v_cache, float *k_scales,
+                           float *v_scales, const int32_t *block_table, int64_t num_layers,
+                           int64_t block_size, int64_t layer, void *stream) {
   if (batch < 0 || seq < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_write: negative size");
   if (batch == 0 || seq == 0 || hkv == 0) return KVECC_OK;
   if (d < 1 || d > kMaxShimD) return set_error(KVECC_EINVAL, "shim_write: head_dim %lld not in [1, %d]", (long long)d, kMaxShimD);
@@ -282,12 +284,20 @@ KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_
     return set_error(KVECC_EINVAL, "shim_write: null pointer");
   if (2 * seq * hkv > 0x7FFFFFFFLL || num_layers * hkv * block_size > 0x7FFFFFFFLL)
     return set_error(KVECC_EINVAL, "shim_write: sizes exceed 32-bit indexing");
+  for (int s = 0; s < 2; ++s)
+    if (xb[s] < 0 || xs[s] < 0 || xh[s] < d)
+      return set_error(KVECC_EINVAL, "shim_write: negative stride or head stride < head_dim");
   ShimWriteArgs a;
   a.geo = {block_table, (uint32_t)hkv, (uint32_t)d,
            (uint32_t)(codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d), (uint32_t)num_layers,
            (uint32_t)block_size, (uint32_t)layer};
   a.x[0] = k;
   a.x[1] = v;
+  for (int s = 0; s < 2; ++s) {
+    a.xb[s] = xb[s];
+    a.xs[s] = xs[s];
+    a.xh[s] = xh[s];
+  }
   a.cache[0] = k_cache;
   a.cache[1] = v_cache;
   a.scales[0] = k_scales;
@@ -314,6 +324,35 @@ KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_
     default: return set_error(KVECC_EINVAL, "shim_write: bad dtype %d", x_dtype);
   }
   return check_launch("shim_write");
+}
+
+KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
+                               int64_t seq, int64_t hkv, int64_t d, int codec, int scale_rule,
+                               int n_bits, int inject, float ber, int64_t seed0, void *k_cache, void *v_cache,
+                               float *k_scales, float *v_scales, const int32_t *block_table,
+                               int64_t num_layers, int64_t block_size, int64_t layer,
+                               void *stream) {
+  const int64_t xh[2] = {d, d}, xs[2] = {hkv * d, hkv * d}, xb[2] = {seq * hkv * d, seq * hkv * d};
+  return shim_write_impl(k, v, xb, xs, xh, x_dtype, batch, seq, hkv, d, codec, scale_rule, n_bits,
+                         inject, ber, seed0, k_cache, v_cache, k_scales, v_scales, block_table,
+                         num_layers, block_size, layer, stream);
+}
+
+KVECC_API int kvecc_shim_write_strided(const void *k, const void *v, int64_t k_batch_stride,
+                                       int64_t k_seq_stride, int64_t k_head_stride,
+                                       int64_t v_batch_stride, int64_t v_seq_stride,
+                                       int64_t v_head_stride, int x_dtype, int64_t batch,
+                                       int64_t seq, int64_t hkv, int64_t d, int codec,
+                                       int scale_rule, int n_bits, int inject, float ber,
+                                       int64_t seed0, void *k_cache, void *v_cache,
+                                       float *k_scales, float *v_scales,
+                                       const int32_t *block_table, int64_t num_layers,
+                                       int64_t block_size, int64_t layer, void *stream) {
+  const int64_t xb[2] = {k_batch_stride, v_batch_stride}, xs[2] = {k_seq_stride, v_seq_stride};
+  const int64_t xh[2] = {k_head_stride, v_head_stride};
+  return shim_write_impl(k, v, xb, xs, xh, x_dtype, batch, seq, hkv, d, codec, scale_rule, n_bits,
+                         inject, ber, seed0, k_cache, v_cache, k_scales, v_scales, block_table,
+                         num_layers, block_size, layer, stream);
 }
 
 KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,

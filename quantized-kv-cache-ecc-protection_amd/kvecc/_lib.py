@@ -54,6 +54,7 @@ SIGNATURES = {
     "kvecc_hamming84_encode_packed": [_vp, _vp, _i64, _vp],
     "kvecc_hamming84_decode_packed": [_vp, _vp, _vp, _i64, _vp, _vp],
     "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    "kvecc_shim_write_strided": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
     "kvecc_paged_attention_workspace": [_i64, _i64, _i64, _i64],
     "kvecc_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,

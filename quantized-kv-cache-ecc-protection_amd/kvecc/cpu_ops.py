@@ -447,11 +447,11 @@ SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84"
 
 def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0,
                scale_rule=None):
-    batch, seq, _ = k.shape
+    batch, seq = k.shape[0], k.shape[1]
     if k.dtype not in _DT or v.dtype != k.dtype:
         raise TypeError(f"unsupported K/V dtype {k.dtype}/{v.dtype}")
     _check_cpu(k)
-    k, v = k.contiguous(), v.contiguous()
+    k, v = k.reshape(batch, seq, -1).contiguous(), v.reshape(batch, seq, -1).contiguous()
     table = manager.block_table[seq_id]
     _lib.call("kvecc_cpu_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq,
               manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec],

@@ -252,14 +252,14 @@ class ECCBackend:
                              _N_BITS[self.config.codec], seed_base)
 
     def write(self, k, v, layer_idx, seq_id=0):
-        """Store K, V [batch, seq, kv_heads*head_dim] for layer `layer_idx`."""
+        """Store K, V [batch, seq, kv_heads*head_dim] (or a [batch, seq, kv_heads,
+        head_dim] view, which the fused path reads in place) for layer `layer_idx`."""
         cfg, mgr = self.config, self.manager
-        batch, seq_len, _ = k.shape
+        batch, seq_len = k.shape[0], k.shape[1]
         d, hk = self.head_dim, self.num_kv_heads
         self._total_values += 2 * batch * seq_len * hk * d
         if mgr.get_context_len(seq_id) < seq_len:
             mgr.allocate(seq_id, seq_len)
-        blk, slot = mgr.slots(seq_id, seq_len)
         rows = batch * seq_len * hk
         inject = cfg.inject_errors and cfg.ber > 0
         seed0 = cfg.seed + self._injection_count
@@ -269,6 +269,7 @@ class ECCBackend:
             if inject:
                 self._injection_count += rows
             return
+        blk, slot = mgr.slots(seq_id, seq_len)
         kr = k.reshape(batch, seq_len, hk, d)
         vr = v.reshape(batch, seq_len, hk, d)
         codec = cfg.codec
@@ -479,8 +480,7 @@ class ECCPagedAttentionShim(nn.Module):
         q = q.view(b, s, self.num_heads, self.head_dim).transpose(1, 2)
         k = k.view(b, s, self.num_kv_heads, self.head_dim).transpose(1, 2)
         v = v.view(b, s, self.num_kv_heads, self.head_dim).transpose(1, 2)
-        self.backend.write(k.transpose(1, 2).contiguous().view(b, s, -1),
-                           v.transpose(1, 2).contiguous().view(b, s, -1), self.layer_idx, seq_id=0)
+        self._write(k, v, b, s)
         out = self.backend.attend(q, self.layer_idx, seq_id=0)
         out = self.c_proj(out.transpose(1, 2).contiguous().view(b, s, self.hidden_size))
         if hasattr(self, "resid_dropout"):
@@ -499,11 +499,21 @@ class ECCPagedAttentionShim(nn.Module):
             position_ids = torch.arange(s, device=hidden_states.device).unsqueeze(0).expand(b, -1)
         cos, sin = self.rotary_emb(v, position_ids)
         q, k = self._apply_rotary_pos_emb(q, k, cos, sin)
-        self.backend.write(k.transpose(1, 2).contiguous().view(b, s, -1),
-                           v.transpose(1, 2).contiguous().view(b, s, -1), self.layer_idx, seq_id=0)
+        self._write(k, v, b, s)
         out = self.backend.attend(q, self.layer_idx, seq_id=0)
         out = self.o_proj(out.transpose(1, 2).contiguous().view(b, s, self.hidden_size))
         return out, None
+
+    def _write(self, k, v, b, s):
+        """backend.write of K/V [b, heads, s, d].  The reference copies them to
+        [b, s, heads*d] first (ecc_shim.py:1290-1291, :1351-1352); the fused
+        write reads the [b, s, heads, d] views in place."""
+        if self.backend._fused_ok(k) and k.dtype == v.dtype:
+            self.backend.write(k.transpose(1, 2), v.transpose(1, 2), self.layer_idx, seq_id=0)
+        else:
+            self.backend.write(k.transpose(1, 2).contiguous().view(b, s, -1),
+                               v.transpose(1, 2).contiguous().view(b, s, -1), self.layer_idx,
+                               seq_id=0)
 
     def _apply_rotary_pos_emb(self, q, k, cos, sin):
         def rotate_half(x):

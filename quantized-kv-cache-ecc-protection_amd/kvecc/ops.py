@@ -556,18 +556,35 @@ SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84"
 def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0,
                scale_rule=None):
     """ECCBackend.write for one layer (ecc_shim.py:557-721): K, V [batch, seq,
-    hkv*d] -> quantize, encode, per-row inject, scatter into manager's caches."""
-    batch, seq, _ = k.shape
+    hkv*d] or [batch, seq, hkv, d] -> quantize, encode, per-row inject, scatter
+    into manager's caches.  Strided views whose head rows are contiguous are read
+    in place (kvecc_shim_write_strided), anything else is made contiguous."""
+    batch, seq = k.shape[0], k.shape[1]
     if k.dtype not in _DT or v.dtype != k.dtype:
         raise TypeError(f"unsupported K/V dtype {k.dtype}/{v.dtype}")
-    k, v = k.contiguous(), v.contiguous()
+    hkv, d = manager.num_kv_heads, manager.head_dim
+    k4 = _head_rows(k, batch, seq, hkv, d)
+    v4 = _head_rows(v, batch, seq, hkv, d)
     table = manager.block_table[seq_id]
-    _lib.call("kvecc_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq,
+    _lib.call("kvecc_shim_write_strided", _ptr(k4), _ptr(v4), k4.stride(0), k4.stride(1),
+              k4.stride(2), v4.stride(0), v4.stride(1), v4.stride(2), _DT[k.dtype], batch, seq,
               manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec],
               _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), int(n_bits),
               int(bool(inject)), float(ber), int(seed0), _ptr(manager.k_cache),
               _ptr(manager.v_cache), _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table),
               manager.num_layers, manager.block_size, int(layer), _stream(k.device))
+
+
+def _head_rows(x, batch, seq, hkv, d):
+    """[batch, seq, hkv, d] view of x with unit element stride and head stride
+    >= d (a copy only when no such view exists)."""
+    try:
+        x4 = x.view(batch, seq, hkv, d)
+    except RuntimeError:
+        x4 = None
+    if x4 is None or x4.stride(3) != 1 or x4.stride(2) < d or min(x4.stride()) < 0:
+        x4 = x.reshape(batch, seq, hkv, d).contiguous()
+    return x4
 
 
 def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=0):

@@ -210,3 +210,32 @@ def test_hip_and_cpu_backends_write_identical_caches(gpu, rule):
         for i in range(6):
             assert torch.equal(hip[i], cpu[i]), (codec, rule, i)
         assert hip[6] == cpu[6], (codec, rule)
+
+
+@pytest.mark.gpu
+def test_strided_write_equals_contiguous(gpu):
+    """kvecc_shim_write_strided reads the projections' views in place: a slice of
+    a fused [b, s, 3*hidden] QKV output (GPT-2) and a transposed [b, h, s, d]
+    tensor (Llama after RoPE) leave the same cache bytes and scales as the
+    reference's .transpose(1, 2).contiguous() copies (ecc_shim.py:1290-1291)."""
+    from kvecc import ops
+    from kvecc.ecc_shim import SimpleBlockManager
+    b, s, hk, d = 3, 37, 4, 64
+    for codec, nb in (("hamming84", 8), ("golay", 24), ("int4", 4)):
+        g = torch.Generator().manual_seed(nb)
+        qkv = torch.randn(b, s, 3 * hk * d, generator=g).to(gpu, torch.float16)
+        _, k, v = qkv.split(hk * d, dim=2)                      # GPT-2: strided slices
+        kh = k.view(b, s, hk, d).transpose(1, 2).contiguous()   # Llama: [b, h, s, d]
+        variants = {"contiguous": (k.contiguous(), v.contiguous()),
+                    "qkv_slice": (k, v),
+                    "heads_first": (kh.transpose(1, 2), v.view(b, s, hk, d))}
+        res = {}
+        for name, (kk, vv) in variants.items():
+            mgr = SimpleBlockManager(4, 16, 2, hk, d, device=gpu, codec=codec)
+            mgr.allocate(0, s)
+            ops.shim_write(kk, vv, mgr, 1, codec, nb, True, 0.03, 17)
+            res[name] = (mgr.k_cache.cpu(), mgr.v_cache.cpu(), mgr.k_scales.cpu(), mgr.v_scales.cpu())
+        for name in ("qkv_slice", "heads_first"):
+            for i in range(4):
+                assert torch.equal(res[name][i], res["contiguous"][i]), (codec, name, i)
+        assert res["contiguous"][2].abs().sum() > 0
