@@ -78,15 +78,18 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
 }
 
 // Rows of at most 64 chunks (every row of the shim and the reference's tests):
-// each lane loads its one 16-byte chunk ONCE, non-temporally, and two row
-// groups are in flight per iteration.
+// each lane loads its one 16-byte chunk ONCE, non-temporally.  One row group
+// per wave-iteration and a deep grid (64 workgroups per CU, ~4 iterations per
+// wave) beat two groups in flight per iteration with 16 per CU, and a prefetch
+// of the next iteration's chunk: fp16 D=128 rows 77.7 -> 68.2 us
+// (tools/exp/run_quant.py).
 template <typename T, int VEC, int LPR>
 __global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__restrict__ x, int codec,
                                                                     int rule, uint8_t *__restrict__ cw,
                                                                     float *__restrict__ scales,
                                                                     int64_t rows, int64_t d) {
   static_assert(sizeof(T) * VEC == 16, "one 16-byte chunk per lane");
-  constexpr int kU = 2;
+  constexpr int kU = 1;
   constexpr int rows_per_wave = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int sub = lane / LPR, li = lane % LPR;
@@ -194,14 +197,13 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_kernel(const uint8_t *_
 // contiguous span; non-temporal, kU accesses in flight per lane.  Row indices
 // are a shift when the chunks per row are a power of two (shift >= 0), else a
 // 32-bit division (64-bit division is ~100 instructions).
-template <typename TO>
+template <typename TO, int kU>
 __global__ __launch_bounds__(kBlock) void decode_dequant_wide_kernel(const uint32_t *__restrict__ cw,
                                                                      const float *__restrict__ scales,
                                                                      TO *__restrict__ out,
                                                                      uint32_t nchunk, int shift,
                                                                      uint32_t total, int zero_doubles,
                                                                      uint64_t *__restrict__ stats) {
-  constexpr int kU = 4;
   constexpr int kW = 4 / sizeof(TO);  // codeword words per access
   using InT = typename std::conditional<kW == 1, uint32_t, u32x2>::type;
   const uint32_t stride = gridDim.x * kBlock;
@@ -253,7 +255,7 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
   bool vec = d % V == 0 && aligned(x, 16) && aligned(cw, V);
   if (vec && d / V <= kWave) {
     const int lpr = lanes_per_row(d / V);
-    const unsigned grid = grid_for(cdiv(rows, kWave / lpr), kBlock / kWave, 16);
+    const unsigned grid = grid_for(cdiv(rows, kWave / lpr), kBlock / kWave, 64);
 #define KVECC_QE1C(L)                                                                         \
   case L:                                                                                     \
     KVECC_LAUNCH((quantize_encode_1c_kernel<T, V, L>), dim3(grid), dim3(kBlock), 0, st, xt, \
@@ -286,9 +288,17 @@ static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t
     const uint32_t total = (uint32_t)(rows * (d / kCw));
     const uint32_t nchunk = (uint32_t)(d / kCw);
     const int shift = (nchunk & (nchunk - 1)) == 0 ? __builtin_ctz(nchunk) : -1;
-    KVECC_LAUNCH((decode_dequant_wide_kernel<TO>), dim3(grid_for(total, kBlock * 4, 16)),
-                       dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o,
-                       nchunk, shift, total, zero_doubles, stats);
+    // deep grids, few accesses in flight per lane (tools/exp/run_dequant.py at
+    // [8,4096,32,128]): fp16/bf16 1 access and 64 workgroups per CU, 86.8 ->
+    // 76.2 us; fp32 4 accesses and 128 per CU, 131.8 -> 119.5 us
+    if (sizeof(TO) == 2)
+      KVECC_LAUNCH((decode_dequant_wide_kernel<TO, 1>), dim3(grid_for(total, kBlock, 64)),
+                   dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o, nchunk,
+                   shift, total, zero_doubles, stats);
+    else
+      KVECC_LAUNCH((decode_dequant_wide_kernel<TO, 4>), dim3(grid_for(total, kBlock * 4, 128)),
+                   dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o, nchunk,
+                   shift, total, zero_doubles, stats);
   } else if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
     int64_t total = rows * (d / 4);
     KVECC_LAUNCH((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),

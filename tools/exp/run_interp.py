@@ -24,7 +24,7 @@ cases = {"prod": lambda: ops.interpolate_into(q.view(-1), err.view(-1), out.view
 for v in range(8):
     R = {0: 8, 1: 8, 2: 8, 3: 16, 4: 16, 5: 16, 6: 4, 7: 8}[v]
     items = B * (L // R) * chunks
-    for grid in sorted({items // 256, 4096, 2048}):
+    for grid in (sorted({items // 256, 4096, 8192, 16384}) if v in (0, 3, 7) else [4096]):
         cases[f"v{v}_g{grid}"] = (lambda v=v, grid=grid: lib.interp_exp(v, P(q), P(err), P(out), B, L, chunks, grid, s))
 ok = {}
 for kk, fn in cases.items():
