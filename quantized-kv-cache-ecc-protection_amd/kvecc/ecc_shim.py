@@ -155,6 +155,11 @@ class SimpleBlockManager:
         self.block_table = torch.full((self.max_seqs, self.max_blocks_per_seq), -1,
                                       dtype=torch.int32, device=device)
         self._host_table = {}  # seq_id -> list of physical blocks (mirror, no device reads)
+        # physical block ids on the device: a contiguous run of new blocks is
+        # written into the table with a device-to-device copy, so allocation in
+        # a steady-state forward issues no host-to-device transfer and the
+        # whole patched forward can be captured in a HIP graph
+        self._block_ids = torch.arange(num_blocks, dtype=torch.int32, device=device)
 
     def allocate(self, seq_id, num_tokens):
         need = (num_tokens + self.block_size - 1) // self.block_size
@@ -167,8 +172,11 @@ class SimpleBlockManager:
         self.seq_to_blocks[seq_id] = blocks
         self.seq_to_len[seq_id] = num_tokens
         if new:
-            self.block_table[seq_id, len(existing):len(blocks)] = torch.tensor(
-                new, dtype=torch.int32, device=self.block_table.device)
+            dst = self.block_table[seq_id, len(existing):len(blocks)]
+            if new == list(range(new[0], new[0] + len(new))):
+                dst.copy_(self._block_ids[new[0]:new[0] + len(new)])
+            else:
+                dst.copy_(torch.tensor(new, dtype=torch.int32, device=self.block_table.device))
         self._host_table[seq_id] = blocks
         return self.block_table[seq_id], num_tokens
 

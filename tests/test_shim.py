@@ -239,3 +239,43 @@ def test_strided_write_equals_contiguous(gpu):
             for i in range(4):
                 assert torch.equal(res[name][i], res["contiguous"][i]), (codec, name, i)
         assert res["contiguous"][2].abs().sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,interp", [("hamming84", True), ("golay", False)])
+def test_patched_forward_replays_in_a_hip_graph(gpu, codec, interp):
+    """The whole patched forward (cache reset included) captures in one HIP graph:
+    no host sync or host-to-device copy in a steady-state forward.  Replays give
+    the eager forward's logits and ECC statistics (same seeds: the reset restarts
+    the injection counter, as the reference's per-text reset does)."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+    from kvecc.ecc_shim import (ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention,
+                                reset_ecc_cache)
+    torch.manual_seed(0)
+    cfg_m = GPT2Config(n_layer=2, n_head=4, n_embd=256, n_positions=128)
+    model = GPT2LMHeadModel(cfg_m).half().to(gpu).eval()
+    ids = torch.randint(0, cfg_m.vocab_size, (1, 96), generator=torch.Generator().manual_seed(1)).to(gpu)
+    cfg = ECCShimConfig(codec=codec, ber=1e-2, inject_errors=True, seed=42, block_size=16,
+                        use_interpolation=interp)
+    with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=6):
+        def fwd():
+            reset_ecc_cache(model)
+            return model(ids).logits
+        eager = fwd().clone()
+        eager_stats = get_ecc_stats(model)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                fwd()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = fwd()
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
+        st = get_ecc_stats(model)
+        assert st["errors_corrected"] == eager_stats["errors_corrected"] > 0
+        assert st["errors_detected"] == eager_stats["errors_detected"]

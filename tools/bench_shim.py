@@ -24,6 +24,21 @@ sys.path.insert(0, os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd"))
 import torch  # noqa: E402
 
 
+def graphed(fn, warmup=3):
+    """Capture fn (one forward) in a HIP graph after warm-up on a side stream;
+    returns a callable that replays it (its outputs live in the graph's pool)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(warmup):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    return g.replay
+
+
 def timed(fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -48,6 +63,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--composed", action="store_true",
                     help="per-op kernels instead of the fused cache write/read")
+    ap.add_argument("--graph", action="store_true",
+                    help="time HIP-graph replays of the whole forward (patched and unpatched)")
     ap.add_argument("--cpu-backend", action="store_true",
                     help="also run the same forward on the host backend (fp32, CPU)")
     args = ap.parse_args()
@@ -64,6 +81,8 @@ def main():
     with torch.no_grad():
         med, mn = timed(lambda: model(ids), args.steps, args.warmup)
         out["unpatched_ms"] = med
+        if args.graph:
+            out["unpatched_graph_ms"] = timed(graphed(lambda: model(ids)), args.steps, args.warmup)[0]
         nblocks = (args.seq + 15) // 16
         for ber in args.bers:
             cfg = ECCShimConfig(codec=args.codec, ber=ber, inject_errors=ber > 0, seed=42,
@@ -74,10 +93,11 @@ def main():
                     reset_ecc_cache(model)
                     return model(ids)
                 med, mn = timed(fwd, args.steps, args.warmup)
+                graph_ms = timed(graphed(fwd), args.steps, args.warmup)[0] if args.graph else None
                 reset_ecc_cache(model)
                 res = model(ids, labels=ids)
                 st = get_ecc_stats(model)
-            out["runs"].append({"ber": ber, "forward_ms": med, "min_ms": mn,
+            out["runs"].append({"ber": ber, "forward_ms": med, "min_ms": mn, "graph_ms": graph_ms,
                                 "tokens_per_s": args.seq / (med * 1e-3),
                                 "loss": float(res.loss),
                                 "logits_finite": bool(torch.isfinite(res.logits).all()),
