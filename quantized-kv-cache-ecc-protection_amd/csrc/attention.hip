@@ -30,6 +30,14 @@ constexpr int kMaxSplit = 1024;   // context tokens per workgroup (upper bound)
 constexpr int kMaxSplits = 1024;  // splits per (batch, head)
 constexpr int kAttnMaxD = 256;
 constexpr int kUnroll = 4;        // token rows in flight per lane group
+// codeword words per lane of a token row (A/B knobs: tools/exp/run_attn.py)
+#ifndef KVECC_ATTN_H84_VEC
+#define KVECC_ATTN_H84_VEC 4
+#endif
+#ifndef KVECC_ATTN_GOLAY_VEC
+#define KVECC_ATTN_GOLAY_VEC 3
+#endif
+constexpr int kH84Vec = KVECC_ATTN_H84_VEC, kGolayVec = KVECC_ATTN_GOLAY_VEC;
 
 struct AttnArgs {
   const void *q;  // [B, H, D]
@@ -58,12 +66,15 @@ struct Chunk {
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
     if (CODEC == KVECC_CODEC_H84) {
       const uint8_t *p = reinterpret_cast<const uint8_t *>(cache) + row * a.d + 4 * VEC * c;
-      if (VEC == 4) {
-        const u32x4 v = *reinterpret_cast<const u32x4 *>(p);
-        w[0] = v.x;
-        w[VEC > 1 ? 1 : 0] = v.y;
-        w[VEC > 2 ? 2 : 0] = v.z;
-        w[VEC > 3 ? 3 : 0] = v.w;
+      if (VEC % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < VEC; k += 4) {
+          const u32x4 v = reinterpret_cast<const u32x4 *>(p)[k / 4];
+          w[k] = v.x;
+          w[k + 1] = v.y;
+          w[k + 2] = v.z;
+          w[k + 3] = v.w;
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) w[k] = reinterpret_cast<const uint32_t *>(p)[k];
@@ -356,10 +367,12 @@ template <typename T, int CODEC>
 static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
   dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads));
   int rc;
-  if (CODEC == KVECC_CODEC_H84 && a.d % 16 == 0)
-    rc = launch_split<T, CODEC, 4>(a, grid, st);  // 16-byte loads, 16 codewords per lane
+  if (CODEC == KVECC_CODEC_H84 && a.d % (4 * kH84Vec) == 0)
+    rc = launch_split<T, CODEC, kH84Vec>(a, grid, st);  // 16-byte loads, 16 codewords per lane
+  else if (CODEC == KVECC_CODEC_H84 && a.d % 16 == 0)
+    rc = launch_split<T, CODEC, 4>(a, grid, st);
   else if (CODEC == KVECC_CODEC_GOLAY)
-    rc = launch_split<T, CODEC, 3>(a, grid, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
+    rc = launch_split<T, CODEC, kGolayVec>(a, grid, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
   else
     rc = launch_split<T, CODEC, 1>(a, grid, st);
   if (rc != KVECC_OK) return rc;
