@@ -213,6 +213,167 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_kernel(
   if (stats) flush_stats2(stats, bits, unc);
 }
 
+// Tiled per-head packing.  A row of D nibbles and its ceil(D/3) codewords are
+// not 16-byte multiples (128 B and 172 B at D = 128), and a codeword's three
+// nibbles straddle lanes.  Each WAVE owns a tile of R whole rows (R * D and
+// R * ceil(D/3) * 4 both multiples of 16 B, ~2 KiB of nibbles): the tile moves
+// through HBM as 16-byte accesses, is staged in the wave's own LDS region, and
+// the codewords are built there (rows in turn, lane = codeword: no division).
+// The regions are wave-private, so no workgroup barrier sits between the
+// phases, and the next tile's loads are issued into registers before the
+// current tile is processed (one tile of loads in flight per wave throughout).
+// The one-thread-per-codeword kernels above stay for short rows (a wave would
+// idle on < 16 codewords per row) and for tiles over 64 KiB of LDS.
+constexpr int kTiledMaxD = 512;
+constexpr int kRowWaves = kBlock / kWave;
+constexpr int kTilePre = 4;  // 16-B vectors per lane held for the next tile
+
+struct RowTile {
+  int rows;      // R rows per wave tile
+  int in_bytes;  // R * d rounded up to 16
+  int cw_bytes;  // R * g * 4
+};
+
+inline int gcd_i(int a, int b) { return b ? gcd_i(b, a % b) : a; }
+inline RowTile row_tile(int64_t d, int64_t g) {
+  const int r0 = 16 / gcd_i((int)(d % 16), 16), r1 = 4 / gcd_i((int)(g % 4), 4);
+  int r = r0 / gcd_i(r0, r1) * r1;  // lcm: both byte counts are 16-B multiples
+  while (2 * r * d <= 2048) r *= 2;  // ~2 KiB of nibbles per wave tile
+  RowTile t;
+  t.rows = r;
+  t.in_bytes = (int)((r * d + 15) & ~15LL);
+  t.cw_bytes = (int)(r * g * 4);
+  return t;
+}
+inline size_t row_tile_lds(const RowTile &t, bool decode) {
+  return (decode ? 16384 : 8192) + (size_t)kRowWaves * (t.in_bytes + t.cw_bytes);
+}
+inline bool row_tiled(int64_t d, int64_t g, bool decode) {
+  return g >= 16 && d <= kTiledMaxD && row_tile_lds(row_tile(d, g), decode) <= 65536;
+}
+
+// The streamed-in side of a wave tile: `bytes` from global `src` into the
+// wave's LDS region.  Full aligned tiles of <= kTilePre vectors per lane go
+// through registers loaded one tile ahead (prefetch / land); anything else is
+// copied in place (byte loop when unaligned or partial).
+struct TileIn {
+  u32x4 v[kTilePre];
+  __device__ __forceinline__ void prefetch(const uint8_t *src, int nvec, int lane) {
+#pragma unroll
+    for (int k = 0; k < kTilePre; ++k)
+      if (lane + k * kWave < nvec) v[k] = ld_stream(reinterpret_cast<const u32x4 *>(src) + lane + k * kWave);
+  }
+  __device__ __forceinline__ void land(uint8_t *lds, int nvec, int lane) const {
+#pragma unroll
+    for (int k = 0; k < kTilePre; ++k)
+      if (lane + k * kWave < nvec) reinterpret_cast<u32x4 *>(lds)[lane + k * kWave] = v[k];
+  }
+};
+
+// wave-cooperative copy of `bytes` (16-B vectors when `vec`)
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, int bytes, bool vec,
+                                          bool to_global, int lane) {
+  if (vec) {
+    for (int v = lane; v < bytes / 16; v += kWave) {
+      if (to_global)
+        st_stream(reinterpret_cast<u32x4 *>(dst) + v, reinterpret_cast<const u32x4 *>(src)[v]);
+      else
+        reinterpret_cast<u32x4 *>(dst)[v] = ld_stream(reinterpret_cast<const u32x4 *>(src) + v);
+    }
+  } else {
+    for (int b = lane; b < bytes; b += kWave) dst[b] = src[b];
+  }
+}
+
+// Tile loop shared by encode and decode: `in` / `in_tile_bytes` / `in_row_bytes`
+// describe the streamed-in array; body(r0, nr) processes rows [r0, r0 + nr)
+// from `lds_in` and stores its results.
+template <typename Body>
+__device__ __forceinline__ void row_tiles(const uint8_t *in, int64_t rows, int rows_per_tile,
+                                          int in_row_bytes, bool aligned16, uint8_t *lds_in,
+                                          int lane, int wave, Body body) {
+  const int64_t ntiles = (rows + rows_per_tile - 1) / rows_per_tile;
+  const int64_t stride = (int64_t)gridDim.x * kRowWaves;
+  const int tile_bytes = rows_per_tile * in_row_bytes;
+  const int nvec = tile_bytes / 16;
+  const bool pre_ok = aligned16 && nvec <= kTilePre * kWave;
+  auto full = [&](int64_t t) { return pre_ok && (t + 1) * rows_per_tile <= rows; };
+  TileIn nxt;
+  int64_t t = (int64_t)blockIdx.x * kRowWaves + wave;
+  if (t < ntiles && full(t)) nxt.prefetch(in + t * tile_bytes, nvec, lane);
+  for (; t < ntiles; t += stride) {
+    const int64_t r0 = t * rows_per_tile;
+    const int nr = (int)min<int64_t>(rows_per_tile, rows - r0);
+    if (full(t))
+      nxt.land(lds_in, nvec, lane);
+    else
+      wave_copy(lds_in, in + t * tile_bytes, nr * in_row_bytes, aligned16 && nr == rows_per_tile,
+                false, lane);
+    if (t + stride < ntiles && full(t + stride)) nxt.prefetch(in + (t + stride) * tile_bytes, nvec, lane);
+    body(r0, nr);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
+    const uint8_t *__restrict__ nib, int32_t *__restrict__ cw, int64_t rows, int d, int g,
+    RowTile tl, bool aligned16, const uint16_t *__restrict__ par) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t *tab = reinterpret_cast<uint16_t *>(smem);
+  for (int i = threadIdx.x; i < 512; i += kBlock)
+    reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(par)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  uint8_t *tin = smem + 8192 + wave * (tl.in_bytes + tl.cw_bytes);
+  uint32_t *tcw = reinterpret_cast<uint32_t *>(tin + tl.in_bytes);
+  row_tiles(nib, rows, tl.rows, d, aligned16, tin, lane, wave, [&](int64_t r0, int nr) {
+    for (int rr = 0; rr < nr; ++rr) {
+      const uint8_t *row = tin + rr * d;
+      for (int j = lane; j < g; j += kWave) {
+        const int c = 3 * j;
+        const uint32_t dw = golay_pack(row[c], c + 1 < d ? row[c + 1] : 0u, c + 2 < d ? row[c + 2] : 0u);
+        tcw[rr * g + j] = dw | (uint32_t)tab[dw] << 12;
+      }
+    }
+    wave_copy(reinterpret_cast<uint8_t *>(cw + r0 * g), reinterpret_cast<const uint8_t *>(tcw),
+              nr * g * 4, aligned16 && nr == tl.rows, true, lane);
+  });
+}
+
+__global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
+    const int32_t *__restrict__ cw, uint8_t *__restrict__ nib, int64_t rows, int d, int g,
+    RowTile tl, bool aligned16, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
+    uint64_t *__restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint16_t *tab = reinterpret_cast<uint16_t *>(smem);
+  for (int i = threadIdx.x; i < 512; i += kBlock) {
+    reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(par)[i];
+    reinterpret_cast<u32x4 *>(tab)[512 + i] = reinterpret_cast<const u32x4 *>(cor)[i];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  uint8_t *tout = smem + 16384 + wave * (tl.in_bytes + tl.cw_bytes);
+  uint32_t *tcw = reinterpret_cast<uint32_t *>(tout + tl.in_bytes);
+  uint32_t bits = 0, unc = 0;
+  row_tiles(reinterpret_cast<const uint8_t *>(cw), rows, tl.rows, g * 4, aligned16,
+            reinterpret_cast<uint8_t *>(tcw), lane, wave, [&](int64_t r0, int nr) {
+    for (int rr = 0; rr < nr; ++rr) {
+      uint8_t *row = tout + rr * d;
+      for (int j = lane; j < g; j += kWave) {
+        uint32_t c;
+        const uint32_t dd = golay_decode1(tcw[rr * g + j], tab, tab + 4096, c);
+        bits += c & 3u;
+        unc += c >> 2;
+        const int k = 3 * j;
+        row[k] = (uint8_t)(dd & 0xFu);
+        if (k + 1 < d) row[k + 1] = (uint8_t)(dd >> 4 & 0xFu);
+        if (k + 2 < d) row[k + 2] = (uint8_t)(dd >> 8);
+      }
+    }
+    wave_copy(nib + r0 * d, tout, nr * d, aligned16 && nr == tl.rows, true, lane);
+  });
+  if (stats) flush_stats2(stats, bits, unc);
+}
+
 }  // namespace kvecc
 
 using namespace kvecc;
@@ -291,6 +452,14 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
   const uint16_t *par = golay_parity_table_dev();
   if (!par) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
+  if (row_tiled(d, g, false)) {
+    const RowTile tl = row_tile(d, g);
+    const bool a16 = aligned(nibbles, 16) && aligned(codewords, 16);
+    const unsigned grid = grid_for(cdiv(rows, tl.rows), kRowWaves, 8);
+    KVECC_LAUNCH(golay_encode_rows_tiled_kernel, dim3(grid), dim3(kBlock), row_tile_lds(tl, false),
+                 as_stream(stream), nibbles, codewords, rows, (int)d, (int)g, tl, a16, par);
+    return check_launch("golay_encode_rows");
+  }
   unsigned grid = grid_for(rows * g, kBlock);
   KVECC_LAUNCH(golay_encode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
                      nibbles, codewords, rows, d, g, par);
@@ -306,6 +475,15 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
   const uint16_t *cor = golay_correct_table_dev();
   if (!par || !cor) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
+  if (row_tiled(d, g, true)) {
+    const RowTile tl = row_tile(d, g);
+    const bool a16 = aligned(nibbles, 16) && aligned(codewords, 16);
+    const unsigned grid = grid_for(cdiv(rows, tl.rows), kRowWaves, 8);
+    KVECC_LAUNCH(golay_decode_rows_tiled_kernel, dim3(grid), dim3(kBlock), row_tile_lds(tl, true),
+                 as_stream(stream), codewords, nibbles, rows, (int)d, (int)g, tl, a16, par, cor,
+                 stats);
+    return check_launch("golay_decode_rows");
+  }
   unsigned grid = grid_for(rows * g, kBlock);
   KVECC_LAUNCH(golay_decode_rows_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream),
                      codewords, nibbles, rows, d, g, par, cor, stats);

@@ -511,3 +511,32 @@ def test_time_next_launch_stamps_one_kernel(gpu):
     ops.hamming84_encode_into(x, out)  # disarmed: the events keep their stamps
     torch.cuda.synchronize()
     assert start.elapsed_time(stop) == t1
+
+
+@pytest.mark.parametrize("d", [1, 2, 5, 46, 47, 64, 100, 127, 128, 129, 255, 256, 300, 511, 513])
+@pytest.mark.parametrize("rows,offset", [(1, 0), (63, 0), (64, 0), (65, 1), (1000, 0), (1000, 3)])
+def test_golay_rows_vs_cpu_backend(gpu, d, rows, offset):
+    """Per-head packing (ecc_shim.py:623-682): the wave-tiled LDS kernels (46 <= d <= 512:
+    full and partial wave tiles, aligned and unaligned buffers) and the
+    per-codeword kernels (short rows, d = 511 and 513) against the host twin, encode and a
+    noisy decode."""
+    from kvecc import cpu_ops, ops
+    g = torch.Generator().manual_seed(d * 1009 + rows)
+    base = torch.randint(0, 16, (rows * d + offset,), generator=g, dtype=torch.uint8)
+    x = base[offset:].view(rows, d)
+    cw = ops.golay_encode_rows(base.to(gpu)[offset:].view(rows, d))
+    ref = cpu_ops.golay_encode_rows(x)
+    assert torch.equal(cw.cpu(), ref)
+    noisy = ref.clone().view(-1)
+    flips = torch.randint(0, 1 << 24, noisy.shape, generator=g, dtype=torch.int32)
+    mask = torch.rand(noisy.shape, generator=g) < 0.3
+    flips &= torch.randint(0, 1 << 24, noisy.shape, generator=g, dtype=torch.int32)  # ~6 bits each
+    noisy[mask] ^= flips[mask]
+    noisy = noisy.view(rows, -1)
+    cbuf = torch.zeros(noisy.numel() + offset, dtype=torch.int32)
+    cbuf[offset:] = noisy.view(-1)
+    st, cst = ops.new_stats(gpu), cpu_ops.new_stats()
+    out = ops.golay_decode_rows(cbuf.to(gpu)[offset:].view(rows, -1), d, st)
+    want = cpu_ops.golay_decode_rows(noisy, d, cst)
+    assert torch.equal(out.cpu(), want)
+    assert ops.read_stats(st) == cpu_ops.read_stats(cst)
