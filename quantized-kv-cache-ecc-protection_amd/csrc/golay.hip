@@ -309,8 +309,12 @@ __device__ __forceinline__ void row_tiles(const uint8_t *in, int64_t rows, int r
     else
       wave_copy(lds_in, in + t * tile_bytes, nr * in_row_bytes, aligned16 && nr == rows_per_tile,
                 false, lane);
+    // lanes read each other's LDS bytes through other types in the next phase:
+    // keep the compiler from moving LDS accesses across the phase boundaries
+    __builtin_amdgcn_wave_barrier();
     if (t + stride < ntiles && full(t + stride)) nxt.prefetch(in + (t + stride) * tile_bytes, nvec, lane);
     body(r0, nr);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -334,6 +338,7 @@ __global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
         tcw[rr * g + j] = dw | (uint32_t)tab[dw] << 12;
       }
     }
+    __builtin_amdgcn_wave_barrier();
     wave_copy(reinterpret_cast<uint8_t *>(cw + r0 * g), reinterpret_cast<const uint8_t *>(tcw),
               nr * g * 4, aligned16 && nr == tl.rows, true, lane);
   });
@@ -369,6 +374,7 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
         if (k + 2 < d) row[k + 2] = (uint8_t)(dd >> 8);
       }
     }
+    __builtin_amdgcn_wave_barrier();
     wave_copy(nib + r0 * d, tout, nr * d, aligned16 && nr == tl.rows, true, lane);
   });
   if (stats) flush_stats2(stats, bits, unc);

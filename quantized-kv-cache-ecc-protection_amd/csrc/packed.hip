@@ -165,6 +165,75 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_kernel(
       st_stream(reinterpret_cast<u32x3v *>(nib + (G0 + g * kWave + lane) * 3), u32x3v{n[0], n[1], n[2]});
       if (WITH_FLAGS) st_stream(flags + G0 + g * kWave + lane, (uint8_t)fl);
     }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (WITH_STATS) flush_stats2<kPkBlock>(stats, bits, unc);
+}
+
+// Staged variant: each wave loads its 3072 contiguous codeword bytes (two
+// groups of 8 codewords per lane) as three 16-byte loads per lane into a
+// wave-private LDS region -- no workgroup barrier -- with the next tile's loads
+// already in registers, and reads its 24-byte groups back as 8-byte LDS reads
+// (lane stride 6 dwords: conflict-free).  43.6 vs 44.9 us for the direct
+// 8-byte-load kernel above (tools/exp/run_packed.py); taken for 16-B aligned
+// codewords (KVECC_PACKED_DEC_STAGED=0 restores the direct kernel).
+#ifndef KVECC_PACKED_DEC_STAGED
+#define KVECC_PACKED_DEC_STAGED 1
+#endif
+constexpr int kPkWaveBytes = kPkWaveCw * 3;  // 3072
+template <bool WITH_FLAGS, bool WITH_STATS>
+__global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
+    const uint32_t *__restrict__ cw, uint32_t *__restrict__ nib, uint8_t *__restrict__ flags,
+    int64_t ntiles, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
+    uint64_t *__restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[8192];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kPkBlock / kWave][kPkWaveBytes];
+  load_tables_pk(lds, par, cor, true);
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  uint8_t *mine = stage[wave];
+  uint32_t bits = 0, unc = 0;
+  constexpr int kV = kPkWaveBytes / 16 / kWave;  // 3 vectors per lane
+  auto src_of = [&](int64_t t) {
+    return reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(cw) +
+                                           (t * kPkTile + wave * kPkWaveCw) * 3);
+  };
+  u32x4 nxt[kV];
+  int64_t t = blockIdx.x;
+  if (t < ntiles) {
+#pragma unroll
+    for (int k = 0; k < kV; ++k) nxt[k] = ld_stream(src_of(t) + lane + k * kWave);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < kV; ++k) reinterpret_cast<u32x4 *>(mine)[lane + k * kWave] = nxt[k];
+    // lanes read each other's bytes through other vector types: keep the
+    // compiler from moving LDS accesses across the phase boundaries
+    __builtin_amdgcn_wave_barrier();
+    if (t + gridDim.x < ntiles) {
+#pragma unroll
+      for (int k = 0; k < kV; ++k) nxt[k] = ld_stream(src_of(t + gridDim.x) + lane + k * kWave);
+    }
+    const int64_t G0 = (t * kPkTile + wave * kPkWaveCw) / 8;
+#pragma unroll
+    for (int g = 0; g < kPkGroups; ++g) {
+      const u32x2 *p = reinterpret_cast<const u32x2 *>(mine + (g * kWave + lane) * 24);
+      const u32x2 a = p[0], b = p[1], c2 = p[2];
+      const uint32_t w[6] = {a.x, a.y, b.x, b.y, c2.x, c2.y};
+      uint32_t c[8], d[8], n[3], fl = 0;
+      cw_unpack8(w, c);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t cnt;
+        d[k] = golay_decode1(c[k], lds, lds + 4096, cnt);
+        bits += cnt & 3u;
+        unc += cnt >> 2;
+        fl |= (cnt >> 2) << k;
+      }
+      nib_pack8(d, n);
+      st_stream(reinterpret_cast<u32x3v *>(nib + (G0 + g * kWave + lane) * 3), u32x3v{n[0], n[1], n[2]});
+      if (WITH_FLAGS) st_stream(flags + G0 + g * kWave + lane, (uint8_t)fl);
+    }
+    __builtin_amdgcn_wave_barrier();
   }
   if (WITH_STATS) flush_stats2<kPkBlock>(stats, bits, unc);
 }
@@ -347,7 +416,23 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
   if (!par || !cor) return KVECC_EHIP;
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
-  if (aligned(nibbles, 4) && aligned(codewords, 4)) {
+  if (KVECC_PACKED_DEC_STAGED && aligned(nibbles, 4) && aligned(codewords, 16)) {
+    const int64_t ntiles = m / kPkTile;
+    if (ntiles > 0) {
+      const dim3 grid(grid_for(ntiles, 1, 32)), block(kPkBlock);
+      const uint32_t *c = reinterpret_cast<const uint32_t *>(codewords);
+      uint32_t *n = reinterpret_cast<uint32_t *>(nibbles);
+      if (uncorrectable && stats)
+        KVECC_LAUNCH((golay_decode_packed_staged_kernel<true, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+      else if (uncorrectable)
+        KVECC_LAUNCH((golay_decode_packed_staged_kernel<true, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+      else if (stats)
+        KVECC_LAUNCH((golay_decode_packed_staged_kernel<false, true>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+      else
+        KVECC_LAUNCH((golay_decode_packed_staged_kernel<false, false>), grid, block, 0, st, c, n, uncorrectable, ntiles, par, cor, stats);
+    }
+    done = ntiles * kPkTile;
+  } else if (aligned(nibbles, 4) && aligned(codewords, 4)) {
     const int64_t ntiles = m / kPkTile;
     if (ntiles > 0) {
       const dim3 grid(grid_for(ntiles, 1, 32)), block(kPkBlock);
