@@ -318,9 +318,30 @@ __device__ __forceinline__ void row_tiles(const uint8_t *in, int64_t rows, int r
   }
 }
 
+// Quad items: when d % 4 == 0 a lane takes 4 consecutive codewords of a row
+// (12 nibble bytes = 3 aligned dwords of the LDS row), item k = lane + 64 * it
+// of the tile -> (row k / Q, quad k % Q), Q = ceil(g / 4), mapped once per
+// kernel; tiles of up to kQuadIters * 64 items.  Otherwise a lane takes one
+// codeword of a row in turn (3 byte reads).
+constexpr int kQuadIters = 4;
+struct QuadItems {
+  int rr[kQuadIters], jj[kQuadIters];
+  __device__ __forceinline__ QuadItems(int lane, int q) {
+#pragma unroll
+    for (int it = 0; it < kQuadIters; ++it) {
+      const int k = lane + it * kWave;
+      rr[it] = k / q;
+      jj[it] = k - rr[it] * q;
+    }
+  }
+};
+inline bool quad_ok(int64_t d, int64_t g, const RowTile &t) {
+  return d % 4 == 0 && t.rows * ((g + 3) / 4) <= kQuadIters * kWave;
+}
+
 __global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
     const uint8_t *__restrict__ nib, int32_t *__restrict__ cw, int64_t rows, int d, int g,
-    RowTile tl, bool aligned16, const uint16_t *__restrict__ par) {
+    RowTile tl, bool aligned16, bool quads, const uint16_t *__restrict__ par) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *tab = reinterpret_cast<uint16_t *>(smem);
   for (int i = threadIdx.x; i < 512; i += kBlock)
@@ -329,7 +350,23 @@ __global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   uint8_t *tin = smem + 8192 + wave * (tl.in_bytes + tl.cw_bytes);
   uint32_t *tcw = reinterpret_cast<uint32_t *>(tin + tl.in_bytes);
+  const int q = (g + 3) / 4;
+  const QuadItems qi(lane, q);
   row_tiles(nib, rows, tl.rows, d, aligned16, tin, lane, wave, [&](int64_t r0, int nr) {
+    if (quads) {
+#pragma unroll
+      for (int it = 0; it < kQuadIters; ++it) {
+        const int rr = qi.rr[it], jj = qi.jj[it];
+        if (rr >= nr) continue;
+        const uint32_t *rw = reinterpret_cast<const uint32_t *>(tin + rr * d) + 3 * jj;
+        const int nw = min(3, (d - 12 * jj) / 4);  // dwords of this quad inside the row
+        uint32_t dd[4];
+        golay_unpack4(rw[0], nw > 1 ? rw[1] : 0u, nw > 2 ? rw[2] : 0u, dd);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (4 * jj + k < g) tcw[rr * g + 4 * jj + k] = dd[k] | (uint32_t)tab[dd[k]] << 12;
+      }
+    } else {
     for (int rr = 0; rr < nr; ++rr) {
       const uint8_t *row = tin + rr * d;
       for (int j = lane; j < g; j += kWave) {
@@ -337,6 +374,7 @@ __global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
         const uint32_t dw = golay_pack(row[c], c + 1 < d ? row[c + 1] : 0u, c + 2 < d ? row[c + 2] : 0u);
         tcw[rr * g + j] = dw | (uint32_t)tab[dw] << 12;
       }
+    }
     }
     __builtin_amdgcn_wave_barrier();
     wave_copy(reinterpret_cast<uint8_t *>(cw + r0 * g), reinterpret_cast<const uint8_t *>(tcw),
@@ -346,8 +384,8 @@ __global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
 
 __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
     const int32_t *__restrict__ cw, uint8_t *__restrict__ nib, int64_t rows, int d, int g,
-    RowTile tl, bool aligned16, const uint16_t *__restrict__ par, const uint16_t *__restrict__ cor,
-    uint64_t *__restrict__ stats) {
+    RowTile tl, bool aligned16, bool quads, const uint16_t *__restrict__ par,
+    const uint16_t *__restrict__ cor, uint64_t *__restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint16_t *tab = reinterpret_cast<uint16_t *>(smem);
   for (int i = threadIdx.x; i < 512; i += kBlock) {
@@ -359,8 +397,33 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
   uint8_t *tout = smem + 16384 + wave * (tl.in_bytes + tl.cw_bytes);
   uint32_t *tcw = reinterpret_cast<uint32_t *>(tout + tl.in_bytes);
   uint32_t bits = 0, unc = 0;
+  const int q = (g + 3) / 4;
+  const QuadItems qi(lane, q);
   row_tiles(reinterpret_cast<const uint8_t *>(cw), rows, tl.rows, g * 4, aligned16,
             reinterpret_cast<uint8_t *>(tcw), lane, wave, [&](int64_t r0, int nr) {
+    if (quads) {
+#pragma unroll
+      for (int it = 0; it < kQuadIters; ++it) {
+        const int rr = qi.rr[it], jj = qi.jj[it];
+        if (rr >= nr) continue;
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          e[k] = 0;
+          if (4 * jj + k < g) {
+            uint32_t c;
+            e[k] = golay_spread(golay_decode1(tcw[rr * g + 4 * jj + k], tab, tab + 4096, c));
+            bits += c & 3u;
+            unc += c >> 2;
+          }
+        }
+        uint32_t *ow = reinterpret_cast<uint32_t *>(tout + rr * d) + 3 * jj;
+        const int nw = min(3, (d - 12 * jj) / 4);
+        ow[0] = e[0] | e[1] << 24;
+        if (nw > 1) ow[1] = e[1] >> 8 | e[2] << 16;
+        if (nw > 2) ow[2] = e[2] >> 16 | e[3] << 8;
+      }
+    } else {
     for (int rr = 0; rr < nr; ++rr) {
       uint8_t *row = tout + rr * d;
       for (int j = lane; j < g; j += kWave) {
@@ -373,6 +436,7 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
         if (k + 1 < d) row[k + 1] = (uint8_t)(dd >> 4 & 0xFu);
         if (k + 2 < d) row[k + 2] = (uint8_t)(dd >> 8);
       }
+    }
     }
     __builtin_amdgcn_wave_barrier();
     wave_copy(nib + r0 * d, tout, nr * d, aligned16 && nr == tl.rows, true, lane);
@@ -463,7 +527,8 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
     const bool a16 = aligned(nibbles, 16) && aligned(codewords, 16);
     const unsigned grid = grid_for(cdiv(rows, tl.rows), kRowWaves, 8);
     KVECC_LAUNCH(golay_encode_rows_tiled_kernel, dim3(grid), dim3(kBlock), row_tile_lds(tl, false),
-                 as_stream(stream), nibbles, codewords, rows, (int)d, (int)g, tl, a16, par);
+                 as_stream(stream), nibbles, codewords, rows, (int)d, (int)g, tl, a16,
+                 quad_ok(d, g, tl), par);
     return check_launch("golay_encode_rows");
   }
   unsigned grid = grid_for(rows * g, kBlock);
@@ -486,8 +551,8 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
     const bool a16 = aligned(nibbles, 16) && aligned(codewords, 16);
     const unsigned grid = grid_for(cdiv(rows, tl.rows), kRowWaves, 8);
     KVECC_LAUNCH(golay_decode_rows_tiled_kernel, dim3(grid), dim3(kBlock), row_tile_lds(tl, true),
-                 as_stream(stream), codewords, nibbles, rows, (int)d, (int)g, tl, a16, par, cor,
-                 stats);
+                 as_stream(stream), codewords, nibbles, rows, (int)d, (int)g, tl, a16,
+                 quad_ok(d, g, tl), par, cor, stats);
     return check_launch("golay_decode_rows");
   }
   unsigned grid = grid_for(rows * g, kBlock);
