@@ -21,7 +21,8 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 M = 8 * 4096 * 32 * 43  # codewords of the bench workload
 ALGO = {"golay_decode_kernel": 8 * M, "golay_encode_kernel": 7 * M,
-        "golay_decode_packed_kernel": 4.625 * M, "golay_encode_packed_kernel": 4.5 * M}
+        "golay_decode_packed_kernel": 4.625 * M, "golay_decode_packed_staged_kernel": 4.625 * M,
+        "golay_encode_packed_kernel": 4.5 * M}
 
 
 def counters(path):
