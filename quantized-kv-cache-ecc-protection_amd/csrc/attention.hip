@@ -38,6 +38,17 @@ constexpr int kUnroll = 4;        // token rows in flight per lane group
 #define KVECC_ATTN_GOLAY_VEC 3
 #endif
 constexpr int kH84Vec = KVECC_ATTN_H84_VEC, kGolayVec = KVECC_ATTN_GOLAY_VEC;
+// Cache rows go through raw buffer loads with 32-bit offsets when the caches
+// and scales are < 4 GiB (the BUF kernels): no 64-bit address arithmetic per
+// load, and reads past the row's last codeword need no clamp (inside the
+// buffer they read a neighbour row's words, which contribute nothing; past it
+// the hardware returns 0).  Golay 105.7 -> 82.1 us at [8,4096,32,128], H84
+// unchanged (tools/exp/run_attn.py).  Larger caches take 64-bit addressing.
+// packed-fp32 FMAs for the dot product and the V update
+#ifndef KVECC_ATTN_PK
+#define KVECC_ATTN_PK 1
+#endif
+constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
 
 struct AttnArgs {
   const void *q;  // [B, H, D]
@@ -49,6 +60,7 @@ struct AttnArgs {
   void *out;  // [B, H, D]
   int64_t heads, kv_heads, d, g;  // g = codewords per token row
   int64_t layers, layer, bs, max_blocks, nsplit, split;
+  uint32_t cache_bytes, scale_bytes;  // buffer-load bounds (BUF kernels)
   float sm_scale;
   const uint16_t *par, *cor;  // Golay tables
 };
@@ -63,6 +75,24 @@ struct Chunk {
   // per element and the kernel folds -8 * kOffset into the sums instead
   static constexpr float kOffset = CODEC == KVECC_CODEC_GOLAY ? 8.0f : 0.0f;
   uint32_t w[VEC];
+  __device__ __forceinline__ void load_buf(const AttnArgs &a, __amdgpu_buffer_rsrc_t rs, int32_t row,
+                                           int c) {
+    if (CODEC == KVECC_CODEC_H84) {
+      const uint32_t off = (uint32_t)row * (uint32_t)a.d + 4u * VEC * c;
+#pragma unroll
+      for (int k = 0; k < VEC; k += 4) {
+        const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * k, 0, 0));
+        w[k] = v.x;
+        w[k + 1 < VEC ? k + 1 : k] = v.y;
+        w[k + 2 < VEC ? k + 2 : k] = v.z;
+        w[k + 3 < VEC ? k + 3 : k] = v.w;
+      }
+    } else {
+      const uint32_t off = ((uint32_t)row * (uint32_t)a.g + VEC * c) * 4u;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0);
+    }
+  }
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
     if (CODEC == KVECC_CODEC_H84) {
       const uint8_t *p = reinterpret_cast<const uint8_t *>(cache) + row * a.d + 4 * VEC * c;
@@ -112,6 +142,15 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // sum_e q[e] * v[e] as packed FMAs (v_pk_fma_f32) into two independent lanes
 template <int E>
 __device__ __forceinline__ float dot(const float *q, const float *v) {
+  if (!KVECC_ATTN_PK) {
+    float a = 0.0f, b = 0.0f;
+#pragma unroll
+    for (int e = 0; e < E; e += 2) {
+      a = fmaf(q[e], v[e], a);
+      if (e + 1 < E) b = fmaf(q[e + 1], v[e + 1], b);
+    }
+    return a + b;
+  }
   f32x2 s = {0.0f, 0.0f};
 #pragma unroll
   for (int e = 0; e + 1 < E; e += 2) s = __builtin_elementwise_fma(f32x2{q[e], q[e + 1]}, f32x2{v[e], v[e + 1]}, s);
@@ -122,6 +161,11 @@ __device__ __forceinline__ float dot(const float *q, const float *v) {
 // acc[e] += p * v[e] as packed FMAs
 template <int E>
 __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
+  if (!KVECC_ATTN_PK) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = fmaf(p, v[e], acc[e]);
+    return;
+  }
 #pragma unroll
   for (int e = 0; e + 1 < E; e += 2) {
     const f32x2 r = __builtin_elementwise_fma(f32x2{p, p}, f32x2{v[e], v[e + 1]}, f32x2{acc[e], acc[e + 1]});
@@ -131,7 +175,7 @@ __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
   if (E % 2) acc[E - 1] = fmaf(p, v[E - 1], acc[E - 1]);
 }
 
-template <typename T, int CODEC, int VEC, int W>
+template <typename T, int CODEC, int VEC, int W, bool BUF>
 __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
@@ -206,6 +250,15 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   }
   __syncthreads();
 
+  // buffer descriptors (BUF kernels; dead code otherwise)
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.k_cache), 0, (int)a.cache_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t vrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.v_cache), 0, (int)a.cache_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t ksrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.k_scales), 0, (int)a.scale_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t vsrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v_scales), 0, (int)a.scale_bytes, kRsrcWord3);
   // ---- one pass: kUnroll K and V rows in flight per lane, online softmax per group
   float m = -INFINITY, l = 0.0f, acc[E];
   float psum = 0.0f;  // sum of p * v_scale, for the kOffset fold of the V sums
@@ -220,10 +273,17 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       const int32_t r = rows[i0 + u * TP];
       ok[u] = r >= 0;
       const int64_t row = ok[u] ? r : 0;
-      kc[u].load(a, a.k_cache, row, cs);
-      vc[u].load(a, a.v_cache, row, cs);
-      ks[u] = a.k_scales[row];
-      vs[u] = a.v_scales[row];
+      if (BUF) {
+        kc[u].load_buf(a, krs, (int32_t)row, cs);
+        vc[u].load_buf(a, vrs, (int32_t)row, cs);
+        ks[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, (uint32_t)row * 4u, 0, 0));
+        vs[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, (uint32_t)row * 4u, 0, 0));
+      } else {
+        kc[u].load(a, a.k_cache, row, cs);
+        vc[u].load(a, a.v_cache, row, cs);
+        ks[u] = a.k_scales[row];
+        vs[u] = a.v_scales[row];
+      }
     }
     float sc[kUnroll];
     float mn = m;
@@ -341,13 +401,13 @@ static int pow2_at_least(int64_t x) {
   return w;
 }
 
-template <typename T, int CODEC, int VEC>
-static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
+template <typename T, int CODEC, int VEC, bool BUF>
+static int launch_split_w(const AttnArgs &a, dim3 grid, hipStream_t st) {
   const int w = pow2_at_least((a.g + VEC - 1) / VEC);
   switch (w) {
 #define KVECC_ATTN_CASE(WW)                                                                       \
   case WW:                                                                                        \
-    KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, WW>), grid, dim3(kBlock), 0, st, a); \
+    KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, WW, BUF>), grid, dim3(kBlock), 0, st, a); \
     return KVECC_OK;
     KVECC_ATTN_CASE(1)
     KVECC_ATTN_CASE(2)
@@ -361,6 +421,12 @@ static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
       return set_error(KVECC_EINVAL, "paged_attention: %lld lane chunks per token row > 64",
                        (long long)((a.g + VEC - 1) / VEC));
   }
+}
+
+template <typename T, int CODEC, int VEC>
+static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
+  return a.cache_bytes ? launch_split_w<T, CODEC, VEC, true>(a, grid, st)
+                       : launch_split_w<T, CODEC, VEC, false>(a, grid, st);
 }
 
 template <typename T, int CODEC>
@@ -462,6 +528,13 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   if (a.nsplit > kMaxSplits)
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
   a.sm_scale = sm_scale;
+  {
+    const int64_t rows_total = num_blocks * num_layers * kv_heads * block_size;
+    const int64_t cb = rows_total * (codec == KVECC_CODEC_H84 ? head_dim : 4 * a.g);
+    const bool fits = cb <= 0xFFFFFFFFLL && rows_total * 4 <= 0xFFFFFFFFLL;
+    a.cache_bytes = fits ? (uint32_t)cb : 0u;  // 0 selects the 64-bit-addressed kernels
+    a.scale_bytes = fits ? (uint32_t)(rows_total * 4) : 0u;
+  }
   a.par = a.cor = nullptr;
   if (codec == KVECC_CODEC_GOLAY) {
     a.par = golay_parity_table_dev();

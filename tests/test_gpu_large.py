@@ -128,3 +128,47 @@ def test_fused_quantize_dequant_past_4g(gpu, oracle):
     ref, _ = oracle.decode_dequant_h84(oracle.hamming84_encode(oq), os_)
     assert ops.read_stats(st) == [0, 0]
     assert torch.equal(out[sample].cpu(), torch.from_numpy(ref).to(torch.float16))
+
+
+@pytest.mark.parametrize("codec", ["hamming84", "golay"])
+def test_paged_attention_cache_past_4g(gpu, codec):
+    """Caches over 4 GiB take the 64-bit-addressed attention kernels (smaller
+    ones use 32-bit buffer offsets).  The sequence's blocks sit past the 4 GiB
+    mark; the result must equal the same blocks copied into a small cache,
+    which runs the buffer-load kernels (~9 GB of HBM)."""
+    import math
+    from kvecc import ops
+    heads, d, bs, ctx, batch = 8, 128, 16, 1000, 2
+    per = d if codec == "hamming84" else (d + 2) // 3
+    cdt = torch.uint8 if codec == "hamming84" else torch.int32
+    row_bytes = heads * bs * per * (1 if codec == "hamming84" else 4)
+    num_blocks = (1 << 32) // row_bytes + 200                    # > 4 GiB per cache
+    nb = (ctx + bs - 1) // bs
+    g = torch.Generator(device=gpu).manual_seed(5)
+    hi = 256 if codec == "hamming84" else 1 << 24
+    used = torch.arange(num_blocks - batch * nb, num_blocks, device=gpu)   # the far end
+    big_k = torch.zeros(num_blocks, 1, heads, bs * per, dtype=cdt, device=gpu)
+    big_v = torch.zeros_like(big_k)
+    small_k = torch.randint(0, hi, (batch * nb, 1, heads, bs * per), dtype=cdt, device=gpu, generator=g)
+    small_v = torch.randint(0, hi, small_k.shape, dtype=cdt, device=gpu, generator=g)
+    big_k[used] = small_k
+    big_v[used] = small_v
+    ks_small = torch.rand(batch * nb, 1, heads, bs, device=gpu, generator=g) + 0.1
+    vs_small = torch.rand_like(ks_small) + 0.1
+    ks_big = torch.zeros(num_blocks, 1, heads, bs, device=gpu)
+    vs_big = torch.zeros_like(ks_big)
+    ks_big[used] = ks_small
+    vs_big[used] = vs_small
+    perm = torch.randperm(batch * nb, device=gpu, generator=g).to(torch.int32).view(batch, nb)
+    lens = torch.tensor([ctx, ctx - 37], dtype=torch.int32, device=gpu)
+    q = torch.randn(batch, heads, d, device=gpu, generator=g).half()
+    outs = []
+    for kc, vc, ks, vs, table in ((big_k, big_v, ks_big, vs_big, perm + (num_blocks - batch * nb)),
+                                  (small_k, small_v, ks_small, vs_small, perm)):
+        out = torch.empty_like(q)
+        ops.paged_attention_into(q, kc, vc, table.contiguous(), lens, ks, vs, out, 0, bs,
+                                 1 / math.sqrt(d), codec, ctx)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
