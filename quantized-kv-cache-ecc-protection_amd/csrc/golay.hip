@@ -28,8 +28,24 @@
 
 namespace kvecc {
 
-constexpr int kGroups = 2;                          // 4-codeword groups per lane per tile
-constexpr int kDecBlock = 512, kEncBlock = 1024;    // threads per workgroup
+// geometry (A/B knobs: tools/exp/run_golay_geom.py)
+#ifndef KVECC_GOLAY_GROUPS
+#define KVECC_GOLAY_GROUPS 2
+#endif
+#ifndef KVECC_GOLAY_DEC_BLOCK
+#define KVECC_GOLAY_DEC_BLOCK 512
+#endif
+#ifndef KVECC_GOLAY_ENC_BLOCK
+#define KVECC_GOLAY_ENC_BLOCK 1024
+#endif
+#ifndef KVECC_GOLAY_DEC_PER_CU
+#define KVECC_GOLAY_DEC_PER_CU 32
+#endif
+#ifndef KVECC_GOLAY_ENC_PER_CU
+#define KVECC_GOLAY_ENC_PER_CU 16
+#endif
+constexpr int kGroups = KVECC_GOLAY_GROUPS;         // 4-codeword groups per lane per tile
+constexpr int kDecBlock = KVECC_GOLAY_DEC_BLOCK, kEncBlock = KVECC_GOLAY_ENC_BLOCK;  // threads per workgroup
 constexpr int kDecTile = kDecBlock * kGroups * 4;   // 4096 codewords
 constexpr int kEncTile = kEncBlock * kGroups * 4;   // 8192 codewords
 constexpr int kWaveCw = kWave * kGroups * 4;        // codewords per wave per tile
@@ -462,7 +478,7 @@ KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, in
   if (aligned(triplets, 4) && aligned(codewords, 16)) {
     int64_t ntiles = m / kEncTile;
     if (ntiles > 0) {
-      unsigned g = grid_for(ntiles, 1, 16);  // <= 16 workgroups per CU, grid-strided
+      unsigned g = grid_for(ntiles, 1, KVECC_GOLAY_ENC_PER_CU);  // grid-strided
       KVECC_LAUNCH(golay_encode_kernel, dim3(g), dim3(kEncBlock), 0, st,
                          reinterpret_cast<const uint32_t *>(triplets),
                          reinterpret_cast<u32x4 *>(codewords), ntiles, par);
@@ -490,7 +506,7 @@ KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, ui
   if (aligned(codewords, 16) && aligned(triplets, 4) && (!counts || aligned(counts, 4))) {
     int64_t ntiles = m / kDecTile;
     if (ntiles > 0) {
-      unsigned g = grid_for(ntiles, 1, 32);  // <= 32 workgroups per CU, grid-strided
+      unsigned g = grid_for(ntiles, 1, KVECC_GOLAY_DEC_PER_CU);  // grid-strided
       auto c = reinterpret_cast<const u32x4 *>(codewords);
       auto t = reinterpret_cast<uint32_t *>(triplets);
       auto n = reinterpret_cast<uint32_t *>(counts);
