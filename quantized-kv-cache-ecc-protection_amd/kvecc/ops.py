@@ -430,6 +430,11 @@ class _EpochFlags:
         self._lock = threading.Lock()
 
     def next(self, device):
+        if torch.cuda.is_current_stream_capturing():
+            # a captured call replays with the epoch it was captured with, so
+            # stale words from the previous replay would read as "seen": give
+            # the graph its own words, zeroed by a captured fill on every replay
+            return torch.zeros(2, dtype=torch.int32, device=device), 1
         key = (device, torch.cuda.current_stream(device).cuda_stream)
         with self._lock:
             buf, epoch = self._bufs.get(key, (None, 0))

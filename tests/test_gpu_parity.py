@@ -540,3 +540,30 @@ def test_golay_rows_vs_cpu_backend(gpu, d, rows, offset):
     want = cpu_ops.golay_decode_rows(noisy, d, cst)
     assert torch.equal(out.cpu(), want)
     assert ops.read_stats(st) == cpu_ops.read_stats(cst)
+
+
+def test_interp_auto_in_a_hip_graph(gpu):
+    """A captured interpolate_double_errors replays correctly with inputs that
+    alternate between 'has doubles' and 'no doubles, q > 15' (the flag words
+    are re-zeroed inside the graph, not epoch-stamped)."""
+    import kvecc
+    q = torch.full((64, 48), 200, dtype=torch.uint8, device=gpu)
+    e = torch.zeros_like(q)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        kvecc.interpolate_double_errors(q, e, seq_dim=0)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = kvecc.interpolate_double_errors(q, e, seq_dim=0)
+    for has_double in (True, False, True, False):
+        e.zero_()
+        if has_double:
+            e[5, 7] = 2
+        graph.replay()
+        torch.cuda.synchronize()
+        if has_double:
+            assert int(out.max()) == 15
+        else:
+            assert torch.equal(out, q)
