@@ -52,7 +52,13 @@ enum {
 /* dtype codes for fused kernels */
 enum { KVECC_F32 = 0, KVECC_F16 = 1, KVECC_BF16 = 2 };
 /* codec codes for fused kernels */
-enum { KVECC_CODEC_NONE = 0, KVECC_CODEC_H74 = 1, KVECC_CODEC_H84 = 2, KVECC_CODEC_GOLAY = 3 };
+enum { KVECC_CODEC_NONE = 0, KVECC_CODEC_H74 = 1, KVECC_CODEC_H84 = 2, KVECC_CODEC_GOLAY = 3,
+       /* shim caches only (kvecc_shim_write / kvecc_shim_read and the cpu twins):
+        * Golay(24,12) codewords stored as 3 little-endian bytes, a token row of
+        * g = ceil(d/3) codewords padded to KVECC_GOLAY_PACKED_ROW(g) bytes --
+        * 132 B instead of the reference's 172 B (int32) at d = 128 */
+       KVECC_CODEC_GOLAY_PACKED = 4 };
+#define KVECC_GOLAY_PACKED_ROW(g) ((3 * (g) + 3) / 4 * 4)
 
 /* Row scale rule of the INT4 quantizer.  The reference computes
  * `abs_max / 7.0` with a Python-scalar divisor (paged_cache_ecc.py:330); torch
@@ -220,7 +226,8 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
  * codeword as ecc_shim.py:555-560) and stored into the paged caches -- only the
  * last batch, which is what the reference's same-slot writes leave behind.
  * Caches: [blocks, num_layers, hkv, block_size, P] with P = d (uint8) or
- * ceil(d/3) (int32, Golay per-head padding); scales fp32 [blocks, num_layers,
+ * ceil(d/3) (int32, Golay per-head padding), or KVECC_GOLAY_PACKED_ROW(ceil(d/3))
+ * bytes for KVECC_CODEC_GOLAY_PACKED (not a reference layout); scales fp32 [blocks, num_layers,
  * hkv, block_size]; token pos lives in physical block block_table[pos / block_size]
  * (device int32).  d <= 512. */
 KVECC_API int kvecc_shim_write(const void *k, const void *v, int x_dtype, int64_t batch,
@@ -264,7 +271,7 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
 /* attention_ecc.py:620-780 (paged_attention_ecc) + :265-427 (kernel): one query
  * token per sequence, query [batch, heads, head_dim] (q_dtype), caches as above
  * (codec H84: uint8, double errors keep their data; GOLAY: int32, uncorrectable
- * data kept), block_table [batch, max_blocks] int32 (-1 = no block, token
+ * data kept; GOLAY_PACKED: 3-byte codewords, rows of KVECC_GOLAY_PACKED_ROW bytes), block_table [batch, max_blocks] int32 (-1 = no block, token
  * skipped), context_lens [batch] int32 (<= max_context_len; <= 0 means
  * max_blocks*block_size), out [batch, heads, head_dim] in q_dtype (0 for an empty
  * context).  Query head h reads cache head h / (heads / kv_heads).  `workspace`:

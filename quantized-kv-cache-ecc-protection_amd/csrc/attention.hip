@@ -49,6 +49,10 @@ constexpr int kH84Vec = KVECC_ATTN_H84_VEC, kGolayVec = KVECC_ATTN_GOLAY_VEC;
 #define KVECC_ATTN_PK 1
 #endif
 constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
+// Packed Golay caches (KVECC_CODEC_GOLAY_PACKED, 3-byte codewords): a lane owns
+// 4 codewords = 12 bytes = 3 aligned dwords of its token row
+constexpr int kGolayPackedVec = 4;
+constexpr bool is_golay(int codec) { return codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED; }
 
 struct AttnArgs {
   const void *q;  // [B, H, D]
@@ -59,6 +63,7 @@ struct AttnArgs {
   float *ws;  // [B*H, nsplit, D + 2]: m, l, acc[D]
   void *out;  // [B, H, D]
   int64_t heads, kv_heads, d, g;  // g = codewords per token row
+  uint32_t rowb;                  // packed Golay: bytes per token row (KVECC_GOLAY_PACKED_ROW(g))
   int64_t layers, layer, bs, max_blocks, nsplit, split;
   uint32_t cache_bytes, scale_bytes;  // buffer-load bounds (BUF kernels)
   float sm_scale;
@@ -73,11 +78,11 @@ struct Chunk {
   static constexpr int E = CODEC == KVECC_CODEC_H84 ? 4 * VEC : 3 * VEC;
   // decode() returns (n - 8) + kOffset: the Golay path skips the subtraction
   // per element and the kernel folds -8 * kOffset into the sums instead
-  static constexpr float kOffset = CODEC == KVECC_CODEC_GOLAY ? 8.0f : 0.0f;
+  static constexpr float kOffset = is_golay(CODEC) ? 8.0f : 0.0f;
   uint32_t w[VEC];
   __device__ __forceinline__ void load_buf(const AttnArgs &a, __amdgpu_buffer_rsrc_t rs, int32_t row,
                                            int c) {
-    if (CODEC == KVECC_CODEC_H84) {
+    if constexpr (CODEC == KVECC_CODEC_H84) {
       const uint32_t off = (uint32_t)row * (uint32_t)a.d + 4u * VEC * c;
 #pragma unroll
       for (int k = 0; k < VEC; k += 4) {
@@ -87,6 +92,12 @@ struct Chunk {
         w[k + 2 < VEC ? k + 2 : k] = v.z;
         w[k + 3 < VEC ? k + 3 : k] = v.w;
       }
+    } else if constexpr (CODEC == KVECC_CODEC_GOLAY_PACKED) {
+      static_assert(CODEC != KVECC_CODEC_GOLAY_PACKED || VEC == 4, "packed lanes own 4 codewords");
+      // past the row's end: a neighbour row's bytes (masked by q = 0) or 0
+      const uint32_t off = (uint32_t)row * a.rowb + 12u * c;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+      unpack3(v[0], v[1], v[2]);
     } else {
       const uint32_t off = ((uint32_t)row * (uint32_t)a.g + VEC * c) * 4u;
 #pragma unroll
@@ -94,7 +105,7 @@ struct Chunk {
     }
   }
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
-    if (CODEC == KVECC_CODEC_H84) {
+    if constexpr (CODEC == KVECC_CODEC_H84) {
       const uint8_t *p = reinterpret_cast<const uint8_t *>(cache) + row * a.d + 4 * VEC * c;
       if (VEC % 4 == 0) {
 #pragma unroll
@@ -109,17 +120,28 @@ struct Chunk {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) w[k] = reinterpret_cast<const uint32_t *>(p)[k];
       }
+    } else if constexpr (CODEC == KVECC_CODEC_GOLAY_PACKED) {
+      const uint32_t *p = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(cache) + row * a.rowb);
+      const int last = (int)(a.rowb / 4) - 1;  // clamp inside the row
+      unpack3(p[min(3 * c, last)], p[min(3 * c + 1, last)], p[min(3 * c + 2, last)]);
     } else {
       const int32_t *p = reinterpret_cast<const int32_t *>(cache) + row * a.g;
 #pragma unroll
       for (int k = 0; k < VEC; ++k) w[k] = (uint32_t)p[min<int64_t>(VEC * c + k, a.g - 1)];
     }
   }
+  // 4 little-endian 3-byte codewords from 3 dwords (golay_decode1 ignores bits 24-31)
+  __device__ __forceinline__ void unpack3(uint32_t d0, uint32_t d1, uint32_t d2) {
+    w[0] = d0;
+    w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbyte(d1, d0, 3);
+    w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbyte(d2, d1, 2);
+    w[3 < VEC ? 3 : 0] = d2 >> 8;
+  }
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
   // correction tables (uncorrectable words keep their data, as golay_decode)
   __device__ __forceinline__ void decode(const float *lut, const uint16_t *gtab, float *v) const {
-    if (CODEC == KVECC_CODEC_H84) {
+    if constexpr (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
 #pragma unroll
@@ -187,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   __shared__ float gml[2][TP];             // per-group running max / sum
   __shared__ float lut[256];               // H(8,4): codeword byte -> data - 8
   // Golay: parity[4096] then correct[4096] (16 KiB) copied from the device tables
-  __shared__ __attribute__((aligned(16))) uint16_t gtab[CODEC == KVECC_CODEC_GOLAY ? 8192 : 8];
+  __shared__ __attribute__((aligned(16))) uint16_t gtab[is_golay(CODEC) ? 8192 : 8];
 
   const int64_t bh = blockIdx.y;
   const int64_t b = bh / a.heads, h = bh % a.heads;
@@ -224,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       rows[i] = row;
     }
   }
-  if (CODEC == KVECC_CODEC_GOLAY) {
+  if (is_golay(CODEC)) {
     const u32x4 *src0 = reinterpret_cast<const u32x4 *>(a.par);
     const u32x4 *src1 = reinterpret_cast<const u32x4 *>(a.cor);
     u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
@@ -433,17 +455,30 @@ template <typename T, int CODEC>
 static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
   dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads));
   int rc;
-  if (CODEC == KVECC_CODEC_H84 && a.d % (4 * kH84Vec) == 0)
-    rc = launch_split<T, CODEC, kH84Vec>(a, grid, st);  // 16-byte loads, 16 codewords per lane
-  else if (CODEC == KVECC_CODEC_H84 && a.d % 16 == 0)
-    rc = launch_split<T, CODEC, 4>(a, grid, st);
-  else if (CODEC == KVECC_CODEC_GOLAY)
+  if constexpr (CODEC == KVECC_CODEC_H84) {
+    if (a.d % (4 * kH84Vec) == 0)
+      rc = launch_split<T, CODEC, kH84Vec>(a, grid, st);  // 16-byte loads, 16 codewords per lane
+    else if (a.d % 16 == 0)
+      rc = launch_split<T, CODEC, 4>(a, grid, st);
+    else
+      rc = launch_split<T, CODEC, 1>(a, grid, st);
+  } else if constexpr (CODEC == KVECC_CODEC_GOLAY) {
     rc = launch_split<T, CODEC, kGolayVec>(a, grid, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
-  else
-    rc = launch_split<T, CODEC, 1>(a, grid, st);
+  } else {
+    rc = launch_split<T, CODEC, kGolayPackedVec>(a, grid, st);  // 4 codewords per lane: 43 -> 11 of 16
+  }
   if (rc != KVECC_OK) return rc;
   KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
   return KVECC_OK;
+}
+
+template <typename T>
+static int launch_codec(int codec, const AttnArgs &a, int64_t batch, hipStream_t st) {
+  switch (codec) {
+    case KVECC_CODEC_H84: return launch_attn<T, KVECC_CODEC_H84>(a, batch, st);
+    case KVECC_CODEC_GOLAY: return launch_attn<T, KVECC_CODEC_GOLAY>(a, batch, st);
+    default: return launch_attn<T, KVECC_CODEC_GOLAY_PACKED>(a, batch, st);
+  }
 }
 
 // tokens per workgroup: the largest power of two <= kMaxSplit that still gives
@@ -489,7 +524,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
                      (long long)heads, (long long)kv_heads);
   if (head_dim < 1 || head_dim > kAttnMaxD)
     return set_error(KVECC_EINVAL, "paged_attention: head_dim %lld not in [1, %d]", (long long)head_dim, kAttnMaxD);
-  if (codec != KVECC_CODEC_H84 && codec != KVECC_CODEC_GOLAY)
+  if (codec != KVECC_CODEC_H84 && codec != KVECC_CODEC_GOLAY && codec != KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "paged_attention: codec %d (hamming84 or golay only)", codec);
   if (codec == KVECC_CODEC_H84 && head_dim % 4 != 0)
     return set_error(KVECC_EINVAL, "paged_attention: hamming84 head_dim must be a multiple of 4");
@@ -519,6 +554,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.kv_heads = kv_heads;
   a.d = head_dim;
   a.g = codec == KVECC_CODEC_H84 ? head_dim / 4 : (head_dim + 2) / 3;
+  a.rowb = (uint32_t)KVECC_GOLAY_PACKED_ROW(a.g);
   a.layers = num_layers;
   a.layer = layer;
   a.bs = block_size;
@@ -530,13 +566,15 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.sm_scale = sm_scale;
   {
     const int64_t rows_total = num_blocks * num_layers * kv_heads * block_size;
-    const int64_t cb = rows_total * (codec == KVECC_CODEC_H84 ? head_dim : 4 * a.g);
+    const int64_t cb = rows_total * (codec == KVECC_CODEC_H84            ? head_dim
+                                     : codec == KVECC_CODEC_GOLAY_PACKED ? (int64_t)a.rowb
+                                                                         : 4 * a.g);
     const bool fits = cb <= 0xFFFFFFFFLL && rows_total * 4 <= 0xFFFFFFFFLL;
     a.cache_bytes = fits ? (uint32_t)cb : 0u;  // 0 selects the 64-bit-addressed kernels
     a.scale_bytes = fits ? (uint32_t)(rows_total * 4) : 0u;
   }
   a.par = a.cor = nullptr;
-  if (codec == KVECC_CODEC_GOLAY) {
+  if (codec != KVECC_CODEC_H84) {
     a.par = golay_parity_table_dev();
     a.cor = golay_correct_table_dev();
     if (!a.par || !a.cor) return KVECC_EHIP;
@@ -544,18 +582,9 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   hipStream_t st = as_stream(stream);
   int rc;
   switch (q_dtype) {
-    case KVECC_F32:
-      rc = codec == KVECC_CODEC_H84 ? launch_attn<float, KVECC_CODEC_H84>(a, batch, st)
-                                    : launch_attn<float, KVECC_CODEC_GOLAY>(a, batch, st);
-      break;
-    case KVECC_F16:
-      rc = codec == KVECC_CODEC_H84 ? launch_attn<__half, KVECC_CODEC_H84>(a, batch, st)
-                                    : launch_attn<__half, KVECC_CODEC_GOLAY>(a, batch, st);
-      break;
-    case KVECC_BF16:
-      rc = codec == KVECC_CODEC_H84 ? launch_attn<__hip_bfloat16, KVECC_CODEC_H84>(a, batch, st)
-                                    : launch_attn<__hip_bfloat16, KVECC_CODEC_GOLAY>(a, batch, st);
-      break;
+    case KVECC_F32: rc = launch_codec<float>(codec, a, batch, st); break;
+    case KVECC_F16: rc = launch_codec<__half>(codec, a, batch, st); break;
+    case KVECC_BF16: rc = launch_codec<__hip_bfloat16>(codec, a, batch, st); break;
     default: return set_error(KVECC_EINVAL, "paged_attention: bad dtype %d", q_dtype);
   }
   if (rc != KVECC_OK) return rc;

@@ -359,7 +359,7 @@ KV_HD uint32_t philox_flip_mask(uint32_t key_base, uint32_t ctr, uint32_t thr, i
   const uint32_t k1 = (uint32_t)((int32_t)key_base >> 31);
   const bool same_sign = k1 == (uint32_t)((int32_t)(key_base + (uint32_t)(nb - 1)) >> 31);
   uint32_t m = 0;
-  if (NB >= 0) {
+  if constexpr (NB >= 0) {
     if (same_sign) {
 #pragma unroll
       for (int b = NB - 1; b >= 0; --b)

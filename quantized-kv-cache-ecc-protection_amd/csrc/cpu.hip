@@ -592,7 +592,7 @@ KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, in
   if (batch < 0 || seq < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_shim_write: negative size");
   if (batch == 0 || seq == 0 || hkv == 0) return KVECC_OK;
   if (d < 1) return set_error(KVECC_EINVAL, "cpu_shim_write: empty rows");
-  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "cpu_shim_write: bad codec %d", codec);
   if (scale_rule != KVECC_SCALE_DIV7 && scale_rule != KVECC_SCALE_MUL_INV7)
     return set_error(KVECC_EINVAL, "cpu_shim_write: bad scale rule %d", scale_rule);
@@ -602,7 +602,8 @@ KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, in
     return set_error(KVECC_EINVAL, "cpu_shim_write: bad cache geometry");
   if (!k || !v || !k_cache || !v_cache || !k_scales || !v_scales || !block_table)
     return set_error(KVECC_EINVAL, "cpu_shim_write: null pointer");
-  const bool golay = codec == KVECC_CODEC_GOLAY;
+  const bool packed = codec == KVECC_CODEC_GOLAY_PACKED;
+  const bool golay = codec == KVECC_CODEC_GOLAY || packed;
   const int64_t g = golay ? (d + 2) / 3 : d;
   const uint32_t rowmul = (uint32_t)((uint64_t)g * (uint64_t)n_bits);
   const uint32_t thr = kvecc_ber_threshold(ber);
@@ -636,12 +637,19 @@ KVECC_API int kvecc_cpu_shim_write(const void *k, const void *v, int x_dtype, in
       } else {
         std::fill(nib.begin(), nib.end(), 0);
         for (int64_t j = 0; j < d; ++j) nib[j] = (uint8_t)quantize_nibble(load_x(x, x_dtype, r * d + j), scale);
-        int32_t *c = reinterpret_cast<int32_t *>(side ? v_cache : k_cache) + slot * g;
+        void *cache = side ? v_cache : k_cache;
         for (int64_t q = 0; q < g; ++q) {
           const uint32_t dw = golay_pack(nib[3 * q], nib[3 * q + 1], nib[3 * q + 2]);
           uint32_t cw = dw | golay_parity12(dw) << 12;
           if (inj) cw ^= philox_flip_mask<-1>(key0 + (uint32_t)q * (uint32_t)n_bits, (uint32_t)q, thr, nb);
-          c[q] = (int32_t)cw;
+          if (packed) {
+            uint8_t *c = reinterpret_cast<uint8_t *>(cache) + slot * KVECC_GOLAY_PACKED_ROW(g) + 3 * q;
+            c[0] = (uint8_t)cw;
+            c[1] = (uint8_t)(cw >> 8);
+            c[2] = (uint8_t)(cw >> 16);
+          } else {
+            reinterpret_cast<int32_t *>(cache)[slot * g + q] = (int32_t)cw;
+          }
         }
       }
     }
@@ -656,7 +664,7 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
                                   int out_dtype, uint64_t *stats, int threads) {
   if (ctx < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "cpu_shim_read: negative size");
   if (ctx == 0 || hkv == 0 || d == 0) return KVECC_OK;
-  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "cpu_shim_read: bad codec %d", codec);
   if (interp && codec != KVECC_CODEC_H84)
     return set_error(KVECC_EINVAL, "cpu_shim_read: interpolation needs the hamming84 codec");
@@ -673,7 +681,8 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
     return true;
   }();
   (void)ready;
-  const bool golay = codec == KVECC_CODEC_GOLAY;
+  const bool packed = codec == KVECC_CODEC_GOLAY_PACKED;
+  const bool golay = codec == KVECC_CODEC_GOLAY || packed;
   const int64_t g = golay ? (d + 2) / 3 : d;
   auto slot_of = [&](int64_t l, int64_t h) {
     return (((int64_t)block_table[l / block_size] * num_layers + layer) * hkv + h) * block_size +
@@ -693,10 +702,16 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
       void *out = side ? v_out : k_out;
       const int64_t o = (h * ctx + l) * d;
       if (golay) {
-        const int32_t *c = reinterpret_cast<const int32_t *>(side ? v_cache : k_cache) + slot * g;
+        const void *cache = side ? v_cache : k_cache;
         for (int64_t q = 0; q < g; ++q) {
-          uint32_t cnt;
-          const uint32_t dw = golay_decode1((uint32_t)c[q], tab, tab + 4096, cnt);
+          uint32_t cnt, w;
+          if (packed) {
+            const uint8_t *c = reinterpret_cast<const uint8_t *>(cache) + slot * KVECC_GOLAY_PACKED_ROW(g) + 3 * q;
+            w = (uint32_t)c[0] | (uint32_t)c[1] << 8 | (uint32_t)c[2] << 16;
+          } else {
+            w = (uint32_t)reinterpret_cast<const int32_t *>(cache)[slot * g + q];
+          }
+          const uint32_t dw = golay_decode1(w, tab, tab + 4096, cnt);
           bits += cnt & 3u;
           unc += cnt >> 2;
           for (int64_t u = 0; u < 3 && 3 * q + u < d; ++u)
@@ -748,7 +763,7 @@ KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const vo
   if (kv_heads < 1 || heads % kv_heads != 0)
     return set_error(KVECC_EINVAL, "cpu_paged_attention: heads not a multiple of kv heads");
   if (head_dim < 1) return set_error(KVECC_EINVAL, "cpu_paged_attention: empty head_dim");
-  if (codec != KVECC_CODEC_H84 && codec != KVECC_CODEC_GOLAY)
+  if (codec != KVECC_CODEC_H84 && codec != KVECC_CODEC_GOLAY && codec != KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "cpu_paged_attention: codec %d (hamming84 or golay only)", codec);
   if (q_dtype < KVECC_F32 || q_dtype > KVECC_BF16)
     return set_error(KVECC_EINVAL, "cpu_paged_attention: bad dtype %d", q_dtype);
@@ -764,17 +779,23 @@ KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const vo
     return true;
   }();
   (void)ready;
-  const bool golay = codec == KVECC_CODEC_GOLAY;
+  const bool packed = codec == KVECC_CODEC_GOLAY_PACKED;
+  const bool golay = codec == KVECC_CODEC_GOLAY || packed;
   const int64_t g = golay ? (head_dim + 2) / 3 : head_dim;
   const int64_t groups = heads / kv_heads;
   parallel_for(batch * heads, threads, 1, [&](int64_t b0, int64_t e0, int) {
     std::vector<float> q(head_dim), kv(head_dim), acc(head_dim);
     auto decode_row = [&](const void *cache, int64_t srow, float s) {
       if (golay) {
-        const int32_t *c = reinterpret_cast<const int32_t *>(cache) + srow * g;
         for (int64_t k = 0; k < g; ++k) {
-          uint32_t cnt;
-          const uint32_t dw = golay_decode1((uint32_t)c[k], tab, tab + 4096, cnt);
+          uint32_t cnt, w;
+          if (packed) {
+            const uint8_t *c = reinterpret_cast<const uint8_t *>(cache) + srow * KVECC_GOLAY_PACKED_ROW(g) + 3 * k;
+            w = (uint32_t)c[0] | (uint32_t)c[1] << 8 | (uint32_t)c[2] << 16;
+          } else {
+            w = (uint32_t)reinterpret_cast<const int32_t *>(cache)[srow * g + k];
+          }
+          const uint32_t dw = golay_decode1(w, tab, tab + 4096, cnt);
           for (int64_t u = 0; u < 3 && 3 * k + u < head_dim; ++u)
             kv[3 * k + u] = ((float)(dw >> (4 * u) & 0xFu) - 8.0f) * s;
         }

@@ -31,6 +31,7 @@ struct ShimGeom {
   // 32-bit index math (the host checks every count fits): 64-bit division is
   // ~100 instructions on gfx950
   uint32_t hkv, d, g;  // g = codewords per token row: d, or ceil(d/3) for Golay
+                       // (packed Golay rows are KVECC_GOLAY_PACKED_ROW(g) bytes)
   uint32_t layers, bs, layer;
   __device__ __forceinline__ int64_t slot(uint32_t pos, uint32_t h) const {
     const uint32_t lb = pos / bs;
@@ -90,7 +91,8 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
     return recip ? nibble_of_quotient(div_recip(x, scale, inv)) : quantize_nibble(x, scale);
   };
 
-  if (CODEC != KVECC_CODEC_GOLAY) {
+  constexpr bool kGolay = CODEC == KVECC_CODEC_GOLAY || CODEC == KVECC_CODEC_GOLAY_PACKED;
+  if (!kGolay) {
     if (!live) return;
     uint8_t *c = reinterpret_cast<uint8_t *>(a.cache[side]) + slot * geo.g;
 #pragma unroll
@@ -115,13 +117,19 @@ __global__ __launch_bounds__(kBlock) void shim_write_kernel(ShimWriteArgs a) {
   }
   __syncthreads();
   if (!live) return;
-  int32_t *c = reinterpret_cast<int32_t *>(a.cache[side]) + slot * geo.g;
   for (uint32_t k = lane; k < geo.g; k += kWave) {
     const uint32_t dw = golay_pack(nib[w][3 * k], nib[w][3 * k + 1], nib[w][3 * k + 2]);
     uint32_t cw = dw | golay_parity12(dw) << 12;
     if (a.inject)
       cw ^= philox_flip_mask<NB>(key0 + k * a.nbits, k, a.thr, a.nb_eff);
-    c[k] = (int32_t)cw;
+    if (CODEC == KVECC_CODEC_GOLAY_PACKED) {
+      uint8_t *c = reinterpret_cast<uint8_t *>(a.cache[side]) + slot * KVECC_GOLAY_PACKED_ROW(geo.g) + 3 * k;
+      c[0] = (uint8_t)cw;
+      c[1] = (uint8_t)(cw >> 8);
+      c[2] = (uint8_t)(cw >> 16);
+    } else {
+      reinterpret_cast<int32_t *>(a.cache[side])[slot * geo.g + k] = (int32_t)cw;
+    }
   }
 }
 
@@ -179,8 +187,8 @@ __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a)
   if (STATS) flush_stats2(a.stats, n1, n2);
 }
 
-// Golay: one lane per codeword of a token row
-template <typename TO, bool STATS>
+// Golay: one lane per codeword of a token row (PACKED: 3-byte codewords)
+template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a) {
   const ShimGeom &geo = a.geo;
   const uint32_t per_side = geo.hkv * a.ctx * geo.g;
@@ -191,7 +199,14 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
     const uint32_t hl = t / geo.g, k = t - hl * geo.g;
     const uint32_t h = hl / a.ctx, l = hl - h * a.ctx;
     const int64_t slot = geo.slot(l, h);
-    const uint32_t w = (uint32_t)reinterpret_cast<const int32_t *>(a.cache[side])[slot * geo.g + k];
+    uint32_t w;
+    if (PACKED) {
+      const uint8_t *c = reinterpret_cast<const uint8_t *>(a.cache[side]) +
+                         slot * KVECC_GOLAY_PACKED_ROW(geo.g) + 3 * k;
+      w = (uint32_t)c[0] | (uint32_t)c[1] << 8 | (uint32_t)c[2] << 16;
+    } else {
+      w = (uint32_t)reinterpret_cast<const int32_t *>(a.cache[side])[slot * geo.g + k];
+    }
     uint32_t cnt;
     const uint32_t dw = golay_decode1(w, a.par, a.cor, cnt);
     bits += cnt & 3u;
@@ -208,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 
 template <typename T, int CODEC>
 static void launch_write_nb(const ShimWriteArgs &a, unsigned grid, hipStream_t st) {
-  constexpr int NB = CODEC == KVECC_CODEC_GOLAY ? 24
+  constexpr int NB = CODEC == KVECC_CODEC_GOLAY || CODEC == KVECC_CODEC_GOLAY_PACKED ? 24
                      : CODEC == KVECC_CODEC_H84 ? 8
                      : CODEC == KVECC_CODEC_H74 ? 7
                                                 : 4;
@@ -224,6 +239,7 @@ static void launch_write(int codec, const ShimWriteArgs &a, unsigned grid, hipSt
     case KVECC_CODEC_NONE: launch_write_nb<T, KVECC_CODEC_NONE>(a, grid, st); break;
     case KVECC_CODEC_H74: launch_write_nb<T, KVECC_CODEC_H74>(a, grid, st); break;
     case KVECC_CODEC_H84: launch_write_nb<T, KVECC_CODEC_H84>(a, grid, st); break;
+    case KVECC_CODEC_GOLAY_PACKED: launch_write_nb<T, KVECC_CODEC_GOLAY_PACKED>(a, grid, st); break;
     default: launch_write_nb<T, KVECC_CODEC_GOLAY>(a, grid, st); break;
   }
 }
@@ -238,12 +254,17 @@ static void launch_read_bytes(const ShimReadArgs &a, unsigned grid, hipStream_t 
 
 template <typename TO>
 static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_t st) {
-  if (codec == KVECC_CODEC_GOLAY) {
+  if (codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED) {
     const unsigned grid = grid_for(2 * a.geo.hkv * a.ctx * a.geo.g, kBlock);
-    if (a.stats)
-      KVECC_LAUNCH((shim_read_golay_kernel<TO, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    const bool pk = codec == KVECC_CODEC_GOLAY_PACKED;
+    if (a.stats && pk)
+      KVECC_LAUNCH((shim_read_golay_kernel<TO, true, true>), dim3(grid), dim3(kBlock), 0, st, a);
+    else if (a.stats)
+      KVECC_LAUNCH((shim_read_golay_kernel<TO, true, false>), dim3(grid), dim3(kBlock), 0, st, a);
+    else if (pk)
+      KVECC_LAUNCH((shim_read_golay_kernel<TO, false, true>), dim3(grid), dim3(kBlock), 0, st, a);
     else
-      KVECC_LAUNCH((shim_read_golay_kernel<TO, false>), dim3(grid), dim3(kBlock), 0, st, a);
+      KVECC_LAUNCH((shim_read_golay_kernel<TO, false, false>), dim3(grid), dim3(kBlock), 0, st, a);
     return;
   }
   const unsigned grid = grid_for(2 * a.geo.hkv * a.ctx * (a.geo.d / 4), kBlock);
@@ -274,8 +295,9 @@ static int shim_write_impl(const void *k, const void *v, const int64_t xb[2], co
   if (batch < 0 || seq < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_write: negative size");
   if (batch == 0 || seq == 0 || hkv == 0) return KVECC_OK;
   if (d < 1 || d > kMaxShimD) return set_error(KVECC_EINVAL, "shim_write: head_dim %lld not in [1, %d]", (long long)d, kMaxShimD);
-  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "shim_write: bad codec %d", codec);
+  const bool golay = codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED;
   if (scale_rule != KVECC_SCALE_DIV7 && scale_rule != KVECC_SCALE_MUL_INV7)
     return set_error(KVECC_EINVAL, "shim_write: bad scale rule %d", scale_rule);
   if (num_layers < 1 || block_size < 1 || layer < 0 || layer >= num_layers)
@@ -289,7 +311,7 @@ static int shim_write_impl(const void *k, const void *v, const int64_t xb[2], co
       return set_error(KVECC_EINVAL, "shim_write: negative stride or head stride < head_dim");
   ShimWriteArgs a;
   a.geo = {block_table, (uint32_t)hkv, (uint32_t)d,
-           (uint32_t)(codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d), (uint32_t)num_layers,
+           (uint32_t)(golay ? (d + 2) / 3 : d), (uint32_t)num_layers,
            (uint32_t)block_size, (uint32_t)layer};
   a.x[0] = k;
   a.x[1] = v;
@@ -311,7 +333,7 @@ static int shim_write_impl(const void *k, const void *v, const int64_t xb[2], co
   a.inject = inject != 0 && ber > 0.0f;
   a.scale_rule = scale_rule;
   // same bit-count clamps as the flat kernels (uint8 caches draw >= 1, <= 8 bits)
-  a.nb_eff = codec == KVECC_CODEC_GOLAY ? (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits))
+  a.nb_eff = golay ? (n_bits < 0 ? 0 : (n_bits > 24 ? 24 : n_bits))
                                         : (n_bits < 1 ? 1 : (n_bits > 8 ? 8 : n_bits));
   const int64_t waves = 2 * seq * hkv;
   const int64_t blocks = cdiv(waves, kWavesPerBlock);
@@ -362,9 +384,10 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
                               int out_dtype, uint64_t *stats, void *stream) {
   if (ctx < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_read: negative size");
   if (ctx == 0 || hkv == 0 || d == 0) return KVECC_OK;
-  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY)
+  if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "shim_read: bad codec %d", codec);
-  if (codec != KVECC_CODEC_GOLAY && d % 4 != 0)
+  const bool golay = codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED;
+  if (!golay && d % 4 != 0)
     return set_error(KVECC_EINVAL, "shim_read: head_dim %lld must be a multiple of 4", (long long)d);
   if (interp && codec != KVECC_CODEC_H84)
     return set_error(KVECC_EINVAL, "shim_read: interpolation needs the hamming84 codec");
@@ -376,7 +399,7 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
     return set_error(KVECC_EINVAL, "shim_read: sizes exceed 32-bit indexing");
   ShimReadArgs a;
   a.geo = {block_table, (uint32_t)hkv, (uint32_t)d,
-           (uint32_t)(codec == KVECC_CODEC_GOLAY ? (d + 2) / 3 : d), (uint32_t)num_layers,
+           (uint32_t)(golay ? (d + 2) / 3 : d), (uint32_t)num_layers,
            (uint32_t)block_size, (uint32_t)layer};
   a.cache[0] = k_cache;
   a.cache[1] = v_cache;
@@ -387,7 +410,7 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
   a.ctx = (uint32_t)ctx;
   a.stats = stats;
   a.par = a.cor = nullptr;
-  if (codec == KVECC_CODEC_GOLAY) {
+  if (golay) {
     a.par = golay_parity_table_dev();
     a.cor = golay_correct_table_dev();
     if (!a.par || !a.cor) return KVECC_EHIP;

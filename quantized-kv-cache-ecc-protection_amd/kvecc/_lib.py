@@ -96,6 +96,12 @@ _RESTYPE = {
 # dtype / codec codes (include/kvecc.h)
 F32, F16, BF16 = 0, 1, 2
 CODEC_NONE, CODEC_H74, CODEC_H84, CODEC_GOLAY = 0, 1, 2, 3
+CODEC_GOLAY_PACKED = 4  # shim caches only: 3-byte Golay codewords (kvecc.h)
+
+
+def golay_packed_row_bytes(g: int) -> int:
+    """KVECC_GOLAY_PACKED_ROW: bytes of a packed token row of g Golay codewords."""
+    return (3 * g + 3) // 4 * 4
 SCALE_DIV7, SCALE_MUL_INV7 = 0, 1
 # INT4 row-scale rules (kvecc.h KVECC_SCALE_*): the reference's `abs_max / 7.0`
 # (paged_cache_ecc.py:330) as torch computes it on CPU tensors ("div7", IEEE

@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ._lib import golay_packed_row_bytes
 from .backends import get_codec_backend
 
 try:  # optional, as in the reference (:54)
@@ -92,13 +93,17 @@ class ECCShimConfig:
     "mul_inv7" (absmax * RN(1/7), what the reference computes on GPU tensors),
     "div7" (IEEE division, the reference on CPU tensors) or None for the
     backend's device (kvecc.h KVECC_SCALE_*).
+    ``golay_storage`` is the Golay cache layout: "int32" (the reference's, one
+    int32 per codeword) or "packed" (3-byte codewords, token rows padded to 4
+    bytes: 132 instead of 172 B per row at head_dim 128).  "packed" needs the
+    fused write / read.
     """
 
     SUPPORTED_CODECS = {"fp16", "fp8", "int4", "hamming74", "hamming84", "golay"}
 
     def __init__(self, codec="hamming84", ber=0.0, block_size=16, num_blocks=256,
                  inject_errors=False, seed=42, use_interpolation=False, backend="hip",
-                 fused=True, scale_rule=None):
+                 fused=True, scale_rule=None, golay_storage="int32"):
         if codec not in self.SUPPORTED_CODECS:
             raise ValueError(f"Unsupported codec: '{codec}'. "
                              f"Supported codecs: {sorted(self.SUPPORTED_CODECS)}")
@@ -112,6 +117,11 @@ class ECCShimConfig:
         self.backend = backend
         self.fused = fused  # one-launch cache write / read (False: per-op kernels)
         self.scale_rule = scale_rule
+        if golay_storage not in ("int32", "packed"):
+            raise ValueError(f"golay_storage must be 'int32' or 'packed', not {golay_storage!r}")
+        if golay_storage == "packed" and not fused:
+            raise ValueError("golay_storage='packed' needs fused=True")
+        self.golay_storage = golay_storage
 
 
 class SimpleBlockManager:
@@ -119,12 +129,14 @@ class SimpleBlockManager:
 
     k_cache / v_cache: [num_blocks, num_layers, num_kv_heads, codewords_per_head]
     with codewords_per_head = block_size * head_dim (uint8 codewords, fp16,
-    fp8) or block_size * ceil(head_dim/3) (int32 Golay codewords);
+    fp8) or block_size * ceil(head_dim/3) (int32 Golay codewords), or with
+    golay_storage="packed" block_size * KVECC_GOLAY_PACKED_ROW(ceil(head_dim/3))
+    uint8 (3-byte Golay codewords, not a reference layout);
     k_scales / v_scales: fp32 [num_blocks, num_layers, num_kv_heads, block_size].
     """
 
     def __init__(self, num_blocks, block_size, num_layers, num_kv_heads, head_dim, device="cuda",
-                 codec="hamming84"):
+                 codec="hamming84", golay_storage="int32"):
         self.num_blocks = num_blocks
         self.block_size = block_size
         self.num_layers = num_layers
@@ -133,7 +145,13 @@ class SimpleBlockManager:
         self.device = device
         self.codec = codec
         self.needs_scales = codec not in ("fp16", "fp8")
-        if codec == "golay":
+        self.golay_packed = codec == "golay" and golay_storage == "packed"
+        # the codec name the fused shim kernels take (ops.SHIM_CODECS)
+        self.shim_codec = "golay_packed" if self.golay_packed else codec
+        if self.golay_packed:
+            self.values_per_head = block_size * golay_packed_row_bytes((head_dim + 2) // 3)
+            self.cache_dtype = torch.uint8
+        elif codec == "golay":
             self.values_per_head = block_size * ((head_dim + 2) // 3)
             self.cache_dtype = torch.int32
         else:
@@ -234,6 +252,9 @@ class ECCBackend:
         self.num_heads = num_heads
         self.num_kv_heads = manager.num_kv_heads
         self.head_dim = manager.head_dim
+        if manager.golay_packed and not self._fused_ok():
+            raise ValueError("packed Golay storage needs the fused shim write / read "
+                             "(fused=True, a backend with shim_write, head_dim <= 512)")
         self.num_kv_groups = num_heads // self.num_kv_heads
         self._injection_count = 0
         self._total_values = 0
@@ -272,11 +293,13 @@ class ECCBackend:
         inject = cfg.inject_errors and cfg.ber > 0
         seed0 = cfg.seed + self._injection_count
         if self._fused_ok(k) and k.dtype == v.dtype:
-            self.codec_backend.shim_write(k, v, mgr, layer_idx, cfg.codec, _N_BITS[cfg.codec],
+            self.codec_backend.shim_write(k, v, mgr, layer_idx, mgr.shim_codec, _N_BITS[cfg.codec],
                                           inject, cfg.ber, seed0, seq_id, cfg.scale_rule)
             if inject:
                 self._injection_count += rows
             return
+        if mgr.golay_packed:
+            raise TypeError(f"packed Golay storage: K/V dtype {k.dtype}/{v.dtype} has no fused write")
         blk, slot = mgr.slots(seq_id, seq_len)
         kr = k.reshape(batch, seq_len, hk, d)
         vr = v.reshape(batch, seq_len, hk, d)
@@ -365,7 +388,7 @@ class ECCBackend:
             # the reference's seq_len==1 Triton path (ecc_shim.py:791-800) keeps no statistics
             interp = cfg.use_interpolation and cfg.codec == "hamming84"
             k_t, v_t = self.codec_backend.shim_read(
-                mgr, layer_idx, ctx, cfg.codec, interp, torch.float32 if fast else q.dtype,
+                mgr, layer_idx, ctx, mgr.shim_codec, interp, torch.float32 if fast else q.dtype,
                 None if fast else self._stats, seq_id)
             if fast:
                 return self._decode_step_attention(q, k_t, v_t)
@@ -638,7 +661,8 @@ def patch_model_with_ecc_attention(model, config, num_blocks=256):
     manager = SimpleBlockManager(num_blocks=num_blocks, block_size=config.block_size,
                                  num_layers=len(layers), num_kv_heads=num_kv_heads,
                                  head_dim=head_dim, device=next(model.parameters()).device,
-                                 codec=config.codec)
+                                 codec=config.codec,
+                                 golay_storage=getattr(config, "golay_storage", "int32"))
     backend = ECCBackend(manager, config, num_heads)
     rotary = None if model_type == "gpt2" else _find_rotary_embedding(model, layers)
     originals = {}

@@ -555,7 +555,7 @@ def fused_decode_dequantize_hamming84(codewords, scales, output_dtype=torch.floa
 # ============================================================================
 
 SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84": _lib.CODEC_H84,
-               "golay": _lib.CODEC_GOLAY}
+               "golay": _lib.CODEC_GOLAY, "golay_packed": _lib.CODEC_GOLAY_PACKED}
 
 
 def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0,

@@ -129,3 +129,53 @@ def test_hip_vs_torch(gpu, codec, batch, heads, kvh, d, ctx, ber, dtype):
         assert got.dtype == dtype
         assert torch.allclose(got.float(), ref, atol=1e-3, rtol=1e-3), \
             float((got.float() - ref).abs().max())
+
+
+def _pack_golay(cache, d):
+    """int32 Golay cache [..., bs * g] -> the packed layout [..., bs * KVECC_GOLAY_PACKED_ROW(g)]
+    (3 little-endian bytes per codeword, rows zero-padded to 4 bytes)."""
+    g = (d + 2) // 3
+    row = (3 * g + 3) // 4 * 4
+    w = cache.view(*cache.shape[:-1], -1, g).numpy().astype(np.uint32)
+    out = np.zeros(w.shape[:-1] + (row,), np.uint8)
+    for byte in range(3):
+        out[..., byte:3 * g:3] = (w >> (8 * byte)) & 0xFF
+    return torch.from_numpy(out.reshape(*cache.shape[:-1], -1))
+
+
+PACKED_CASES = [(2, 4, 4, 128, 513, 0.02), (1, 6, 3, 64, 77, 0.0), (3, 8, 2, 100, 300, 0.01),
+                (2, 2, 1, 7, 41, 0.05), (1, 4, 4, 256, 2050, 0.01)]
+
+
+@pytest.mark.parametrize("batch,heads,kvh,d,ctx,ber", PACKED_CASES[:3])
+def test_cpu_packed_golay_equals_int32(batch, heads, kvh, d, ctx, ber):
+    """The host twin reads the packed layout (KVECC_CODEC_GOLAY_PACKED) to the
+    same bits as the int32 one."""
+    from kvecc import cpu_ops
+    kc, vc, table, lens, ks, vs = _cache("cpu", "golay", batch, heads, kvh, d, ctx, ber, seed=ctx)
+    q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(1))
+    outs = []
+    for codec, k, v in (("golay", kc, vc), ("golay_packed", _pack_golay(kc, d), _pack_golay(vc, d))):
+        out = torch.empty(batch, heads, d)
+        cpu_ops.paged_attention_into(q, k, v, table, lens, ks, vs, out, 1, 16, 1 / math.sqrt(d), codec)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,heads,kvh,d,ctx,ber", PACKED_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_hip_packed_golay_vs_torch(gpu, batch, heads, kvh, d, ctx, ber, dtype):
+    """kvecc_paged_attention on packed Golay caches (4 codewords per lane from
+    one 12-byte buffer load) against the torch fp32 reference of the int32 layout."""
+    from kvecc import ops
+    kc, vc, table, lens, ks, vs = _cache("cpu", "golay", batch, heads, kvh, d, ctx, ber, seed=ctx)
+    q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(1)).to(dtype)
+    ref = _torch_reference(q.float(), kc, vc, table, lens, ks, vs, 1, 16, "golay")
+    dev = lambda t: t.to(gpu)  # noqa: E731
+    out = torch.empty(batch, heads, d, dtype=dtype, device=gpu)
+    ops.paged_attention_into(dev(q), dev(_pack_golay(kc, d)), dev(_pack_golay(vc, d)), dev(table),
+                             dev(lens), dev(ks), dev(vs), out, 1, 16, 1 / math.sqrt(d), "golay_packed")
+    got = out.float().cpu()
+    tol = (ATOL, RTOL) if dtype == torch.float32 else (1e-2, 1e-2)  # bf16 output rounding
+    assert torch.allclose(got, ref, atol=tol[0], rtol=tol[1]), float((got - ref).abs().max())

@@ -22,12 +22,22 @@ def test_config_validation():
         ECCShimConfig(codec="reed-solomon")
     c = ECCShimConfig(codec="golay", ber=1e-3, backend="hip")
     assert c.backend == "hip" and c.block_size == 16 and c.seed == 42
+    assert c.golay_storage == "int32"
+    with pytest.raises(ValueError):
+        ECCShimConfig(codec="golay", golay_storage="int24")
+    with pytest.raises(ValueError):
+        ECCShimConfig(codec="golay", golay_storage="packed", fused=False)
 
 
 def test_block_manager_layout_cpu():
     from kvecc.ecc_shim import SimpleBlockManager
     m = SimpleBlockManager(8, 16, 3, 4, 128, device="cpu", codec="golay")
     assert m.k_cache.shape == (8, 3, 4, 16 * 43) and m.k_cache.dtype == torch.int32
+    mp = SimpleBlockManager(8, 16, 3, 4, 128, device="cpu", codec="golay", golay_storage="packed")
+    assert mp.k_cache.shape == (8, 3, 4, 16 * 132) and mp.k_cache.dtype == torch.uint8
+    assert mp.shim_codec == "golay_packed" and m.shim_codec == "golay"
+    mp = SimpleBlockManager(8, 16, 3, 4, 64, device="cpu", codec="golay", golay_storage="packed")
+    assert mp.k_cache.shape == (8, 3, 4, 16 * 68)  # 22 codewords = 66 B, padded to 68
     m2 = SimpleBlockManager(8, 16, 3, 4, 64, device="cpu", codec="hamming84")
     assert m2.k_cache.shape == (8, 3, 4, 16 * 64) and m2.k_scales.shape == (8, 3, 4, 16)
     m2.allocate(0, 40)
@@ -279,3 +289,80 @@ def test_patched_forward_replays_in_a_hip_graph(gpu, codec, interp):
         st = get_ecc_stats(model)
         assert st["errors_corrected"] == eager_stats["errors_corrected"] > 0
         assert st["errors_detected"] == eager_stats["errors_detected"]
+
+
+def _packed_equals_int32(device, backend):
+    """golay_storage="packed" keeps the low 3 bytes of every int32 codeword the
+    reference layout stores (row padding zero), the same scales, and reads back
+    the same attention outputs and statistics (prefill and seq_len==1)."""
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    for d, dt in ((128, torch.float16), (100, torch.float32), (64, torch.bfloat16), (7, torch.float16)):
+        b, s, hk, nh = 2, 37, 2, 4
+        res = {}
+        for storage in ("int32", "packed"):
+            cfg = ECCShimConfig(codec="golay", ber=0.02, inject_errors=True, seed=11,
+                                backend=backend, golay_storage=storage)
+            mgr = SimpleBlockManager(6, 16, 3, hk, d, device=device, codec="golay",
+                                     golay_storage=storage)
+            be = ECCBackend(mgr, cfg, num_heads=nh)
+            g = torch.Generator().manual_seed(d)
+            k = torch.randn(b, s, hk * d, generator=g).to(device=device, dtype=dt)
+            v = torch.randn(b, s, hk * d, generator=g).to(device=device, dtype=dt)
+            q = torch.randn(b, nh, s, d, generator=g).to(device=device, dtype=dt)
+            be.write(k, v, layer_idx=2)
+            out = be.attend(q, layer_idx=2)
+            out1 = be.attend(q[:, :, :1], layer_idx=2)
+            res[storage] = (mgr, out.float().cpu(), out1.float().cpu(), be._errors_corrected,
+                            be._errors_detected)
+        m32, mpk = res["int32"][0], res["packed"][0]
+        gw = (d + 2) // 3
+        row = (3 * gw + 3) // 4 * 4
+        for c32, cpk in ((m32.k_cache, mpk.k_cache), (m32.v_cache, mpk.v_cache)):
+            w = m32.view5(c32).cpu().numpy().astype(np.uint32)           # [..., gw]
+            exp = np.zeros(w.shape[:-1] + (row,), np.uint8)
+            for byte in range(3):
+                exp[..., byte:3 * gw:3] = (w >> (8 * byte)) & 0xFF
+            assert np.array_equal(mpk.view5(cpk).cpu().numpy(), exp), d
+        assert torch.equal(m32.k_scales.cpu(), mpk.k_scales.cpu())
+        assert torch.equal(m32.v_scales.cpu(), mpk.v_scales.cpu())
+        assert res["int32"][3:] == res["packed"][3:] and res["int32"][3] > 0, d
+        assert torch.equal(res["int32"][1], res["packed"][1]), d
+        assert torch.equal(res["int32"][2], res["packed"][2]), d
+
+
+def test_golay_packed_storage_cpu_backend():
+    _packed_equals_int32(torch.device("cpu"), "cpu")
+
+
+@pytest.mark.gpu
+def test_golay_packed_storage(gpu):
+    _packed_equals_int32(gpu, "hip")
+
+
+@pytest.mark.gpu
+def test_golay_packed_storage_hip_equals_cpu(gpu):
+    """The HIP and host shim kernels write the same packed cache bytes and read
+    back the same K/V and statistics."""
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    for d, dt in ((128, torch.bfloat16), (100, torch.float16), (5, torch.float32)):
+        b, s, hk = 2, 29, 3
+        g = torch.Generator().manual_seed(d)
+        k = (torch.randn(b, s, hk * d, generator=g) * 2).to(dt)
+        v = (torch.randn(b, s, hk * d, generator=g) * 2).to(dt)
+        res = []
+        for backend, dev in (("hip", gpu), ("cpu", torch.device("cpu"))):
+            cfg = ECCShimConfig(codec="golay", ber=0.02, inject_errors=True, seed=5,
+                                backend=backend, scale_rule="div7", golay_storage="packed")
+            mgr = SimpleBlockManager(4, 16, 2, hk, d, device=dev, codec="golay",
+                                     golay_storage="packed")
+            be = ECCBackend(mgr, cfg, num_heads=hk)
+            be.write(k.to(dev), v.to(dev), layer_idx=1)
+            k_t, v_t = be.codec_backend.shim_read(mgr, 1, s, mgr.shim_codec, False, torch.float32,
+                                                  be._stats)
+            res.append((mgr.k_cache.cpu(), mgr.v_cache.cpu(), mgr.k_scales.cpu(),
+                        mgr.v_scales.cpu(), k_t.cpu(), v_t.cpu(),
+                        be.codec_backend.read_stats(be._stats, 2)))
+        hip, cpu = res
+        for i in range(6):
+            assert torch.equal(hip[i], cpu[i]), (d, i)
+        assert hip[6] == cpu[6] and hip[6][0] > 0, d

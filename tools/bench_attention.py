@@ -37,7 +37,9 @@ def main():
     nb = (args.ctx + args.bs - 1) // args.bs
     blocks = args.batch * nb
     per = args.d if args.codec == "hamming84" else (args.d + 2) // 3
-    if args.codec == "hamming84":
+    if args.codec == "golay_packed":  # bytes per token row (KVECC_GOLAY_PACKED_ROW)
+        per = (3 * per + 3) // 4 * 4
+    if args.codec != "golay":
         kc = torch.randint(0, 256, (blocks, 1, args.kv_heads, args.bs * per), dtype=torch.uint8,
                            device=dev, generator=g)
     else:

@@ -165,12 +165,14 @@ def extended(reps):
     out["packed_h84_decode"] = entry(timed(lambda: ops.hamming84_decode_packed_into(
         hcw, hn2, ht, n, st), reps), n, "values", 1.75)
     # paged decode attention, [8 seqs x 4096 ctx, 32 heads, D=128]
-    for codec in ("hamming84", "golay"):
+    for codec in ("hamming84", "golay", "golay_packed"):
         b, hq, d, ctx, bs = 8, 32, 128, 4096, 16
         per = d if codec == "hamming84" else (d + 2) // 3
+        if codec == "golay_packed":  # bytes per token row (KVECC_GOLAY_PACKED_ROW)
+            per = (3 * per + 3) // 4 * 4
         nb = ctx // bs
         blocks = b * nb
-        if codec == "hamming84":
+        if codec != "golay":
             kc = torch.randint(0, 256, (blocks, 1, hq, bs * per), dtype=torch.uint8, device=dev)
         else:
             kc = torch.randint(0, 1 << 24, (blocks, 1, hq, bs * per), dtype=torch.int32, device=dev)
