@@ -52,6 +52,13 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data fo
 // Packed Golay caches (KVECC_CODEC_GOLAY_PACKED, 3-byte codewords): a lane owns
 // 4 codewords = 12 bytes = 3 aligned dwords of its token row
 constexpr int kGolayPackedVec = 4;
+// Golay decode through the spread tables (golay_attn_table_dev: 32-bit entries,
+// nibbles one per byte): per codeword 2 LDS reads + 9 VALU ops (address math,
+// one masked xor, three v_cvt_f32_ubyteN) instead of ~13 through the 16-bit
+// tables; 0 = the 16-bit tables (A/B: tools/exp/run_attn.py)
+#ifndef KVECC_ATTN_GOLAY_SPREAD
+#define KVECC_ATTN_GOLAY_SPREAD 1
+#endif
 constexpr bool is_golay(int codec) { return codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED; }
 
 struct AttnArgs {
@@ -68,6 +75,7 @@ struct AttnArgs {
   uint32_t cache_bytes, scale_bytes;  // buffer-load bounds (BUF kernels)
   float sm_scale;
   const uint16_t *par, *cor;  // Golay tables
+  const uint32_t *atab;       // Golay spread tables (KVECC_ATTN_GOLAY_SPREAD)
 };
 
 // Lane chunk c of a token row: VEC 32-bit words = 4*VEC H(8,4) codewords, or
@@ -140,7 +148,7 @@ struct Chunk {
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
   // correction tables (uncorrectable words keep their data, as golay_decode)
-  __device__ __forceinline__ void decode(const float *lut, const uint16_t *gtab, float *v) const {
+  __device__ __forceinline__ void decode(const float *lut, const uint32_t *gtab, float *v) const {
     if constexpr (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
@@ -150,10 +158,26 @@ struct Chunk {
     } else {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        uint32_t cnt;
-        const uint32_t dw = golay_decode1(w[k], gtab, gtab + 4096, cnt);
+        if (KVECC_ATTN_GOLAY_SPREAD) {
+          // P = spread(lo) | parity(lo) << 20; syndrome = (w >> 12) ^ parity,
+          // as a byte offset into the correction half: ((w >> 10) ^ (P >> 18)) & 0x3FFC
+          const uint32_t p = gtab[w[k] & 0xFFFu];
+          const uint32_t off = ((w[k] >> 10) ^ (p >> 18)) & 0x3FFCu;
+          const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab + 4096) + off);
+          // corrected nibbles, one per byte: (p ^ e) & 0x0F0F0F in one v_bitop3
+          // (0x28 = (S0 ^ S1) & S2); the conversions are written out because
+          // the compiler otherwise re-extracts each nibble with a shift and a mask
+          const uint32_t sp = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
+          asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(v[3 * k]) : "v"(sp));  // n, see kOffset
+          asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(v[3 * k + 1]) : "v"(sp));
+          asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(v[3 * k + 2]) : "v"(sp));
+        } else {
+          const uint16_t *t16 = reinterpret_cast<const uint16_t *>(gtab);
+          uint32_t cnt;
+          const uint32_t dw = golay_decode1(w[k], t16, t16 + 4096, cnt);
 #pragma unroll
-        for (int e = 0; e < 3; ++e) v[3 * k + e] = (float)__builtin_amdgcn_ubfe(dw, 4 * e, 4);  // n, see kOffset
+          for (int e = 0; e < 3; ++e) v[3 * k + e] = (float)__builtin_amdgcn_ubfe(dw, 4 * e, 4);  // n, see kOffset
+        }
       }
     }
   }
@@ -205,11 +229,18 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   // cache row of each token of the split (-1 = no block / past the split),
   // padded so the unrolled loop reads it without bounds checks
   __shared__ int32_t rows[kMaxSplit + (kUnroll - 1) * kBlock];
-  __shared__ float red[TP * W * E];        // per-group acc
+  // Golay tables copied from the device: the 32 KiB spread tables, or
+  // parity[4096] then correct[4096] as uint16 (16 KiB).  With the spread
+  // tables the block-table slice (before the copy) and the merge buffer (after
+  // the loop) live in the same LDS, which keeps 4 workgroups per CU.
+  constexpr bool kSpread = is_golay(CODEC) && KVECC_ATTN_GOLAY_SPREAD;
+  constexpr int kTabWords = !is_golay(CODEC) ? 4 : kSpread ? 8192 : 4096;
+  static_assert(!kSpread || (TP * W * E <= kTabWords && kMaxSplit + 1 <= kTabWords), "LDS aliasing");
+  __shared__ __attribute__((aligned(16))) uint32_t gtab[kTabWords];
+  __shared__ float red_own[kSpread ? 1 : TP * W * E];  // per-group acc
+  float *red = kSpread ? reinterpret_cast<float *>(gtab) : red_own;
   __shared__ float gml[2][TP];             // per-group running max / sum
-  __shared__ float lut[256];               // H(8,4): codeword byte -> data - 8
-  // Golay: parity[4096] then correct[4096] (16 KiB) copied from the device tables
-  __shared__ __attribute__((aligned(16))) uint16_t gtab[is_golay(CODEC) ? 8192 : 8];
+  __shared__ float lut[CODEC == KVECC_CODEC_H84 ? 256 : 1];  // H(8,4): codeword byte -> data - 8
 
   const int64_t bh = blockIdx.y;
   const int64_t b = bh / a.heads, h = bh % a.heads;
@@ -225,7 +256,8 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
 
   {  // block-table slice -> LDS (one load per logical block), then one 32-bit
      // division per token; none in the streaming loop
-    __shared__ int32_t blks[kMaxSplit + 1];
+    __shared__ int32_t blks_own[kSpread ? 1 : kMaxSplit + 1];
+    int32_t *blks = kSpread ? reinterpret_cast<int32_t *>(gtab) : blks_own;
     const uint32_t bs = (uint32_t)a.bs;
     const uint32_t lb0 = (uint32_t)(t0 / a.bs);
     const int nlb = ntok > 0 ? (int)((uint32_t)(t1 - 1) / bs - lb0 + 1) : 0;
@@ -246,7 +278,13 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       rows[i] = row;
     }
   }
-  if (is_golay(CODEC)) {
+  if (kSpread) {
+    __syncthreads();  // blks (aliased) fully read
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
+#pragma unroll
+    for (int i = threadIdx.x; i < 2048; i += kBlock) dst[i] = src[i];
+  } else if (is_golay(CODEC)) {
     const u32x4 *src0 = reinterpret_cast<const u32x4 *>(a.par);
     const u32x4 *src1 = reinterpret_cast<const u32x4 *>(a.cor);
     u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
@@ -345,6 +383,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   }
 
   // ---- merge the TP groups ------------------------------------------------------
+  if (kSpread) __syncthreads();  // the tables (aliased by red) fully read
   if (live) {
 #pragma unroll
     for (int e = 0; e < E; ++e)
@@ -574,10 +613,12 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     a.scale_bytes = fits ? (uint32_t)(rows_total * 4) : 0u;
   }
   a.par = a.cor = nullptr;
+  a.atab = nullptr;
   if (codec != KVECC_CODEC_H84) {
     a.par = golay_parity_table_dev();
     a.cor = golay_correct_table_dev();
-    if (!a.par || !a.cor) return KVECC_EHIP;
+    a.atab = golay_attn_table_dev();
+    if (!a.par || !a.cor || !a.atab) return KVECC_EHIP;
   }
   hipStream_t st = as_stream(stream);
   int rc;

@@ -30,6 +30,12 @@ int current_device();
 //   correct[s]  (uint16) = data-error(12) | count(3) << 12      (decode)
 const uint16_t *golay_parity_table_dev();
 const uint16_t *golay_correct_table_dev();
+// Golay tables for paged attention (uint32[8192]): data nibbles spread one per
+// byte, spread(x) = x&15 | (x>>4&15)<<8 | (x>>8&15)<<16, so a value converts
+// with one v_cvt_f32_ubyteN:
+//   [0, 4096)    spread(d) | parity(d) << 20
+//   [4096, 8192) spread(data error of syndrome s)   (0 when uncorrectable)
+const uint32_t *golay_attn_table_dev();
 // host-side table builders (product copy, independent of the test oracle)
 void build_golay_parity_table(uint16_t *out4096);
 void build_golay_correct_table(uint16_t *out4096);

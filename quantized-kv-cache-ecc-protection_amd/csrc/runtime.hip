@@ -35,6 +35,7 @@ static std::mutex g_mu;
 static int g_cu[kMaxDev];
 static uint16_t *g_parity[kMaxDev];
 static uint16_t *g_correct[kMaxDev];
+static uint32_t *g_attn[kMaxDev];
 
 int current_device() {
   int d = 0;
@@ -109,6 +110,32 @@ void build_golay_correct_table(uint16_t *out) {
   }
 }
 
+static uint32_t spread12(uint32_t x) { return (x & 0xFu) | (x >> 4 & 0xFu) << 8 | (x >> 8 & 0xFu) << 16; }
+
+static int ensure_attn_table(int d) {
+  if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_attn[d]) return KVECC_OK;
+  uint16_t par[4096], cor[4096];
+  build_golay_parity_table(par);
+  build_golay_correct_table(cor);
+  static uint32_t host[8192];
+  for (uint32_t i = 0; i < 4096; ++i) {
+    host[i] = spread12(i) | (uint32_t)par[i] << 20;
+    host[4096 + i] = spread12(cor[i] & 0xFFFu);
+  }
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
+  if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
+  uint32_t *buf = nullptr;
+  hipError_t e = hipMalloc(&buf, sizeof(host));
+  if (e == hipSuccess) e = hipMemcpy(buf, host, sizeof(host), hipMemcpyHostToDevice);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(KVECC_EHIP, "golay attention table upload: %s", hipGetErrorString(e));
+  g_attn[d] = buf;
+  return KVECC_OK;
+}
+
 static int ensure_tables(int d) {
   if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
   std::lock_guard<std::mutex> lk(g_mu);
@@ -134,6 +161,13 @@ const uint16_t *golay_parity_table_dev() {
   if (d >= 0 && d < kMaxDev && g_parity[d]) return g_parity[d];
   if (ensure_tables(d) != KVECC_OK) return nullptr;
   return g_parity[d];
+}
+
+const uint32_t *golay_attn_table_dev() {
+  int d = current_device();
+  if (d >= 0 && d < kMaxDev && g_attn[d]) return g_attn[d];
+  if (ensure_attn_table(d) != KVECC_OK) return nullptr;
+  return g_attn[d];
 }
 
 const uint16_t *golay_correct_table_dev() {

@@ -1,6 +1,6 @@
 """A/B: paged attention lane widths (tools/exp/libattn_v*.so built with other
 KVECC_ATTN_*_VEC) vs production libkvecc.so, interleaved, same inputs, both codecs.
-Build: make -C tools/exp libattn_v8.so libattn_v16.so   Run (GPU box): python tools/exp/run_attn.py"""
+Build: make -C tools/exp libattn_v8.so libattn_v16.so libattn_u16.so   Run (GPU box): python tools/exp/run_attn.py"""
 import ctypes, math, os, statistics, sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
@@ -9,7 +9,7 @@ import torch
 from kvecc import _lib, ops
 VP, I64 = ctypes.c_void_p, ctypes.c_int64
 libs = {"prod": _lib.load()}
-for name in ("v2", "v8", "v16", "buf", "nopk", "bufnopk"):
+for name in ("v2", "v8", "v16", "buf", "nopk", "bufnopk", "u16"):
     path = os.path.join(HERE, f"libattn_{name}.so")
     if os.path.exists(path):
         libs[name] = ctypes.CDLL(path)
@@ -39,8 +39,15 @@ pad = torch.zeros(blocks * H * BS, G * 3, dtype=torch.uint8, device=dev)
 pad[:, :D] = nib.view(-1, D)
 caches = {("hamming84", "random"): torch.randint(0, 256, (blocks, 1, H, BS * D), dtype=torch.uint8, device=dev, generator=g),
           ("hamming84", "encoded"): ops.hamming84_encode(nib).view(blocks, 1, H, BS * D),
-          ("golay", "encoded"): ops.golay_encode(pad.view(-1, 3)).view(blocks, 1, H, BS * G)}
-codes = {"hamming84": _lib.CODEC_H84, "golay": _lib.CODEC_GOLAY}
+          ("golay", "encoded"): ops.golay_encode(pad.view(-1, 3)).view(blocks, 1, H, BS * G),
+          ("golay", "random"): torch.randint(0, 1 << 24, (blocks, 1, H, BS * G), dtype=torch.int32, device=dev, generator=g)}
+RB = _lib.golay_packed_row_bytes(G)  # packed rows: low 3 bytes of each int32 codeword
+for kind in ("encoded", "random"):
+    w = caches[("golay", kind)].view(-1, G).view(torch.uint8).view(-1, G, 4)[:, :, :3].reshape(-1, 3 * G)
+    pk = torch.zeros(w.shape[0], RB, dtype=torch.uint8, device=dev)
+    pk[:, :3 * G] = w
+    caches[("golay_packed", kind)] = pk.view(blocks, 1, H, BS * RB)
+codes = {"hamming84": _lib.CODEC_H84, "golay": _lib.CODEC_GOLAY, "golay_packed": _lib.CODEC_GOLAY_PACKED}
 outs = {}
 for (codec, kind), kc in caches.items():
     vc = kc.roll(1, 0).contiguous()
