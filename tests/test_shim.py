@@ -62,15 +62,19 @@ def _model(golden, manifest, device):
     return model.to(device), torch.from_numpy(g["input_ids"]).to(device), g
 
 
-def _shim_matches_reference(device, backend, golden, manifest):
+def _shim_matches_reference(device, backend, golden, manifest, golay_storage="int32"):
     from kvecc.ecc_shim import (ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention,
                                 reset_ecc_cache)
     model, ids, g = _model(golden, manifest, device)
-    for i, run in enumerate(manifest["shim_gpt2"]["params"]["runs"]):
+    runs = list(enumerate(manifest["shim_gpt2"]["params"]["runs"]))
+    if golay_storage != "int32":
+        runs = [(i, r) for i, r in runs if r["codec"] == "golay"]
+        assert runs
+    for i, run in runs:
         # the fixtures come from the reference run on CPU tensors: IEEE scale division
         cfg = ECCShimConfig(codec=run["codec"], ber=run["ber"], inject_errors=run["ber"] > 0,
                             seed=42, block_size=16, use_interpolation=run["use_interpolation"],
-                            backend=backend, scale_rule="div7")
+                            backend=backend, scale_rule="div7", golay_storage=golay_storage)
         with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=16):
             reset_ecc_cache(model)
             out = model(ids)
@@ -90,6 +94,17 @@ def test_shim_gpt2_matches_reference(gpu, golden, manifest):
 def test_shim_gpt2_matches_reference_cpu_backend(golden, manifest):
     """The same end-to-end run on the host backend (model and cache on the CPU)."""
     _shim_matches_reference(torch.device("cpu"), "cpu", golden, manifest)
+
+
+def test_shim_gpt2_packed_golay_matches_reference_cpu_backend(golden, manifest):
+    """The packed Golay cache layout reproduces the reference shim's Golay runs
+    (statistics exactly, logits within the float tolerance)."""
+    _shim_matches_reference(torch.device("cpu"), "cpu", golden, manifest, golay_storage="packed")
+
+
+@pytest.mark.gpu
+def test_shim_gpt2_packed_golay_matches_reference(gpu, golden, manifest):
+    _shim_matches_reference(gpu, "hip", golden, manifest, golay_storage="packed")
 
 
 def _cache_bits_match_oracle(gpu, backend):
@@ -252,7 +267,7 @@ def test_strided_write_equals_contiguous(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("codec,interp", [("hamming84", True), ("golay", False)])
+@pytest.mark.parametrize("codec,interp", [("hamming84", True), ("golay", False), ("golay_packed", False)])
 def test_patched_forward_replays_in_a_hip_graph(gpu, codec, interp):
     """The whole patched forward (cache reset included) captures in one HIP graph:
     no host sync or host-to-device copy in a steady-state forward.  Replays give
@@ -265,8 +280,9 @@ def test_patched_forward_replays_in_a_hip_graph(gpu, codec, interp):
     cfg_m = GPT2Config(n_layer=2, n_head=4, n_embd=256, n_positions=128)
     model = GPT2LMHeadModel(cfg_m).half().to(gpu).eval()
     ids = torch.randint(0, cfg_m.vocab_size, (1, 96), generator=torch.Generator().manual_seed(1)).to(gpu)
-    cfg = ECCShimConfig(codec=codec, ber=1e-2, inject_errors=True, seed=42, block_size=16,
-                        use_interpolation=interp)
+    storage = "packed" if codec == "golay_packed" else "int32"
+    cfg = ECCShimConfig(codec=codec.replace("_packed", ""), ber=1e-2, inject_errors=True, seed=42,
+                        block_size=16, use_interpolation=interp, golay_storage=storage)
     with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=6):
         def fwd():
             reset_ecc_cache(model)
