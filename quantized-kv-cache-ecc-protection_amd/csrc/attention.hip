@@ -29,7 +29,17 @@ namespace kvecc {
 constexpr int kMaxSplit = 1024;   // context tokens per workgroup (upper bound)
 constexpr int kMaxSplits = 1024;  // splits per (batch, head)
 constexpr int kAttnMaxD = 256;
-constexpr int kUnroll = 4;        // token rows in flight per lane group
+#ifndef KVECC_ATTN_UNROLL
+#define KVECC_ATTN_UNROLL 4
+#endif
+// int32 Golay rows: 2 in flight measured 72.8 vs 80.0 us at 4 (H84 and packed
+// Golay lose with 2; every codec loses with 8): tools/exp/run_attn.py
+#ifndef KVECC_ATTN_GOLAY_UNROLL
+#define KVECC_ATTN_GOLAY_UNROLL 2
+#endif
+constexpr int kUnroll = KVECC_ATTN_UNROLL;  // token rows in flight per lane group
+constexpr int kGolayUnroll = KVECC_ATTN_GOLAY_UNROLL;
+constexpr int kMaxUnroll = kUnroll > kGolayUnroll ? kUnroll : kGolayUnroll;
 // codeword words per lane of a token row (A/B knobs: tools/exp/run_attn.py)
 #ifndef KVECC_ATTN_H84_VEC
 #define KVECC_ATTN_H84_VEC 4
@@ -228,7 +238,8 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
   // cache row of each token of the split (-1 = no block / past the split),
   // padded so the unrolled loop reads it without bounds checks
-  __shared__ int32_t rows[kMaxSplit + (kUnroll - 1) * kBlock];
+  constexpr int U = CODEC == KVECC_CODEC_GOLAY ? kGolayUnroll : kUnroll;  // rows in flight
+  __shared__ int32_t rows[kMaxSplit + (kMaxUnroll - 1) * kBlock];
   // Golay tables copied from the device: the 32 KiB spread tables, or
   // parity[4096] then correct[4096] as uint16 (16 KiB).  With the spread
   // tables the block-table slice (before the copy) and the merge buffer (after
@@ -266,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
     __syncthreads();
     const int32_t head_row0 = (int32_t)((a.layer * a.kv_heads + hk) * a.bs);
     const int32_t blk_rows = (int32_t)(a.layers * a.kv_heads * a.bs);
-    const int npad = (int)a.split + (kUnroll - 1) * kBlock;
+    const int npad = (int)a.split + (U - 1) * kBlock;
     for (int i = threadIdx.x; i < npad; i += kBlock) {
       int32_t row = -1;
       if (i < ntok) {
@@ -319,17 +330,17 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.k_scales), 0, (int)a.scale_bytes, kRsrcWord3);
   const __amdgpu_buffer_rsrc_t vsrs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v_scales), 0, (int)a.scale_bytes, kRsrcWord3);
-  // ---- one pass: kUnroll K and V rows in flight per lane, online softmax per group
+  // ---- one pass: U K and V rows in flight per lane, online softmax per group
   float m = -INFINITY, l = 0.0f, acc[E];
   float psum = 0.0f;  // sum of p * v_scale, for the kOffset fold of the V sums
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = 0.0f;
-  for (int i0 = grp; i0 < ntok; i0 += TP * kUnroll) {
-    C kc[kUnroll], vc[kUnroll];
-    float ks[kUnroll], vs[kUnroll];
-    bool ok[kUnroll];
+  for (int i0 = grp; i0 < ntok; i0 += TP * U) {
+    C kc[U], vc[U];
+    float ks[U], vs[U];
+    bool ok[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {  // branch-free: invalid rows read row 0, masked
+    for (int u = 0; u < U; ++u) {  // branch-free: invalid rows read row 0, masked
       const int32_t r = rows[i0 + u * TP];
       ok[u] = r >= 0;
       const int64_t row = ok[u] ? r : 0;
@@ -345,10 +356,10 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
         vs[u] = a.v_scales[row];
       }
     }
-    float sc[kUnroll];
+    float sc[U];
     float mn = m;
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       float part = 0.0f;
       if (live) {
         float kv[E];
@@ -368,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] *= alpha;
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
+    for (int u = 0; u < U; ++u) {
       const float p = expf(sc[u] - mn);  // invalid rows: exp(-inf) = 0
       l += p;
       if (live) {
