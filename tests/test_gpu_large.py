@@ -130,7 +130,7 @@ def test_fused_quantize_dequant_past_4g(gpu, oracle):
     assert torch.equal(out[sample].cpu(), torch.from_numpy(ref).to(torch.float16))
 
 
-@pytest.mark.parametrize("codec", ["hamming84", "golay"])
+@pytest.mark.parametrize("codec", ["hamming84", "golay", "golay_packed"])
 def test_paged_attention_cache_past_4g(gpu, codec):
     """Caches over 4 GiB take the 64-bit-addressed attention kernels (smaller
     ones use 32-bit buffer offsets).  The sequence's blocks sit past the 4 GiB
@@ -140,12 +140,14 @@ def test_paged_attention_cache_past_4g(gpu, codec):
     from kvecc import ops
     heads, d, bs, ctx, batch = 8, 128, 16, 1000, 2
     per = d if codec == "hamming84" else (d + 2) // 3
-    cdt = torch.uint8 if codec == "hamming84" else torch.int32
-    row_bytes = heads * bs * per * (1 if codec == "hamming84" else 4)
+    if codec == "golay_packed":  # bytes per token row (KVECC_GOLAY_PACKED_ROW)
+        per = (3 * per + 3) // 4 * 4
+    cdt = torch.int32 if codec == "golay" else torch.uint8
+    row_bytes = heads * bs * per * (4 if codec == "golay" else 1)
     num_blocks = (1 << 32) // row_bytes + 200                    # > 4 GiB per cache
     nb = (ctx + bs - 1) // bs
     g = torch.Generator(device=gpu).manual_seed(5)
-    hi = 256 if codec == "hamming84" else 1 << 24
+    hi = 1 << 24 if codec == "golay" else 256
     used = torch.arange(num_blocks - batch * nb, num_blocks, device=gpu)   # the far end
     big_k = torch.zeros(num_blocks, 1, heads, bs * per, dtype=cdt, device=gpu)
     big_v = torch.zeros_like(big_k)
