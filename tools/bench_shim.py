@@ -57,6 +57,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--codec", default="hamming84")
     ap.add_argument("--interp", type=int, default=1)
+    ap.add_argument("--golay-storage", default="int32", choices=["int32", "packed"])
     ap.add_argument("--bers", type=float, nargs="*", default=[0.0, 1e-3, 1e-2])
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=10)
@@ -76,7 +77,8 @@ def main():
     model = GPT2LMHeadModel(GPT2Config(n_positions=1024)).half().to(dev).eval()
     ids = torch.randint(0, 50257, (1, args.seq), generator=torch.Generator().manual_seed(0)).to(dev)
     out = {"config": {"model": "gpt2 12L/12H/768 random-init fp16", "seq_len": args.seq,
-                      "codec": args.codec, "use_interpolation": bool(args.interp),
+                      "codec": args.codec, "golay_storage": args.golay_storage,
+                      "use_interpolation": bool(args.interp),
                       "block_size": 16, "seed": 42, "fused": not args.composed}, "runs": []}
     with torch.no_grad():
         med, mn = timed(lambda: model(ids), args.steps, args.warmup)
@@ -87,7 +89,7 @@ def main():
         for ber in args.bers:
             cfg = ECCShimConfig(codec=args.codec, ber=ber, inject_errors=ber > 0, seed=42,
                                 block_size=16, use_interpolation=bool(args.interp),
-                                fused=not args.composed)
+                                fused=not args.composed, golay_storage=args.golay_storage)
             with patch_model_with_ecc_attention(model, cfg, num_blocks=nblocks):
                 def fwd():
                     reset_ecc_cache(model)
