@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--event-every", type=int, default=10,
                     help="time the kernels of every k-th timed step (a timed dispatch costs the "
                          "step ~8 us; timing every step cost 7-9%% of throughput)")
+    ap.add_argument("--dist", action="store_true",
+                    help="create the RCCL process group even at world size 1 (exercises the "
+                         "barrier and the stats/timing all-reduces on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -110,6 +113,16 @@ def cpu_baseline(budget_s, threads):
                       f"oracle/kvecc_oracle.c on {threads} host threads"}
 
 
+def cpu_quota():
+    """cgroup v2 CPU quota of this process as 'N cores' (or 'unlimited')."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return "unlimited" if q == "max" else f"{int(q) / int(p):g} cores"
+    except (OSError, ValueError):
+        return "unknown"
+
+
 def host_info():
     """CPU model, visible cores and OMP_NUM_THREADS of the host."""
     model = None
@@ -119,7 +132,7 @@ def host_info():
                          None)
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count(),
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpu_quota": cpu_quota(),
             "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
@@ -185,8 +198,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     import kvecc
@@ -345,6 +363,11 @@ def main():
     cpu = host = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds, args.cpu_threads)
+        all_cores = os.cpu_count() or 1
+        cpu["all_cores"] = cpu_baseline(min(args.cpu_seconds, 6.0), all_cores)
+        cpu["all_cores"]["note"] = (f"{all_cores} threads = os.cpu_count(); the process's CPU "
+                                    f"quota is {cpu_quota()} (cgroup cpu.max), so threads beyond "
+                                    f"it time-share")
         host = cpu_backend_baseline(min(args.cpu_seconds, 5.0), args.cpu_threads)
     line = {
         "metric": "INT4 codewords/sec encode+decode (Golay24, L=4096) + achieved HBM GB/s",

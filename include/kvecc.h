@@ -266,6 +266,20 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
                               int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
                               int64_t layer, int codec, int interp, void *k_out, void *v_out,
                               int out_dtype, uint64_t *stats, void *stream);
+/* kvecc_shim_read over `batch` sequences in one call: sequence b reads its first
+ * ctx tokens through block_table row b (block_table[b * table_stride + lb],
+ * table_stride >= ceil(ctx / block_size)); k_out / v_out are [batch, hkv, ctx,
+ * d].  Golay caches with d % 8 == 0 take the wave-tile kernel (one launch for
+ * every sequence and both sides; the fused decode BASELINE's north_star
+ * measures); the other codecs launch once per sequence.  A negative block id
+ * reads as zeros (no statistics) instead of faulting.  batch 1 is
+ * kvecc_shim_read. */
+KVECC_API int kvecc_shim_read_batch(const void *k_cache, const void *v_cache, const float *k_scales,
+                                    const float *v_scales, const int32_t *block_table,
+                                    int64_t table_stride, int64_t batch, int64_t ctx, int64_t hkv,
+                                    int64_t d, int64_t num_layers, int64_t block_size, int64_t layer,
+                                    int codec, int interp, void *k_out, void *v_out, int out_dtype,
+                                    uint64_t *stats, void *stream);
 
 /* ---- Paged decode attention with inline ECC decode ---------------------------- */
 /* attention_ecc.py:620-780 (paged_attention_ecc) + :265-427 (kernel): one query
@@ -273,8 +287,10 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
  * (codec H84: uint8, double errors keep their data; GOLAY: int32, uncorrectable
  * data kept; GOLAY_PACKED: 3-byte codewords, rows of KVECC_GOLAY_PACKED_ROW bytes), block_table [batch, max_blocks] int32 (-1 = no block, token
  * skipped), context_lens [batch] int32 (<= max_context_len; <= 0 means
- * max_blocks*block_size), out [batch, heads, head_dim] in q_dtype (0 for an empty
- * context).  Query head h reads cache head h / (heads / kv_heads).  `workspace`:
+ * max_blocks*block_size), out [batch, heads, head_dim] in q_dtype.  A sequence
+ * with no valid token (context_len <= 0 or only -1 blocks) gets the reference's
+ * values: -8.0 in every lane for H84 (its kernel's -1e20 masking,
+ * attention_ecc.py:342,391-423), 0 for Golay (reference_attention_ecc).  Query head h reads cache head h / (heads / kv_heads).  `workspace`:
  * kvecc_paged_attention_workspace(...) floats.  head_dim <= 256. */
 KVECC_API int64_t kvecc_paged_attention_workspace(int64_t batch, int64_t heads, int64_t head_dim,
                                                   int64_t max_context_len);
@@ -357,6 +373,13 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
                                   int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
                                   int64_t layer, int codec, int interp, void *k_out, void *v_out,
                                   int out_dtype, uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_shim_read_batch(const void *k_cache, const void *v_cache,
+                                        const float *k_scales, const float *v_scales,
+                                        const int32_t *block_table, int64_t table_stride,
+                                        int64_t batch, int64_t ctx, int64_t hkv, int64_t d,
+                                        int64_t num_layers, int64_t block_size, int64_t layer,
+                                        int codec, int interp, void *k_out, void *v_out,
+                                        int out_dtype, uint64_t *stats, int threads);
 KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const void *k_cache,
                                         const void *v_cache, const int32_t *block_table,
                                         const int32_t *context_lens, const float *k_scales,

@@ -20,8 +20,17 @@
 // groups merge through LDS.  The split's (max, sum, acc[D]) go to a workspace
 // that a second small launch combines.  Query head h reads cache head
 // h / (H / Hkv) (the reference indexes cache head h, which only agrees without
-// GQA).  Numerics: fp32 throughout, expf; the result differs from the
-// reference's sequential online softmax only by fp32 summation order.
+// GQA).  Numerics: fp32 throughout, expf.  The result differs from the
+// reference's sequential online softmax by fp32 summation order and, for Golay,
+// by the -8 fold: the kernel sums q*n and p*s*n over the raw nibbles and
+// subtracts 8*sum(q) / 8*sum(p*s) once per split (acc - 8*psum), which loses a
+// few bits when the values are small against 8*scale (bounded by the
+// long-context test in tests/test_attention.py).  A context with no valid
+// token (context_len <= 0, or only -1 blocks) gives the reference's values:
+// Hamming(8,4) -8.0 in every lane (its kernel scores invalid tokens -1e20, the
+// same as its initial max, so each accumulates weight 1 on the masked row
+// decode(0) - 8 = -8, attention_ecc.py:342,391-423), Golay 0
+// (reference_attention_ecc's torch.zeros, :806-807,885-886).
 #include "kvecc_internal.h"
 
 namespace kvecc {
@@ -84,6 +93,7 @@ struct AttnArgs {
   int64_t layers, layer, bs, max_blocks, nsplit, split;
   uint32_t cache_bytes, scale_bytes;  // buffer-load bounds (BUF kernels)
   float sm_scale;
+  float empty_value;          // output when a (b, h) has no valid token
   const uint16_t *par, *cor;  // Golay tables
   const uint32_t *atab;       // Golay spread tables (KVECC_ATTN_GOLAY_SPREAD)
 };
@@ -102,13 +112,18 @@ struct Chunk {
                                            int c) {
     if constexpr (CODEC == KVECC_CODEC_H84) {
       const uint32_t off = (uint32_t)row * (uint32_t)a.d + 4u * VEC * c;
+      if constexpr (VEC % 4 == 0) {
 #pragma unroll
-      for (int k = 0; k < VEC; k += 4) {
-        const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * k, 0, 0));
-        w[k] = v.x;
-        w[k + 1 < VEC ? k + 1 : k] = v.y;
-        w[k + 2 < VEC ? k + 2 : k] = v.z;
-        w[k + 3 < VEC ? k + 3 : k] = v.w;
+        for (int k = 0; k < VEC; k += 4) {
+          const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * k, 0, 0));
+          w[k] = v.x;
+          w[k + 1] = v.y;
+          w[k + 2] = v.z;
+          w[k + 3] = v.w;
+        }
+      } else {  // head_dim % 16 != 0: one dword per word (VEC 1 or 2)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0);
       }
     } else if constexpr (CODEC == KVECC_CODEC_GOLAY_PACKED) {
       static_assert(CODEC != KVECC_CODEC_GOLAY_PACKED || VEC == 4, "packed lanes own 4 codewords");
@@ -125,7 +140,7 @@ struct Chunk {
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
     if constexpr (CODEC == KVECC_CODEC_H84) {
       const uint8_t *p = reinterpret_cast<const uint8_t *>(cache) + row * a.d + 4 * VEC * c;
-      if (VEC % 4 == 0) {
+      if constexpr (VEC % 4 == 0) {
 #pragma unroll
         for (int k = 0; k < VEC; k += 4) {
           const u32x4 v = reinterpret_cast<const u32x4 *>(p)[k / 4];
@@ -463,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) 
     float acc = 0.0f;
 #pragma unroll 4
     for (int64_t s = 0; s < a.nsplit; ++s) acc += ws[s * stride + 2 + di] * wt[s];
-    out[di] = from_f32<T>(L > 0.0f ? acc / L : 0.0f);  // empty context -> 0 (:424)
+    out[di] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);  // no valid token: see the header
   }
 }
 
@@ -614,6 +629,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   if (a.nsplit > kMaxSplits)
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
   a.sm_scale = sm_scale;
+  a.empty_value = codec == KVECC_CODEC_H84 ? -8.0f : 0.0f;
   {
     const int64_t rows_total = num_blocks * num_layers * kv_heads * block_size;
     const int64_t cb = rows_total * (codec == KVECC_CODEC_H84            ? head_dim

@@ -746,9 +746,33 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
   return KVECC_OK;
 }
 
+KVECC_API int kvecc_cpu_shim_read_batch(const void *k_cache, const void *v_cache,
+                                        const float *k_scales, const float *v_scales,
+                                        const int32_t *block_table, int64_t table_stride,
+                                        int64_t batch, int64_t ctx, int64_t hkv, int64_t d,
+                                        int64_t num_layers, int64_t block_size, int64_t layer,
+                                        int codec, int interp, void *k_out, void *v_out,
+                                        int out_dtype, uint64_t *stats, int threads) {
+  if (batch < 0) return set_error(KVECC_EINVAL, "cpu_shim_read_batch: negative batch");
+  if (batch > 1 && ctx > 0 && table_stride < (ctx + block_size - 1) / std::max<int64_t>(block_size, 1))
+    return set_error(KVECC_EINVAL, "cpu_shim_read_batch: table stride too small");
+  const int64_t osz = out_dtype == KVECC_F32 ? 4 : 2;
+  for (int64_t b = 0; b < batch; ++b) {
+    const int64_t off = b * hkv * ctx * d * osz;
+    const int rc = kvecc_cpu_shim_read(k_cache, v_cache, k_scales, v_scales, block_table + b * table_stride,
+                                       ctx, hkv, d, num_layers, block_size, layer, codec, interp,
+                                       reinterpret_cast<char *>(k_out) + off,
+                                       reinterpret_cast<char *>(v_out) + off, out_dtype, stats, threads);
+    if (rc != KVECC_OK) return rc;
+  }
+  return KVECC_OK;
+}
+
 // ---- paged decode attention (host twin of attention.hip) ---------------------
 // The reference's order exactly: one (b, h) at a time, tokens in order, online
-// softmax in fp32 (attention_ecc.py:355-427).
+// softmax in fp32 (attention_ecc.py:355-427).  No valid token: Hamming(8,4)
+// -8.0 per lane (the reference kernel's -1e20 masking, :342,391-423), Golay 0
+// (reference_attention_ecc, :806-807,885-886).
 KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const void *k_cache,
                                         const void *v_cache, const int32_t *block_table,
                                         const int32_t *context_lens, const float *k_scales,
@@ -833,7 +857,7 @@ KVECC_API int kvecc_cpu_paged_attention(const void *query, int q_dtype, const vo
         m = mn;
       }
       for (int64_t j = 0; j < head_dim; ++j)
-        store_y(out, q_dtype, bh * head_dim + j, l > 0.0f ? acc[j] / l : 0.0f);
+        store_y(out, q_dtype, bh * head_dim + j, l > 0.0f ? acc[j] / l : golay ? 0.0f : -8.0f);
     }
   });
   return KVECC_OK;

@@ -327,10 +327,10 @@ __device__ __forceinline__ void row_tiles(const uint8_t *in, int64_t rows, int r
                 false, lane);
     // lanes read each other's LDS bytes through other types in the next phase:
     // keep the compiler from moving LDS accesses across the phase boundaries
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (t + stride < ntiles && full(t + stride)) nxt.prefetch(in + (t + stride) * tile_bytes, nvec, lane);
     body(r0, nr);
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
   }
 }
 
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void golay_encode_rows_tiled_kernel(
       }
     }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     wave_copy(reinterpret_cast<uint8_t *>(cw + r0 * g), reinterpret_cast<const uint8_t *>(tcw),
               nr * g * 4, aligned16 && nr == tl.rows, true, lane);
   });
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
       }
     }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     wave_copy(nib + r0 * d, tout, nr * d, aligned16 && nr == tl.rows, true, lane);
   });
   if (stats) flush_stats2(stats, bits, unc);

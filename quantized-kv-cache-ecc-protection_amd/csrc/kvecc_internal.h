@@ -34,7 +34,8 @@ const uint16_t *golay_correct_table_dev();
 // byte, spread(x) = x&15 | (x>>4&15)<<8 | (x>>8&15)<<16, so a value converts
 // with one v_cvt_f32_ubyteN:
 //   [0, 4096)    spread(d) | parity(d) << 20
-//   [4096, 8192) spread(data error of syndrome s)   (0 when uncorrectable)
+//   [4096, 8192) spread(data error of syndrome s) | count(s) << 24
+//                (spread part 0 and count 4 when uncorrectable)
 const uint32_t *golay_attn_table_dev();
 // host-side table builders (product copy, independent of the test oracle)
 void build_golay_parity_table(uint16_t *out4096);
@@ -77,6 +78,17 @@ inline unsigned grid_for(int64_t work, int64_t per_block, int per_cu = 8) {
 inline bool aligned(const void *p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
 
 // ---- device helpers ----------------------------------------------------------
+
+// Phase boundary of a wave-private LDS tile (lanes exchange data through LDS
+// with accesses of different vector types).  wave_barrier alone is only a
+// scheduling/convergence hint; the wavefront-scope release/acquire fences make
+// the LDS ordering a guarantee of the memory model instead of current codegen
+// (they emit s_waitcnt lgkmcnt, no cache maintenance for LDS).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // element conversions of the fused kernels (fp32 / fp16 / bf16, RNE on the way out)
 template <typename T>

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_kernel(
       st_stream(reinterpret_cast<u32x3v *>(nib + (G0 + g * kWave + lane) * 3), u32x3v{n[0], n[1], n[2]});
       if (WITH_FLAGS) st_stream(flags + G0 + g * kWave + lane, (uint8_t)fl);
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
   }
   if (WITH_STATS) flush_stats2<kPkBlock>(stats, bits, unc);
 }
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
     for (int k = 0; k < kV; ++k) reinterpret_cast<u32x4 *>(mine)[lane + k * kWave] = nxt[k];
     // lanes read each other's bytes through other vector types: keep the
     // compiler from moving LDS accesses across the phase boundaries
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (t + gridDim.x < ntiles) {
 #pragma unroll
       for (int k = 0; k < kV; ++k) nxt[k] = ld_stream(src_of(t + gridDim.x) + lane + k * kWave);
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
       st_stream(reinterpret_cast<u32x3v *>(nib + (G0 + g * kWave + lane) * 3), u32x3v{n[0], n[1], n[2]});
       if (WITH_FLAGS) st_stream(flags + G0 + g * kWave + lane, (uint8_t)fl);
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
   }
   if (WITH_STATS) flush_stats2<kPkBlock>(stats, bits, unc);
 }

@@ -4,6 +4,7 @@
 // (the B matrix of ecc_codecs/triton_kernels/config.py:329-347), and uploaded
 // once per device; they replace the per-device syndrome-table cache of
 // golay_triton.py:304-330.
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -33,9 +34,9 @@ int check_launch(const char *what) {
 constexpr int kMaxDev = 64;
 static std::mutex g_mu;
 static int g_cu[kMaxDev];
-static uint16_t *g_parity[kMaxDev];
-static uint16_t *g_correct[kMaxDev];
-static uint32_t *g_attn[kMaxDev];
+static std::atomic<uint16_t *> g_parity[kMaxDev];
+static std::atomic<uint16_t *> g_correct[kMaxDev];
+static std::atomic<uint32_t *> g_attn[kMaxDev];
 
 int current_device() {
   int d = 0;
@@ -112,70 +113,53 @@ void build_golay_correct_table(uint16_t *out) {
 
 static uint32_t spread12(uint32_t x) { return (x & 0xFu) | (x >> 4 & 0xFu) << 8 | (x >> 8 & 0xFu) << 16; }
 
-static int ensure_attn_table(int d) {
+// All Golay device tables of a device in one allocation, built together the
+// first time any of them is needed (kvecc_init_device builds them eagerly, so
+// no upload ever happens inside a HIP-graph capture): parity[4096] and
+// correct[4096] as uint16, then the attention spread tables (uint32[8192]).
+// The pointers are published through atomics after the upload completes.
+static int ensure_tables(int d) {
   if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_attn[d]) return KVECC_OK;
-  uint16_t par[4096], cor[4096];
-  build_golay_parity_table(par);
-  build_golay_correct_table(cor);
-  static uint32_t host[8192];
+  if (g_attn[d].load(std::memory_order_acquire)) return KVECC_OK;
+  struct Host {
+    uint16_t par[4096], cor[4096];
+    uint32_t attn[8192];
+  };
+  static Host host;  // guarded by g_mu
+  build_golay_parity_table(host.par);
+  build_golay_correct_table(host.cor);
   for (uint32_t i = 0; i < 4096; ++i) {
-    host[i] = spread12(i) | (uint32_t)par[i] << 20;
-    host[4096 + i] = spread12(cor[i] & 0xFFFu);
+    host.attn[i] = spread12(i) | (uint32_t)host.par[i] << 20;
+    // correction half: data bits of the error pattern spread one nibble per
+    // byte, the error count (0-3, 4 = uncorrectable) in byte 3
+    host.attn[4096 + i] = spread12(host.cor[i] & 0xFFFu) | (uint32_t)(host.cor[i] >> 12) << 24;
   }
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
   if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
-  uint32_t *buf = nullptr;
-  hipError_t e = hipMalloc(&buf, sizeof(host));
-  if (e == hipSuccess) e = hipMemcpy(buf, host, sizeof(host), hipMemcpyHostToDevice);
-  (void)hipSetDevice(prev);
-  if (e != hipSuccess) return set_error(KVECC_EHIP, "golay attention table upload: %s", hipGetErrorString(e));
-  g_attn[d] = buf;
-  return KVECC_OK;
-}
-
-static int ensure_tables(int d) {
-  if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_parity[d] && g_correct[d]) return KVECC_OK;
-  uint16_t host[2][4096];
-  build_golay_parity_table(host[0]);
-  build_golay_correct_table(host[1]);
-  int prev = 0;
-  if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
-  if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
-  uint16_t *buf = nullptr;
-  hipError_t e = hipMalloc(&buf, sizeof(host));
-  if (e == hipSuccess) e = hipMemcpy(buf, host, sizeof(host), hipMemcpyHostToDevice);
+  Host *buf = nullptr;
+  hipError_t e = hipMalloc(&buf, sizeof(Host));
+  if (e == hipSuccess) e = hipMemcpy(buf, &host, sizeof(Host), hipMemcpyHostToDevice);
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return set_error(KVECC_EHIP, "golay table upload: %s", hipGetErrorString(e));
-  g_parity[d] = buf;
-  g_correct[d] = buf + 4096;
+  g_parity[d].store(buf->par, std::memory_order_release);
+  g_correct[d].store(buf->cor, std::memory_order_release);
+  g_attn[d].store(buf->attn, std::memory_order_release);  // last: the "built" flag
   return KVECC_OK;
 }
 
-const uint16_t *golay_parity_table_dev() {
-  int d = current_device();
-  if (d >= 0 && d < kMaxDev && g_parity[d]) return g_parity[d];
+template <typename P>
+static const P *table_dev(std::atomic<P *> *tabs) {
+  const int d = current_device();
+  if (d >= 0 && d < kMaxDev && g_attn[d].load(std::memory_order_acquire)) return tabs[d].load(std::memory_order_acquire);
   if (ensure_tables(d) != KVECC_OK) return nullptr;
-  return g_parity[d];
+  return tabs[d].load(std::memory_order_acquire);
 }
 
-const uint32_t *golay_attn_table_dev() {
-  int d = current_device();
-  if (d >= 0 && d < kMaxDev && g_attn[d]) return g_attn[d];
-  if (ensure_attn_table(d) != KVECC_OK) return nullptr;
-  return g_attn[d];
-}
-
-const uint16_t *golay_correct_table_dev() {
-  int d = current_device();
-  if (d >= 0 && d < kMaxDev && g_correct[d]) return g_correct[d];
-  if (ensure_tables(d) != KVECC_OK) return nullptr;
-  return g_correct[d];
-}
+const uint16_t *golay_parity_table_dev() { return table_dev(g_parity); }
+const uint16_t *golay_correct_table_dev() { return table_dev(g_correct); }
+const uint32_t *golay_attn_table_dev() { return table_dev(g_attn); }
 
 }  // namespace kvecc
 

@@ -19,6 +19,8 @@
 // Cache layout (SimpleBlockManager): codewords [blocks, layers, Hkv, bs, P]
 // with P = D (uint8) or ceil(D/3) (int32 Golay); scales fp32 [blocks, layers,
 // Hkv, bs]; logical block b of the sequence is physical block table[b].
+#include <algorithm>
+
 #include "kvecc_internal.h"
 
 namespace kvecc {
@@ -221,6 +223,202 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
   if (STATS) flush_stats2(a.stats, bits, unc);
 }
 
+// ---- Golay read through wave tiles (the fused decode the headline names) -------
+// A wave owns a tile: up to `tr` consecutive token rows of one (side, sequence,
+// head, block) -- contiguous codewords in the cache, a contiguous run of the
+// [hkv, ctx, d] output.  Phase 1: each lane takes groups of 4 codewords of a
+// row (one 16-byte buffer load; packed: 12 bytes), decodes them through the
+// spread tables in LDS (2 lookups + a v_bitop3 per codeword, nibbles one per
+// byte, the error count in byte 3 of the correction entry) and writes 12
+// nibble bytes to the wave's LDS tile (rows `lr` bytes apart).  Phase 2: each
+// lane takes 8 consecutive values of a row (two LDS dwords), dequantizes
+// (q - 8) * scale in fp32 and writes them with one 16-byte store (fp16/bf16).
+// The next tile's loads are issued before phase 2 (register prefetch).  HBM
+// traffic is the algorithm's: 4 B (3 B packed) per codeword in, d * sizeof(TO)
+// per row out, 4 B of scale per row.
+constexpr int kTileBlock = 512;                    // 8 waves per workgroup
+constexpr int kTileWaves = kTileBlock / kWave;
+constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
+constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
+
+struct ShimTileArgs {
+  const void *cache[2];
+  const float *scales[2];
+  void *out[2];           // [batch, hkv, ctx, d]
+  const int32_t *table;   // [batch, tstride]
+  const uint32_t *atab;   // spread tables (golay_attn_table_dev)
+  uint64_t *stats;
+  uint32_t tstride, hkv, d, g, layers, bs, layer, ctx;
+  uint32_t gpr;           // 4-codeword groups per row: ceil(g / 4)
+  uint32_t lr;            // LDS bytes per staged row: 12 * gpr
+  uint32_t tr;            // rows per tile
+  uint32_t tpb;           // tiles per block: ceil(bs / tr)
+  uint32_t nlb;           // logical blocks covering ctx
+  uint32_t units;         // 2 * batch * hkv * nlb * tpb
+  uint32_t rowb;          // bytes per cache row (4g int32, KVECC_GOLAY_PACKED_ROW(g) packed)
+};
+
+// a wave's tile: rows [row0, row0 + rows) of one cache side (wave-uniform)
+struct ShimTile {
+  uint32_t side, rows, pos0, bh;
+  int64_t row0;  // first cache row; -1 = no physical block (zeros out)
+};
+
+__device__ __forceinline__ ShimTile shim_tile(const ShimTileArgs &a, uint32_t u) {
+  ShimTile t;
+  const uint32_t per_side = a.units / 2;
+  t.side = u >= per_side ? 1u : 0u;
+  u -= t.side * per_side;
+  const uint32_t ch = u % a.tpb;
+  u /= a.tpb;
+  const uint32_t lb = u % a.nlb;
+  t.bh = u / a.nlb;
+  const uint32_t b = t.bh / a.hkv, h = t.bh - b * a.hkv;
+  t.pos0 = lb * a.bs + ch * a.tr;
+  t.rows = t.pos0 < a.ctx ? min(min(a.tr, a.bs - ch * a.tr), a.ctx - t.pos0) : 0u;
+  const int32_t blk = a.table[(int64_t)b * a.tstride + lb];
+  t.row0 = blk < 0 ? -1 : (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + ch * a.tr;
+  return t;
+}
+
+template <bool PACKED>
+__device__ __forceinline__ void tile_issue(const ShimTileArgs &a, const ShimTile &t, uint32_t lane,
+                                           u32x4 (&w)[kTileGroups]) {
+  // buffer descriptor over exactly the tile's bytes: a row's last group reads
+  // past its row (the next row's first codeword, or 0 past the tile), ignored
+  const char *base = reinterpret_cast<const char *>(a.cache[t.side]) + (t.row0 < 0 ? 0 : t.row0) * (int64_t)a.rowb;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char *>(base), 0, t.row0 < 0 ? 0 : (int)(t.rows * a.rowb), 0x00020000);
+  const uint32_t groups = a.tr * a.gpr;
+#pragma unroll
+  for (int i = 0; i < kTileGroups; ++i) {
+    if (i * kWave >= (int)groups) break;  // uniform
+    const uint32_t f = lane + kWave * i;
+    const uint32_t r = f / a.gpr, q = f - r * a.gpr;
+    const uint32_t off = (r < t.rows ? r : 0u) * a.rowb + (PACKED ? 12u : 16u) * q;
+    if (PACKED) {  // 4 three-byte codewords from 3 dwords
+      const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+      w[i] = u32x4{v[0], __builtin_amdgcn_alignbyte(v[1], v[0], 3), __builtin_amdgcn_alignbyte(v[2], v[1], 2),
+                   v[2] >> 8};
+    } else {
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  }
+}
+
+template <typename TO>
+__device__ __forceinline__ void store8(TO *dst, const float (&v)[8]) {
+  if constexpr (sizeof(TO) == 4) {
+    reinterpret_cast<float4 *>(dst)[0] = float4{v[0], v[1], v[2], v[3]};
+    reinterpret_cast<float4 *>(dst)[1] = float4{v[4], v[5], v[6], v[7]};
+  } else {
+    uint32_t p[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      p[k] = (uint32_t)__builtin_bit_cast(uint16_t, from_f32<TO>(v[2 * k])) |
+             (uint32_t)__builtin_bit_cast(uint16_t, from_f32<TO>(v[2 * k + 1])) << 16;
+    *reinterpret_cast<u32x4 *>(dst) = u32x4{p[0], p[1], p[2], p[3]};
+  }
+}
+
+template <typename TO, bool STATS, bool PACKED>
+__global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  {
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(tab);
+#pragma unroll
+    for (int i = threadIdx.x; i < 2048; i += kTileBlock) dst[i] = src[i];
+  }
+  __syncthreads();
+  // wave-uniform from here on (readfirstlane: the compiler cannot prove it)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  uint8_t *stage = stage_all[wave];
+  const uint32_t lane = threadIdx.x % kWave;
+  const uint32_t nwaves = gridDim.x * kTileWaves;
+  const uint32_t groups = a.tr * a.gpr;  // <= 64 * kTileGroups (host check)
+  const uint32_t d8 = a.d / 8;
+  uint32_t bits = 0, unc = 0;
+
+  uint32_t u = blockIdx.x * kTileWaves + wave;
+  if (u >= a.units) return;  // no workgroup barrier below: waves retire independently
+  ShimTile cur = shim_tile(a, u);
+  u32x4 w[kTileGroups];
+  tile_issue<PACKED>(a, cur, lane, w);
+  for (;;) {
+    // ---- phase 1: decode 4 codewords per group into the LDS tile --------------
+#pragma unroll
+    for (int i = 0; i < kTileGroups; ++i) {
+      if (i * kWave >= (int)groups) break;  // uniform
+      const uint32_t f = lane + kWave * i;
+      const uint32_t r = f / a.gpr, q = f - r * a.gpr;
+      if (r < cur.rows) {
+        uint32_t sp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t cw = w[i][k];
+          const uint32_t p = tab[cw & 0xFFFu];
+          // syndrome = parity bits ^ parity(data): (cw >> 12 ^ p >> 20) & 0xFFF
+          const uint32_t e = tab[4096 + (((cw >> 12) ^ (p >> 20)) & 0xFFFu)];
+          sp[k] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
+          if (STATS && cur.row0 >= 0 && 4 * q + k < a.g) {
+            const uint32_t c = e >> 24;  // 0-3 bits corrected, 4 = uncorrectable
+            bits += c & 3u;
+            unc += c >> 2;
+          }
+        }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(stage + r * a.lr + 12 * q);
+        dst[0] = sp[0] | sp[1] << 24;
+        dst[1] = sp[1] >> 8 | sp[2] << 16;
+        dst[2] = sp[2] >> 16 | sp[3] << 8;
+      }
+    }
+    wave_lds_sync();
+    // ---- prefetch the next tile's codewords ------------------------------------
+    const ShimTile t = cur;
+    u += nwaves;
+    const bool more = u < a.units;
+    if (more) {
+      cur = shim_tile(a, u);
+      tile_issue<PACKED>(a, cur, lane, w);
+    }
+    // ---- phase 2: dequantize 8 values per lane, 16-byte stores -----------------
+    const uint32_t tasks = t.rows * d8;
+    const float *sc = a.scales[t.side] + (t.row0 < 0 ? 0 : t.row0);
+    TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
+    for (uint32_t v = lane; v < tasks; v += kWave) {
+      const uint32_t r = v / d8, j = v - r * d8;
+      float o[8];
+      if (t.row0 >= 0) {
+        const float s = sc[r];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + 8 * j);
+        const uint32_t lo = src[0], hi = src[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = ((float)(lo >> (8 * e) & 0xFFu) - 8.0f) * s;
+          o[4 + e] = ((float)(hi >> (8 * e) & 0xFFu) - 8.0f) * s;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0.0f;
+      }
+      store8<TO>(out + (int64_t)r * a.d + 8 * j, o);
+    }
+    if (!more) break;
+    wave_lds_sync();  // phase 2 reads done before the next phase 1 overwrites
+  }
+  if (STATS) {  // wave reduction, one atomic pair per wave
+    bits = wave_sum(bits);
+    unc = wave_sum(unc);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + ((blockIdx.x * kTileWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
+      if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+    }
+  }
+}
+
 template <typename T, int CODEC>
 static void launch_write_nb(const ShimWriteArgs &a, unsigned grid, hipStream_t st) {
   constexpr int NB = CODEC == KVECC_CODEC_GOLAY || CODEC == KVECC_CODEC_GOLAY_PACKED ? 24
@@ -278,6 +476,19 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
   } else {
     launch_read_bytes<TO, KVECC_CODEC_NONE, false>(a, grid, st);
   }
+}
+
+template <typename TO>
+static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * 3);
+  if (a.stats && packed)
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
+  else if (a.stats)
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
+  else if (packed)
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
+  else
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
 }
 
 }  // namespace kvecc
@@ -377,13 +588,13 @@ KVECC_API int kvecc_shim_write_strided(const void *k, const void *v, int64_t k_b
                          num_layers, block_size, layer, stream);
 }
 
-KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,
-                              const float *v_scales, const int32_t *block_table, int64_t ctx,
-                              int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
-                              int64_t layer, int codec, int interp, void *k_out, void *v_out,
-                              int out_dtype, uint64_t *stats, void *stream) {
-  if (ctx < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_read: negative size");
-  if (ctx == 0 || hkv == 0 || d == 0) return KVECC_OK;
+static int shim_read_impl(const void *k_cache, const void *v_cache, const float *k_scales,
+                          const float *v_scales, const int32_t *block_table, int64_t tstride,
+                          int64_t batch, int64_t ctx, int64_t hkv, int64_t d, int64_t num_layers,
+                          int64_t block_size, int64_t layer, int codec, int interp, void *k_out,
+                          void *v_out, int out_dtype, uint64_t *stats, void *stream) {
+  if (batch < 0 || ctx < 0 || hkv < 0 || d < 0) return set_error(KVECC_EINVAL, "shim_read: negative size");
+  if (batch == 0 || ctx == 0 || hkv == 0 || d == 0) return KVECC_OK;
   if (codec < KVECC_CODEC_NONE || codec > KVECC_CODEC_GOLAY_PACKED)
     return set_error(KVECC_EINVAL, "shim_read: bad codec %d", codec);
   const bool golay = codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED;
@@ -395,34 +606,99 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
     return set_error(KVECC_EINVAL, "shim_read: bad cache geometry");
   if (!k_cache || !v_cache || !k_scales || !v_scales || !block_table || !k_out || !v_out)
     return set_error(KVECC_EINVAL, "shim_read: null pointer");
+  if (batch > 1 && tstride < cdiv(ctx, block_size))
+    return set_error(KVECC_EINVAL, "shim_read: table stride %lld < %lld blocks", (long long)tstride,
+                     (long long)cdiv(ctx, block_size));
   if (2 * hkv * ctx * d > 0x7FFFFFFFLL || num_layers * hkv * block_size > 0x7FFFFFFFLL)
     return set_error(KVECC_EINVAL, "shim_read: sizes exceed 32-bit indexing");
-  ShimReadArgs a;
-  a.geo = {block_table, (uint32_t)hkv, (uint32_t)d,
-           (uint32_t)(golay ? (d + 2) / 3 : d), (uint32_t)num_layers,
-           (uint32_t)block_size, (uint32_t)layer};
-  a.cache[0] = k_cache;
-  a.cache[1] = v_cache;
-  a.scales[0] = k_scales;
-  a.scales[1] = v_scales;
-  a.out[0] = k_out;
-  a.out[1] = v_out;
-  a.ctx = (uint32_t)ctx;
-  a.stats = stats;
-  a.par = a.cor = nullptr;
-  if (golay) {
-    a.par = golay_parity_table_dev();
-    a.cor = golay_correct_table_dev();
-    if (!a.par || !a.cor) return KVECC_EHIP;
-  }
+  if (out_dtype != KVECC_F32 && out_dtype != KVECC_F16 && out_dtype != KVECC_BF16)
+    return set_error(KVECC_EINVAL, "shim_read: bad dtype %d", out_dtype);
   hipStream_t st = as_stream(stream);
-  switch (out_dtype) {
-    case KVECC_F32: launch_read<float>(codec, interp, a, st); break;
-    case KVECC_F16: launch_read<__half>(codec, interp, a, st); break;
-    case KVECC_BF16: launch_read<__hip_bfloat16>(codec, interp, a, st); break;
-    default: return set_error(KVECC_EINVAL, "shim_read: bad dtype %d", out_dtype);
+  const int64_t g = golay ? (d + 2) / 3 : d;
+  const int64_t gpr = cdiv(g, 4), lr = 12 * gpr;
+  if (golay && d % 8 == 0 && lr <= kTileStage && 2 * batch * hkv * cdiv(ctx, block_size) * block_size <= 0x7FFFFFFFLL) {
+    // Golay: the wave-tile kernel, all sequences in one launch
+    ShimTileArgs a;
+    a.cache[0] = k_cache;
+    a.cache[1] = v_cache;
+    a.scales[0] = k_scales;
+    a.scales[1] = v_scales;
+    a.out[0] = k_out;
+    a.out[1] = v_out;
+    a.table = block_table;
+    a.atab = golay_attn_table_dev();
+    if (!a.atab) return KVECC_EHIP;
+    a.stats = stats;
+    a.tstride = (uint32_t)tstride;
+    a.hkv = (uint32_t)hkv;
+    a.d = (uint32_t)d;
+    a.g = (uint32_t)g;
+    a.layers = (uint32_t)num_layers;
+    a.bs = (uint32_t)block_size;
+    a.layer = (uint32_t)layer;
+    a.ctx = (uint32_t)ctx;
+    a.gpr = (uint32_t)gpr;
+    a.lr = (uint32_t)lr;
+    a.tr = (uint32_t)std::min<int64_t>({block_size, kTileStage / lr, (int64_t)kWave * kTileGroups / gpr});
+    a.tpb = (uint32_t)cdiv(block_size, a.tr);
+    a.nlb = (uint32_t)cdiv(ctx, block_size);
+    a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+    a.rowb = (uint32_t)(codec == KVECC_CODEC_GOLAY_PACKED ? KVECC_GOLAY_PACKED_ROW(g) : 4 * g);
+    const bool pk = codec == KVECC_CODEC_GOLAY_PACKED;
+    switch (out_dtype) {
+      case KVECC_F32: launch_read_tiles<float>(pk, a, st); break;
+      case KVECC_F16: launch_read_tiles<__half>(pk, a, st); break;
+      default: launch_read_tiles<__hip_bfloat16>(pk, a, st); break;
+    }
+    return check_launch("shim_read");
+  }
+  const int64_t osz = out_dtype == KVECC_F32 ? 4 : 2;
+  for (int64_t b = 0; b < batch; ++b) {  // one launch per sequence
+    ShimReadArgs a;
+    a.geo = {block_table + b * tstride, (uint32_t)hkv, (uint32_t)d, (uint32_t)g, (uint32_t)num_layers,
+             (uint32_t)block_size, (uint32_t)layer};
+    a.cache[0] = k_cache;
+    a.cache[1] = v_cache;
+    a.scales[0] = k_scales;
+    a.scales[1] = v_scales;
+    a.out[0] = reinterpret_cast<char *>(k_out) + b * hkv * ctx * d * osz;
+    a.out[1] = reinterpret_cast<char *>(v_out) + b * hkv * ctx * d * osz;
+    a.ctx = (uint32_t)ctx;
+    a.stats = stats;
+    a.par = a.cor = nullptr;
+    if (golay) {
+      a.par = golay_parity_table_dev();
+      a.cor = golay_correct_table_dev();
+      if (!a.par || !a.cor) return KVECC_EHIP;
+    }
+    switch (out_dtype) {
+      case KVECC_F32: launch_read<float>(codec, interp, a, st); break;
+      case KVECC_F16: launch_read<__half>(codec, interp, a, st); break;
+      default: launch_read<__hip_bfloat16>(codec, interp, a, st); break;
+    }
   }
   return check_launch("shim_read");
+}
+
+KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const float *k_scales,
+                              const float *v_scales, const int32_t *block_table, int64_t ctx,
+                              int64_t hkv, int64_t d, int64_t num_layers, int64_t block_size,
+                              int64_t layer, int codec, int interp, void *k_out, void *v_out,
+                              int out_dtype, uint64_t *stats, void *stream) {
+  return shim_read_impl(k_cache, v_cache, k_scales, v_scales, block_table, 0, 1, ctx, hkv, d,
+                        num_layers, block_size, layer, codec, interp, k_out, v_out, out_dtype, stats,
+                        stream);
+}
+
+KVECC_API int kvecc_shim_read_batch(const void *k_cache, const void *v_cache, const float *k_scales,
+                                    const float *v_scales, const int32_t *block_table,
+                                    int64_t table_stride, int64_t batch, int64_t ctx, int64_t hkv,
+                                    int64_t d, int64_t num_layers, int64_t block_size, int64_t layer,
+                                    int codec, int interp, void *k_out, void *v_out, int out_dtype,
+                                    uint64_t *stats, void *stream) {
+  return shim_read_impl(k_cache, v_cache, k_scales, v_scales, block_table, table_stride, batch, ctx,
+                        hkv, d, num_layers, block_size, layer, codec, interp, k_out, v_out, out_dtype,
+                        stats, stream);
 }
 
 }  // extern "C"

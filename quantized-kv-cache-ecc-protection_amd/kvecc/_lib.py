@@ -56,6 +56,8 @@ SIGNATURES = {
     "kvecc_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_write_strided": [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "kvecc_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _vp],
+    "kvecc_shim_read_batch": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int,
+                              _vp, _vp, _int, _vp, _vp],
     "kvecc_paged_attention_workspace": [_i64, _i64, _i64, _i64],
     "kvecc_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64,
                               _i64, _i64, _i64, _i64, _i64, _i64, _f32, _int, _vp, _i64, _vp],
@@ -83,6 +85,8 @@ SIGNATURES = {
     "kvecc_cpu_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _int],
     "kvecc_cpu_shim_write": [_vp, _vp, _int, _i64, _i64, _i64, _i64, _int, _int, _int, _int, _f32, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _int],
     "kvecc_cpu_shim_read": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp, _int, _vp, _int],
+    "kvecc_cpu_shim_read_batch": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int,
+                                  _int, _vp, _vp, _int, _vp, _int],
     "kvecc_cpu_paged_attention": [_vp, _int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
                                   _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _int, _int],
 }

@@ -474,6 +474,35 @@ def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=
     return k_out, v_out
 
 
+def shim_read_batch(k_cache, v_cache, k_scales, v_scales, block_table, ctx, head_dim, layer, codec,
+                    out_dtype, stats=None, interp=False, out=None):
+    """The shim's fused read (gather -> decode -> dequantize, ecc_shim.py:990-1071)
+    for every sequence of a paged cache at once: block_table [B, max_blocks]
+    int32 (row b = sequence b), caches [blocks, layers, hkv, block_size * P]
+    -> (K, V) [B, hkv, ctx, head_dim] in out_dtype (kvecc_shim_read_batch)."""
+    nb, nl, hkv, row = k_cache.shape
+    per = {"golay": (head_dim + 2) // 3, "golay_packed": (3 * ((head_dim + 2) // 3) + 3) // 4 * 4}.get(
+        codec, head_dim)
+    if row % per:
+        raise ValueError(f"cache rows of {row} words do not hold whole token rows of {per}")
+    bs = row // per
+    if block_table.dim() != 2 or block_table.dtype != torch.int32 or not block_table.is_contiguous():
+        raise ValueError("block_table must be a contiguous int32 [B, max_blocks] tensor")
+    if block_table.shape[1] * bs < ctx:
+        raise ValueError(f"block_table covers {block_table.shape[1] * bs} tokens < ctx {ctx}")
+    batch = block_table.shape[0]
+    shape = (batch, hkv, ctx, head_dim)
+    if out is None:
+        out = (torch.empty(shape, dtype=out_dtype, device=k_cache.device),
+               torch.empty(shape, dtype=out_dtype, device=k_cache.device))
+    k_out, v_out = out
+    _lib.call("kvecc_cpu_shim_read_batch", _ptr(k_cache), _ptr(v_cache), _ptr(k_scales), _ptr(v_scales),
+              _ptr(block_table), block_table.shape[1], batch, int(ctx), hkv, head_dim, nl, bs,
+              int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
+              _DT[out_dtype], _ptr(stats), NUM_THREADS)
+    return k_out, v_out
+
+
 # ============================================================================
 # Paged decode attention (host twin of ops.paged_attention_ecc)
 # ============================================================================

@@ -54,6 +54,37 @@ def trial_key(codec, ber, seed):
     return f"{codec}|{ber:.6g}|{seed}"
 
 
+def injected_elements(codec, shape):
+    """Elements the trial's flat injection draws over (its global N): INT4
+    values for the Hamming codecs, per-head-padded codewords for Golay."""
+    b, l, h, d = shape
+    return b * l * h * ((d + 2) // 3 if codec == "golay" else d)
+
+
+def stream_key(codec, seed, shape):
+    """The 32-bit Philox key base of a trial's flips.  Element `off`, bit `b`
+    draws under int32(seed*N*n_bits + off*n_bits + b) (fault_injection_triton.py
+    :247-294), so two seeds whose seed*N*n_bits agree mod 2^32
+    draw the SAME flips: with N = 2^27 and 8 bits, seeds 101 and 997 collide
+    ((997-101)*2^30 = 224*2^32)."""
+    return (seed * injected_elements(codec, shape) * N_BITS[codec]) & 0xFFFFFFFF
+
+
+def seed_aliases(cfg: MonteCarloConfig):
+    """{trial key: key of the first trial it duplicates}: same codec and BER, and
+    a seed whose Philox key base collides (stream_key).  Such trials reproduce
+    the reference's bits exactly and are NOT independent samples."""
+    first, alias = {}, {}
+    for codec, ber, seed in cfg.trials():
+        k = (codec, ber, stream_key(codec, seed, cfg.shape), cfg.data_seed)
+        key = trial_key(codec, ber, seed)
+        if k in first:
+            alias[key] = first[k]
+        else:
+            first[k] = key
+    return alias
+
+
 def shard_bounds(batch, rank, world):
     """Contiguous split of the batch axis; the first batch % world ranks get one more row."""
     base, extra = divmod(batch, world)
@@ -162,15 +193,23 @@ def run_sweep(cfg: MonteCarloConfig, shard, dist=None, rank=0):
     if shard.dev.type == "cuda":
         torch.cuda.synchronize(shard.dev)
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        dist.all_reduce(table, op=dist.ReduceOp.SUM)  # the sweep's single collective
+    if dist is not None:  # the sweep's single collective
+        if table.is_cuda and dist.get_backend() == "gloo":
+            host = table.cpu()  # gloo reduces host tensors; RCCL reduces in HBM
+            dist.all_reduce(host, op=dist.ReduceOp.SUM)
+            table.copy_(host)
+        else:
+            dist.all_reduce(table, op=dist.ReduceOp.SUM)
     rows = []
     vals = table.cpu().tolist()
+    aliases = seed_aliases(cfg)
     b, l, h, d = cfg.shape
     for i, (codec, ber, seed) in enumerate(todo):
         r = {"key": trial_key(codec, ber, seed), "codec": codec, "ber": ber, "seed": seed,
              "shape": list(cfg.shape), "values": b * l * h * d,
              **{k: int(v) for k, v in zip(STAT_NAMES, vals[i])}}
+        if r["key"] in aliases:
+            r["alias_of"] = aliases[r["key"]]
         rows.append(r)
     if rank == 0 and cfg.output and rows:
         with open(cfg.output, "a") as f:

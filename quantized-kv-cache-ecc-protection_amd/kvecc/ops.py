@@ -608,25 +608,128 @@ def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=
     return k_out, v_out
 
 
+def shim_read_batch(k_cache, v_cache, k_scales, v_scales, block_table, ctx, head_dim, layer, codec,
+                    out_dtype, stats=None, interp=False, out=None):
+    """The shim's fused read (gather -> decode -> dequantize, ecc_shim.py:990-1071)
+    for every sequence of a paged cache at once: block_table [B, max_blocks]
+    int32 (row b = sequence b), caches [blocks, layers, hkv, block_size * P]
+    -> (K, V) [B, hkv, ctx, head_dim] in out_dtype (kvecc_shim_read_batch)."""
+    nb, nl, hkv, row = k_cache.shape
+    per = {"golay": (head_dim + 2) // 3, "golay_packed": (3 * ((head_dim + 2) // 3) + 3) // 4 * 4}.get(
+        codec, head_dim)
+    if row % per:
+        raise ValueError(f"cache rows of {row} words do not hold whole token rows of {per}")
+    bs = row // per
+    if block_table.dim() != 2 or block_table.dtype != torch.int32 or not block_table.is_contiguous():
+        raise ValueError("block_table must be a contiguous int32 [B, max_blocks] tensor")
+    if block_table.shape[1] * bs < ctx:
+        raise ValueError(f"block_table covers {block_table.shape[1] * bs} tokens < ctx {ctx}")
+    batch = block_table.shape[0]
+    shape = (batch, hkv, ctx, head_dim)
+    if out is None:
+        out = (torch.empty(shape, dtype=out_dtype, device=k_cache.device),
+               torch.empty(shape, dtype=out_dtype, device=k_cache.device))
+    k_out, v_out = out
+    _lib.call("kvecc_shim_read_batch", _ptr(k_cache), _ptr(v_cache), _ptr(k_scales), _ptr(v_scales),
+              _ptr(block_table), block_table.shape[1], batch, int(ctx), hkv, head_dim, nl, bs,
+              int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
+              _DT[out_dtype], _ptr(stats), _stream(k_cache.device))
+    return k_out, v_out
+
+
 # ============================================================================
 # Paged decode attention with inline ECC decode
 # ============================================================================
 
+_ATTN_ROW_WORDS = {"hamming84": lambda d: d, "golay": lambda d: (d + 2) // 3,
+                   "golay_packed": lambda d: (3 * ((d + 2) // 3) + 3) // 4 * 4}  # KVECC_GOLAY_PACKED_ROW
+_ATTN_CACHE_DT = {"hamming84": torch.uint8, "golay": torch.int32, "golay_packed": torch.uint8}
+_attn_ws = {}  # (device index, stream) -> float32 workspace, grown on demand
+_attn_ws_retired = []  # outgrown workspaces stay alive: a captured HIP graph may still name them
+
+
+def _attn_workspace(device, n):
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _attn_ws.get(key)
+    if ws is None or ws.numel() < n:
+        if ws is not None:
+            _attn_ws_retired.append(ws)
+        ws = torch.empty(max(n, 1), dtype=torch.float32, device=device)
+        _attn_ws[key] = ws
+    return ws
+
+
+def _check_attention_args(query, k_cache, v_cache, block_table, context_lens, k_scales, v_scales,
+                          out, block_size, codec):
+    if codec not in _ATTN_CACHE_DT:
+        raise ValueError(f"paged attention codec {codec!r} (hamming84, golay or golay_packed)")
+    if query.dim() != 3 or query.dtype not in _DT:
+        raise ValueError(f"query must be [B, H, D] fp32/fp16/bf16, got {tuple(query.shape)} {query.dtype}")
+    batch, heads, head_dim = query.shape
+    if k_cache.dim() != 4 or k_cache.shape != v_cache.shape:
+        raise ValueError("k_cache / v_cache must share one [blocks, layers, kv_heads, row] shape")
+    nb, nl, kvh, row = k_cache.shape
+    per = _ATTN_ROW_WORDS[codec](head_dim)
+    for name, c in (("k_cache", k_cache), ("v_cache", v_cache)):
+        if c.dtype != _ATTN_CACHE_DT[codec]:
+            raise ValueError(f"{codec} {name} must be {_ATTN_CACHE_DT[codec]}, got {c.dtype}")
+    if row != block_size * per:
+        raise ValueError(f"{codec} cache rows hold {row} words, expected block_size*{per} = "
+                         f"{block_size * per}")
+    if kvh < 1 or heads % kvh:
+        raise ValueError(f"{heads} query heads not a multiple of {kvh} kv heads")
+    if block_table.dim() != 2 or block_table.shape[0] != batch or block_table.dtype != torch.int32:
+        raise ValueError("block_table must be int32 [B, max_blocks]")
+    if context_lens.shape != (batch,) or context_lens.dtype != torch.int32:
+        raise ValueError("context_lens must be int32 [B]")
+    for name, sc in (("k_scales", k_scales), ("v_scales", v_scales)):
+        if sc.shape != (nb, nl, kvh, block_size) or sc.dtype != torch.float32:
+            raise ValueError(f"{name} must be float32 [{nb}, {nl}, {kvh}, {block_size}], got "
+                             f"{tuple(sc.shape)} {sc.dtype}")
+    if out.shape != query.shape or out.dtype not in _DT:
+        raise ValueError("out must match query's [B, H, D]")
+    for name, t in (("query", query), ("k_cache", k_cache), ("v_cache", v_cache),
+                    ("block_table", block_table), ("context_lens", context_lens),
+                    ("k_scales", k_scales), ("v_scales", v_scales), ("out", out)):
+        if t.device != query.device:
+            raise ValueError(f"{name} is on {t.device}, query on {query.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+
+
 def paged_attention_into(query, k_cache, v_cache, block_table, context_lens, k_scales, v_scales,
                          out, layer_idx, block_size, sm_scale, codec, max_context_len=0):
-    """kvecc_paged_attention on [B, H, D] query / out (see include/kvecc.h)."""
+    """kvecc_paged_attention on [B, H, D] query / out (see include/kvecc.h).
+
+    Every argument is validated (dtypes, geometry against codec and block_size,
+    contiguity, one device): a mismatch raises ValueError instead of reading
+    past an allocation.  The split workspace is cached per (device, stream).
+    ``out`` may differ in dtype from ``query`` only as the kernel allows (the
+    query dtype is the output dtype)."""
+    _check_gpu(query, "Query")
+    _check_attention_args(query, k_cache, v_cache, block_table, context_lens, k_scales, v_scales,
+                          out, block_size, codec)
+    if out.dtype != query.dtype:
+        raise ValueError(f"out dtype {out.dtype} != query dtype {query.dtype}")
     batch, heads, head_dim = query.shape
     num_blocks, num_layers, kv_heads, _ = k_cache.shape
     max_blocks = block_table.shape[1]
     mcl = int(max_context_len) if max_context_len and max_context_len > 0 else max_blocks * block_size
     ws_n = _lib.load().kvecc_paged_attention_workspace(batch, heads, head_dim, mcl)
-    ws = torch.empty(max(ws_n, 1), dtype=torch.float32, device=query.device)
+    ws = _attn_workspace(query.device, ws_n)
     _lib.call("kvecc_paged_attention", _ptr(query), _DT[query.dtype], _ptr(k_cache), _ptr(v_cache),
               _ptr(block_table), _ptr(context_lens), _ptr(k_scales), _ptr(v_scales), _ptr(out),
               batch, heads, kv_heads, head_dim, num_blocks, num_layers, int(layer_idx), int(block_size),
-              max_blocks, mcl, float(sm_scale), SHIM_CODECS[codec], _ptr(ws), ws_n,
+              max_blocks, mcl, float(sm_scale), SHIM_CODECS[codec], _ptr(ws), ws.numel(),
               _stream(query.device))
     return out
+
+
+def _conform(t, dtype):
+    """t itself when it already has dtype and is contiguous (no copy)."""
+    if t.dtype != dtype:
+        t = t.to(dtype)
+    return t if t.is_contiguous() else t.contiguous()
 
 
 def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_scales, layer_idx,
@@ -664,12 +767,10 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
     if out_dtype != q.dtype:
         q = q.to(out_dtype)
     out = torch.empty(q.shape, dtype=out_dtype, device=q.device)
-    paged_attention_into(q, k_cache.contiguous(), v_cache.contiguous(),
-                         block_table.to(torch.int32).contiguous(),
-                         context_lens.to(torch.int32).contiguous(),
-                         k_scales.to(torch.float32).contiguous(),
-                         v_scales.to(torch.float32).contiguous(), out, layer_idx, block_size,
-                         sm_scale, codec)
+    paged_attention_into(q, _conform(k_cache, k_cache.dtype), _conform(v_cache, v_cache.dtype),
+                         _conform(block_table, torch.int32), _conform(context_lens, torch.int32),
+                         _conform(k_scales, torch.float32), _conform(v_scales, torch.float32),
+                         out, layer_idx, block_size, sm_scale, codec)
     return out
 
 

@@ -161,3 +161,87 @@ def test_hip_shard_matches_oracle_shard(gpu):
             hip.run_trial(codec, ber, seed, a)
             ora.run_trial(codec, ber, seed, b)
             assert a.cpu().tolist() == b.tolist(), (codec, ber, world, rank)
+
+
+def test_seed_aliases_config5():
+    """Config 5 on [8,4096,32,128]: seeds 101 and 997 draw identical Hamming
+    flips (int32 key wrap, fault_injection_triton.py:247-294); Golay's
+    N = 45,088,768 codewords keeps them apart.  The sweep marks the duplicate."""
+    cfg = mc.MonteCarloConfig()
+    al = mc.seed_aliases(cfg)
+    for codec in ("hamming74", "hamming84", "hamming84_interp"):
+        for ber in cfg.bers:
+            assert al[mc.trial_key(codec, ber, 997)] == mc.trial_key(codec, ber, 101)
+            assert mc.trial_key(codec, ber, 101) not in al
+            assert mc.trial_key(codec, ber, 42) not in al
+    assert not any(k.startswith("golay|") for k in al)
+    assert len(al) == 9
+
+
+def test_seed_alias_rows_identical_and_flagged():
+    """Seeds whose keys collide mod 2^32 give identical counters, and run_sweep
+    flags the later one with alias_of (shape with N*n_bits = 2^30)."""
+    shape = (1, 1, 1, 1 << 27)
+    assert mc.stream_key("hamming84", 101, shape) == mc.stream_key("hamming84", 997, shape)
+    # a small shape where two seeds collide: N*8 = 2^k  ->  seeds differing by 2^(32-k)
+    small = (4, 16, 2, 8)                      # N = 1024, N*8 = 2^13
+    s1, s2 = 5, 5 + (1 << 19)
+    assert mc.stream_key("hamming84", s1, small) == mc.stream_key("hamming84", s2, small)
+    cfg = mc.MonteCarloConfig(shape=small, codecs=("hamming84",), bers=(0.05,), seeds=(s1, s2))
+    rows, _ = mc.run_sweep(cfg, OracleShard(cfg, 0, 1))
+    a, b = rows
+    assert "alias_of" not in a and b["alias_of"] == a["key"]
+    assert [a[k] for k in mc.STAT_NAMES] == [b[k] for k in mc.STAT_NAMES]
+    assert a["flips"] > 0
+
+
+MP_SHAPE = (5, 64, 3, 128)
+
+
+def _launch_ranks(backend, world, out, timeout=110):
+    """Start `world` fresh worker processes (tests/mp_sweep_worker.py) and wait."""
+    import subprocess
+    import sys
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "mp_sweep_worker.py")
+    procs = []
+    for rank in range(world):
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, "-u", worker, backend, out,
+                                       *map(str, MP_SHAPE)], env=env))
+    try:
+        codes = [p.wait(timeout=timeout) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert codes == [0] * world, codes
+    with open(out) as f:
+        return json.load(f)
+
+
+def _single_hip_rows(gpu):
+    cfg = mc.MonteCarloConfig(shape=MP_SHAPE, bers=(1e-3, 0.03), seeds=(42, 7))
+    rows, _ = mc.run_sweep(cfg, mc.HipShard(cfg, 0, 1, gpu))
+    return rows
+
+
+@pytest.mark.gpu
+def test_hip_sweep_nccl_world1_equals_single(gpu, tmp_path):
+    """HipShard + run_sweep under a real RCCL ("nccl") process group: the
+    device-tensor all_reduce runs in HBM; rows equal the single-process run."""
+    res = _launch_ranks("nccl", 1, str(tmp_path / "nccl1.json"))
+    assert res["backend"] == "nccl"
+    assert res["rows"] == _single_hip_rows(gpu)
+
+
+@pytest.mark.gpu
+def test_hip_sweep_gloo_world2_on_one_gpu_equals_single(gpu, tmp_path):
+    """Two ranks sharing cuda:0 over gloo (RCCL refuses two ranks on one
+    device): each HipShard owns half the batch, the counters are all-reduced
+    (staged through the host) and equal the single-process rows bit for bit."""
+    res = _launch_ranks("gloo", 2, str(tmp_path / "gloo2.json"))
+    assert res["backend"] == "gloo" and res["world"] == 2
+    assert res["rows"] == _single_hip_rows(gpu)

@@ -269,8 +269,89 @@ def gen_shim(manifest):
     _save("shim_gpt2", manifest, {"model": cfg.to_dict(), "runs": params, "seq_len": 24}, **arrays)
 
 
+def gen_attention(manifest):
+    """Pin paged_attention_ecc (kv_cache/attention_ecc.py:620-780).
+
+    hamming84 runs the reference's ``paged_attention_ecc_kernel`` (:264-427)
+    under the interpreter; golay runs its Python ``reference_attention_ecc``
+    (:783-909) through the interpreted golay_decode.  Cases cover what the
+    reference's own tests leave at "shape only": empty contexts (H84 -> -8.0 in
+    every lane, golay -> zeros), -1 blocks before and after valid ones, a
+    table of only -1 blocks, head_dim 100 (BLOCK_HEAD_DIM 128), v_scales=None,
+    an fp16 query, and random (mostly noisy) codewords so every decode branch
+    runs.  No GQA: the reference indexes cache head = query head.
+    """
+    import torch
+    from ecc_codecs.triton_kernels import golay_encode
+    from kv_cache.attention_ecc import paged_attention_ecc
+    rng = np.random.default_rng(2024)
+    arrays = {}
+    params = []
+
+    def golay_cache(shape, g):
+        # codewords of random data with 0..4 random bit errors (every decode outcome)
+        m = int(np.prod(shape[:-1])) * shape[-1]
+        data = rng.integers(0, 4096, size=m, dtype=np.int64)
+        trip = np.stack([data & 15, (data >> 4) & 15, (data >> 8) & 15], 1).astype(np.uint8)
+        cw = golay_encode(torch.from_numpy(trip)).numpy().astype(np.int64)
+        nerr = rng.integers(0, 5, size=m)
+        for i in range(m):
+            for b in rng.choice(24, size=nerr[i], replace=False):
+                cw[i] ^= 1 << int(b)
+        return cw.astype(np.int32).reshape(shape)
+
+    cases = [
+        # name, codec, batch, heads, d, layers, layer, bs, nblocks, table, ctx, qdtype, v_scales
+        ("h84_basic", "hamming84", 2, 2, 32, 2, 1, 4, 8, [[3, 0, 6, -1], [5, 1, 2, 7]], [13, 16],
+         "f32", True),
+        ("h84_empty", "hamming84", 2, 2, 32, 1, 0, 4, 6, [[0, 1, -1, -1], [2, 3, -1, -1]], [0, 6],
+         "f32", True),
+        ("h84_holes", "hamming84", 2, 3, 32, 2, 0, 4, 8, [[-1, 3, 5, -1], [4, -1, 0, 2]], [16, 15],
+         "f32", True),
+        ("h84_all_missing", "hamming84", 1, 2, 16, 1, 0, 4, 3, [[-1, -1, -1]], [9], "f32", True),
+        ("h84_d100", "hamming84", 1, 2, 100, 1, 0, 4, 4, [[2, 0, 3]], [10], "f32", True),
+        ("h84_vscales_none", "hamming84", 2, 2, 64, 2, 1, 4, 6, [[1, 4, -1], [0, 5, 2]], [7, 12],
+         "f32", False),
+        ("h84_fp16", "hamming84", 1, 4, 64, 1, 0, 4, 4, [[3, 1, 0]], [11], "f16", True),
+        ("golay_basic", "golay", 2, 2, 64, 2, 1, 4, 6, [[2, 0, 5], [1, 4, 3]], [9, 12], "f32", True),
+        ("golay_empty_holes", "golay", 2, 2, 32, 1, 0, 4, 6, [[0, 1, -1], [-1, 3, 2]], [0, 11],
+         "f32", True),
+        ("golay_d100", "golay", 1, 2, 100, 1, 0, 4, 4, [[1, 3, 0]], [12], "f32", True),
+    ]
+    for (name, codec, batch, heads, d, layers, layer, bs, nblocks, table, ctx, qdt,
+         with_vs) in cases:
+        per = d if codec == "hamming84" else (d + 2) // 3
+        shape = (nblocks, layers, heads, bs * per)
+        if codec == "hamming84":
+            kc = rng.integers(0, 256, size=shape, dtype=np.int64).astype(np.uint8)
+            vc = rng.integers(0, 256, size=shape, dtype=np.int64).astype(np.uint8)
+        else:
+            kc, vc = golay_cache(shape, per), golay_cache(shape, per)
+        ks = (rng.random((nblocks, layers, heads, bs)) * 0.3 + 0.05).astype(np.float32)
+        vs = (rng.random((nblocks, layers, heads, bs)) * 0.3 + 0.05).astype(np.float32)
+        q = rng.standard_normal((batch, heads, d)).astype(np.float32)
+        if qdt == "f16":
+            q = q.astype(np.float16)
+        tab = np.array(table, dtype=np.int32)
+        lens = np.array(ctx, dtype=np.int32)
+        out = paged_attention_ecc(torch.from_numpy(q), torch.from_numpy(kc), torch.from_numpy(vc),
+                                  torch.from_numpy(tab), torch.from_numpy(lens), torch.from_numpy(ks),
+                                  layer, bs, codec=codec,
+                                  v_scales=torch.from_numpy(vs) if with_vs else None)
+        for k, v in (("q", q), ("k_cache", kc), ("v_cache", vc), ("block_table", tab),
+                     ("context_lens", lens), ("k_scales", ks), ("v_scales", vs),
+                     ("out", out.numpy())):
+            arrays[f"{name}_{k}"] = v
+        params.append({"name": name, "codec": codec, "layer": layer, "block_size": bs,
+                       "v_scales": with_vs, "q_dtype": qdt, "out_dtype": str(out.dtype)})
+        print(f"    {name}: out {tuple(out.shape)} {out.dtype}, "
+              f"range [{float(out.min()):.4f}, {float(out.max()):.4f}]")
+    _save("attention", manifest, {"cases": params}, **arrays)
+
+
 GENERATORS = {"hamming": gen_hamming, "golay": gen_golay, "inject": gen_inject,
-              "interp": gen_interp, "fused": gen_fused, "shim": gen_shim}
+              "interp": gen_interp, "fused": gen_fused, "shim": gen_shim,
+              "attention": gen_attention}
 
 
 def main():

@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace and
 # HBM counter passes.  Each GPU step has its own time limit; a step that ends
 # in anything but success/test-failure (fault, abort, timeout) stops the script.
-# usage: tools/gpu_check.sh <tag> [steps...]   steps: test smoke bench prof pmc
+# usage: tools/gpu_check.sh <tag> [steps...]   steps: test smoke bench dist prof pmc
 set -u
 TAG=${1:-r01}
 shift || true
@@ -30,7 +30,9 @@ run() {  # name seconds cmd...
 
 for s in $STEPS; do
   case $s in
-    test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    test)  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
+             --timeout 120 --timeout-method thread ;;
+    dist)  run bench_dist 300 python bench.py --dist --steps 20 --no-cpu-baseline --no-packed ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     prof)  run prof_trace 600 rocprofv3 --kernel-trace --stats -T --output-format csv \
