@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--event-every", type=int, default=10,
                     help="time the kernels of every k-th timed step (a timed dispatch costs the "
                          "step ~8 us; timing every step cost 7-9%% of throughput)")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="skip the fused Golay read (shim_read_batch) measurement")
     ap.add_argument("--dist", action="store_true",
                     help="create the RCCL process group even at world size 1 (exercises the "
                          "barrier and the stats/timing all-reduces on one GPU)")
@@ -111,6 +113,64 @@ def cpu_baseline(budget_s, threads):
             "host": host_info(),
             "sample": f"{done} codewords of Golay encode+decode (BER 1e-2 on a slice) in {el:.1f} s, "
                       f"oracle/kvecc_oracle.c on {threads} host threads"}
+
+
+def fused_decode_bench(dev, steps, warmup, packed=False):
+    """The shim's fused Golay read (gather -> Golay decode -> dequantize -> fp16,
+    ecc_shim.py:990-1071; kvecc_shim_read_batch's wave-tile kernel) over a paged
+    cache of B=8 sequences x L=4096 tokens, Hkv=32, D=128, block_size 16, K and
+    V, BER 1e-2 codewords.  Algorithmic bytes per token row and side: 43
+    codewords (4 B each, 3 B packed) + 4 B scale in, 128 fp16 out."""
+    from kvecc import ops
+    bs, g = 16, (D + 2) // 3
+    nlb = L // bs
+    nb = B * nlb
+    gen = torch.Generator().manual_seed(7)
+    caches, scales = [], []
+    for side in range(2):
+        x = torch.randint(0, 16, (nb, 1, H, bs, D), generator=gen, dtype=torch.uint8).to(dev)
+        cw = ops.golay_encode_rows(x).view(-1)
+        ops.inject_into(cw, cw, BER, 24, seed=SEED + side)
+        cw = cw.view(nb, 1, H, bs * g)
+        if packed:
+            cw = torch.stack([(cw >> (8 * k)) & 0xFF for k in range(3)], -1).to(torch.uint8)
+            cw = cw.view(nb, 1, H, bs, 3 * g)
+            row = (3 * g + 3) // 4 * 4
+            pad = torch.zeros(nb, 1, H, bs, row, dtype=torch.uint8, device=dev)
+            pad[..., :3 * g] = cw
+            cw = pad.view(nb, 1, H, bs * row)
+        caches.append(cw.contiguous())
+        scales.append((torch.rand(nb, 1, H, bs, generator=gen) * 0.1 + 0.01).to(dev))
+        del x
+    table = torch.randperm(nb, generator=gen).to(torch.int32).view(B, nlb).to(dev)
+    codec = "golay_packed" if packed else "golay"
+    outs = (torch.empty(B, H, L, D, dtype=torch.float16, device=dev),
+            torch.empty(B, H, L, D, dtype=torch.float16, device=dev))
+    st = ops.new_stats(dev)
+
+    def call():
+        ops.shim_read_batch(caches[0], caches[1], scales[0], scales[1], table, L, D, 0, codec,
+                            torch.float16, stats=st, out=outs)
+
+    for _ in range(warmup):
+        call()
+    evs = [ops.kernel_timer(dev) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ops.time_next_launch(*evs[k])
+        call()
+    torch.cuda.synchronize()
+    ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
+    rows = 2 * B * L * H
+    bytes_per_row = (3 * g if packed else 4 * g) + 4 + 2 * D
+    gbs = rows * bytes_per_row / (ms * 1e-3) / 1e9
+    return {"workload": f"shim_read_batch {codec} -> fp16, [B={B},L={L},Hkv={H},D={D}] K+V, "
+                        f"block_size {bs}, BER {BER}",
+            "kernel": "shim_read_golay_tiles_kernel", "kernel_ms": ms,
+            "codewords_per_s": rows * g / (ms * 1e-3),
+            "bytes_per_launch": rows * bytes_per_row,
+            "bytes_per_token_row": bytes_per_row, "hbm_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
+            "timing": f"HIP events carried by the dispatch, mean of {steps} launches"}
 
 
 def cpu_quota():
@@ -347,6 +407,11 @@ def main():
                   "hbm_gbs": {"encode": 4.5 * m / (p_enc * 1e-3) / 1e9,
                               "decode": 4.625 * m / (p_dec * 1e-3) / 1e9}}
 
+    fused = None
+    if not args.no_fused:
+        fused = fused_decode_bench(dev, max(args.steps, 10), args.warmup)
+        fused["packed"] = fused_decode_bench(dev, max(args.steps, 10), args.warmup, packed=True)
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -397,6 +462,7 @@ def main():
                                 f"hipEventRecord markers on every {args.event_every}th timed step")},
         "decode_stats": {"bits_corrected": bits, "uncorrectable": unc, "steps": args.steps},
         "inject": inject,
+        "fused_golay_decode": fused,
         "packed": packed,
         "cpu_baseline": cpu,
         "cpu_backend": host,

@@ -698,9 +698,13 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
       const int64_t hl = item - side * per_side;
       const int64_t h = hl / ctx, l = hl % ctx;
       const int64_t slot = slot_of(l, h);
-      const float s = (side ? v_scales : k_scales)[slot];
       void *out = side ? v_out : k_out;
       const int64_t o = (h * ctx + l) * d;
+      if (golay && block_table[l / block_size] < 0) {  // no physical block: zeros
+        for (int64_t j = 0; j < d; ++j) store_y(out, out_dtype, o + j, 0.0f);
+        continue;
+      }
+      const float s = (side ? v_scales : k_scales)[slot];
       if (golay) {
         const void *cache = side ? v_cache : k_cache;
         for (int64_t q = 0; q < g; ++q) {

@@ -200,6 +200,14 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
     const uint32_t t = i - side * per_side;
     const uint32_t hl = t / geo.g, k = t - hl * geo.g;
     const uint32_t h = hl / a.ctx, l = hl - h * a.ctx;
+    TO *o = reinterpret_cast<TO *>(a.out[side]) + ((int64_t)h * a.ctx + l) * geo.d + 3 * k;
+    const uint32_t left = geo.d - 3 * k;
+    if (geo.table[l / geo.bs] < 0) {  // no physical block: zeros
+      o[0] = from_f32<TO>(0.0f);
+      if (left > 1) o[1] = from_f32<TO>(0.0f);
+      if (left > 2) o[2] = from_f32<TO>(0.0f);
+      continue;
+    }
     const int64_t slot = geo.slot(l, h);
     uint32_t w;
     if (PACKED) {
@@ -214,8 +222,6 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
     bits += cnt & 3u;
     unc += cnt >> 2;
     const float s = a.scales[side][slot];
-    TO *o = reinterpret_cast<TO *>(a.out[side]) + ((int64_t)h * a.ctx + l) * geo.d + 3 * k;
-    const uint32_t left = geo.d - 3 * k;
     o[0] = from_f32<TO>(((float)(dw & 0xFu) - 8.0f) * s);
     if (left > 1) o[1] = from_f32<TO>(((float)(dw >> 4 & 0xFu) - 8.0f) * s);
     if (left > 2) o[2] = from_f32<TO>(((float)(dw >> 8) - 8.0f) * s);

@@ -1,0 +1,201 @@
+"""Batched fused shim read (kvecc_shim_read_batch): gather -> decode -> dequantize
+for every sequence of a paged cache (ecc_shim.py:990-1071, the consumer of
+golay_decode the headline's "fused Golay decode" names).
+
+CPU tier: the host twin against a numpy restatement over the oracle's decoders
+(bit-exact values and statistics).  GPU tier: the HIP path -- the wave-tile
+Golay kernel for d % 8 == 0, the per-sequence kernels otherwise -- against the
+host twin, bit for bit, over codecs, output dtypes, head dims, block sizes,
+partial blocks, missing blocks, and the full [B=8, L=4096, Hkv=32, D=128] size.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+BER = 2e-2
+
+
+def _pack_golay(cache, g):
+    """int32 Golay cache [..., bs * g] -> packed rows of KVECC_GOLAY_PACKED_ROW(g) bytes."""
+    row = (3 * g + 3) // 4 * 4
+    w = cache.reshape(*cache.shape[:-1], -1, g).numpy().astype(np.uint32)
+    out = np.zeros(w.shape[:-1] + (row,), np.uint8)
+    for byte in range(3):
+        out[..., byte:3 * g:3] = (w >> (8 * byte)) & 0xFF
+    return torch.from_numpy(out.reshape(*cache.shape[:-1], -1))
+
+
+def make_cache(codec, batch, ctx, hkv, d, bs, layers=2, seed=0, spare=3):
+    """Random paged caches (cpu backend, oracle-pinned codecs) with BER-level errors.
+    Returns caches, scales, block table [batch, max_blocks] (a random
+    permutation of physical blocks) and the codeword count per row."""
+    from kvecc import cpu_ops
+    g = torch.Generator().manual_seed(seed)
+    nlb = (ctx + bs - 1) // bs
+    nb = batch * nlb + spare
+    golay = codec in ("golay", "golay_packed")
+    per = (d + 2) // 3 if golay else d
+    vals = torch.randint(0, 16, (2, nb, layers, hkv, bs, d), generator=g, dtype=torch.uint8)
+    caches = []
+    for side in range(2):
+        x = vals[side]
+        if golay:
+            cw = cpu_ops.golay_encode_rows(x).reshape(nb, layers, hkv, bs * per)
+            cw = cpu_ops.inject_bit_errors_triton(cw, BER, 24, seed=seed + side)
+            caches.append(_pack_golay(cw, per) if codec == "golay_packed" else cw)
+        else:
+            enc = {"hamming84": cpu_ops.hamming84_encode, "hamming74": cpu_ops.hamming74_encode,
+                   "int4": lambda t: t}[codec](x).reshape(nb, layers, hkv, bs * d)
+            if codec != "int4":
+                enc = cpu_ops.inject_bit_errors_triton(enc, BER, 8 if codec == "hamming84" else 7,
+                                                       seed=seed + side)
+            caches.append(enc)
+    ks = torch.rand(nb, layers, hkv, bs, generator=g) * 0.5 + 0.01
+    vs = torch.rand(nb, layers, hkv, bs, generator=g) * 0.5 + 0.01
+    max_blocks = nlb + 1
+    table = torch.full((batch, max_blocks), -1, dtype=torch.int32)
+    table[:, :nlb] = torch.randperm(nb, generator=g)[: batch * nlb].to(torch.int32).view(batch, nlb)
+    return caches[0], caches[1], ks, vs, table
+
+
+def oracle_read(oracle, cache, scales, table, ctx, d, layer, codec, out_dtype):
+    """numpy restatement of the read for one side: [B, hkv, ctx, d] and (stat0, stat1)."""
+    nb, layers, hkv, row = cache.shape
+    golay = codec in ("golay", "golay_packed")
+    g = (d + 2) // 3
+    per = ((3 * g + 3) // 4 * 4) if codec == "golay_packed" else (g if golay else d)
+    bs = row // per
+    c = cache.numpy().reshape(nb, layers, hkv, bs, per)
+    sc = scales.numpy()
+    batch = table.shape[0]
+    out = np.zeros((batch, hkv, ctx, d), np.float32)
+    st = [0, 0]
+    for b in range(batch):
+        pos = np.arange(ctx)
+        blk = table[b, pos // bs].numpy().astype(np.int64)
+        slot = pos % bs
+        ok = blk >= 0
+        rows = c[blk[ok], layer, :, slot[ok]]  # [n, hkv, per]
+        s = sc[blk[ok], layer, :, slot[ok]]  # [n, hkv]
+        if golay:
+            if codec == "golay_packed":
+                b3 = rows[..., :3 * g].astype(np.uint32).reshape(*rows.shape[:-1], g, 3)
+                w = (b3[..., 0] | b3[..., 1] << 8 | b3[..., 2] << 16).astype(np.int32)
+            else:
+                w = rows.astype(np.int32)
+            trip, _, (bits, unc) = oracle.golay_decode(w.reshape(-1))
+            q = trip.reshape(*w.shape[:-1], 3 * g)[..., :d]
+            st[0] += bits
+            st[1] += unc
+        elif codec == "hamming84":
+            q, _, (c1, c2) = oracle.hamming84_decode(rows.reshape(-1))
+            q = q.reshape(rows.shape)
+            st[0] += c1
+            st[1] += c2
+        elif codec == "hamming74":
+            q, _, (c1,) = oracle.hamming74_decode(rows.reshape(-1))
+            q = q.reshape(rows.shape)
+            st[0] += c1
+        else:
+            q = rows
+        val = (q.astype(np.float32) - np.float32(8.0)) * s[..., None].astype(np.float32)
+        out[b][:, pos[ok]] = val.transpose(1, 0, 2)
+    t = torch.from_numpy(out)
+    return t.to(out_dtype), st
+
+
+CPU_CASES = [("golay", 2, 37, 3, 128, 16), ("golay_packed", 2, 37, 3, 128, 16),
+             ("golay", 3, 20, 2, 64, 7), ("golay", 1, 9, 2, 100, 4), ("hamming84", 2, 33, 2, 64, 16),
+             ("hamming74", 2, 17, 2, 32, 8), ("int4", 1, 12, 3, 16, 4)]
+
+
+@pytest.mark.parametrize("codec,batch,ctx,hkv,d,bs", CPU_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_cpu_batch_read_vs_oracle(oracle, codec, batch, ctx, hkv, d, bs, dtype):
+    from kvecc import cpu_ops
+    kc, vc, ks, vs, table = make_cache(codec, batch, ctx, hkv, d, bs, seed=ctx)
+    st = cpu_ops.new_stats()
+    k, v = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 1, codec, dtype, stats=st)
+    ek, sk = oracle_read(oracle, kc, ks, table, ctx, d, 1, codec, dtype)
+    ev, sv = oracle_read(oracle, vc, vs, table, ctx, d, 1, codec, dtype)
+    assert torch.equal(k, ek) and torch.equal(v, ev)
+    assert cpu_ops.read_stats(st) == [sk[0] + sv[0], sk[1] + sv[1]]
+
+
+def test_cpu_missing_golay_block_reads_zero(oracle):
+    from kvecc import cpu_ops
+    kc, vc, ks, vs, table = make_cache("golay", 2, 40, 2, 64, 16, seed=4)
+    table[1, 1] = -1
+    k, v = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 40, 64, 1, "golay", torch.float32)
+    assert torch.equal(k[1, :, 16:32], torch.zeros(2, 16, 64))
+    ek, _ = oracle_read(oracle, kc, ks, table, 40, 64, 1, "golay", torch.float32)
+    assert torch.equal(k, ek)
+
+
+GPU_CASES = CPU_CASES + [("golay", 4, 257, 4, 128, 16), ("golay_packed", 3, 100, 8, 64, 32),
+                         ("golay", 2, 50, 2, 256, 8), ("golay", 1, 3, 1, 8, 16),
+                         ("golay_packed", 2, 64, 2, 512, 2), ("golay", 2, 31, 2, 96, 5)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,batch,ctx,hkv,d,bs", GPU_CASES)
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_hip_batch_read_vs_cpu(gpu, codec, batch, ctx, hkv, d, bs, dtype):
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache(codec, batch, ctx, hkv, d, bs, seed=ctx + d)
+    st = cpu_ops.new_stats()
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 1, codec, dtype, stats=st)
+    gst = ops.new_stats(gpu)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 1, codec, dtype, stats=gst)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
+@pytest.mark.gpu
+def test_hip_batch_read_interp_vs_cpu(gpu):
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache("hamming84", 3, 70, 2, 64, 16, seed=9)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 70, 64, 1, "hamming84", torch.float16,
+                                     interp=True)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), 70, 64, 1, "hamming84",
+                               torch.float16, interp=True)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["golay", "golay_packed"])
+def test_hip_missing_golay_block_reads_zero(gpu, codec):
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache(codec, 2, 40, 2, 64, 16, seed=4)
+    table[1, 1] = -1
+    table[0, 0] = -1
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 40, 64, 1, codec, torch.float16, stats=st)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), 40, 64, 1, codec, torch.float16,
+                               stats=gst)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert torch.equal(k[1, :, 16:32].cpu(), torch.zeros(2, 16, 64, dtype=torch.float16))
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["golay", "golay_packed"])
+def test_hip_batch_read_full_size(gpu, codec):
+    """[B=8, L=4096, Hkv=32, D=128] (the bench's fused-decode workload), fp16,
+    bit-exact against the host twin, statistics included."""
+    from kvecc import cpu_ops, ops
+    batch, ctx, hkv, d, bs = 8, 4096, 32, 128, 16
+    kc, vc, ks, vs, table = make_cache(codec, batch, ctx, hkv, d, bs, layers=1, seed=1, spare=0)
+    st = cpu_ops.new_stats()
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 0, codec, torch.float16, stats=st)
+    gst = ops.new_stats(gpu)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 0, codec, torch.float16,
+                               stats=gst)
+    assert torch.equal(k.cpu(), ek)
+    assert torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
