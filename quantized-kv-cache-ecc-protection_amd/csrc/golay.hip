@@ -24,6 +24,8 @@
 //    grid-strided.  More work per lane (4 groups) or lane-contiguous layouts
 //    lost 8-45%; computing the parity with VALU instead of the LDS table lost
 //    12-20% (the kernel turns VALU-bound).
+#include <algorithm>
+
 #include "kvecc_internal.h"
 
 namespace kvecc {
@@ -43,6 +45,9 @@ namespace kvecc {
 #endif
 #ifndef KVECC_GOLAY_ENC_PER_CU
 #define KVECC_GOLAY_ENC_PER_CU 16
+#endif
+#ifndef KVECC_GOLAY_ROWS_PER_CU  // register-tile row kernels (512 threads, ~50 KB LDS)
+#define KVECC_GOLAY_ROWS_PER_CU 2
 #endif
 constexpr int kGroups = KVECC_GOLAY_GROUPS;         // 4-codeword groups per lane per tile
 constexpr int kDecBlock = KVECC_GOLAY_DEC_BLOCK, kEncBlock = KVECC_GOLAY_ENC_BLOCK;  // threads per workgroup
@@ -460,6 +465,239 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
   if (stats) flush_stats2(stats, bits, unc);
 }
 
+// ---- per-head rows through register tiles (d % 16 == 0) --------------------------
+// The layout of the shim's fused read (shim.hip): a wave owns a tile of `tr`
+// whole rows, contiguous in both arrays.  The codeword side moves as 16-byte
+// buffer loads straight into registers, one 4-codeword group of a row per lane
+// (rows are 4g bytes, so a group may start on any dword; a row's last group
+// reads up to 3 codewords of the next row, which are decoded but masked out of
+// the statistics and never staged); the nibble side moves as 16-byte
+// non-temporal accesses of the tile's contiguous rows through a wave-private
+// LDS tile whose rows are `lr` = 16-byte-rounded 12 * ceil(g / 4) bytes apart,
+// so every LDS access of that side is one aligned ds_read/write_b128.
+//  decode: codewords -> registers -> spread-table decode (nibbles one per byte,
+//          exactly the output format) -> LDS rows -> 16-byte stores
+//  encode: nibbles -> 16-byte loads -> LDS rows -> 4 data words per lane ->
+//          parity table -> LDS codeword tile -> 16-byte stores
+// Every lane's (row, group) and (row, 16-byte chunk) items are the same for
+// every tile, computed once; the next tile's loads are issued before the
+// current tile's stores.  Per-lane offsets are 32-bit inside a tile, tile
+// bases 64-bit and wave-uniform (descriptors in SGPRs).
+constexpr int kRegBlock = 512;
+constexpr int kRegWaves = kRegBlock / kWave;
+constexpr int kRegGroups = 4;        // 4-codeword groups per lane per tile (max)
+constexpr int kRegChunks = 3;        // 16-byte nibble chunks per lane per tile (max)
+constexpr int kRegDecStage = 2304;   // decode: LDS nibble rows per wave
+constexpr int kRegEncIn = 2304;      // encode: LDS nibble rows per wave
+constexpr int kRegEncOut = 2816;     // encode: LDS codeword tile per wave
+
+struct RegRowsArgs {
+  const void *src;  // decode: int32 codewords; encode: uint8 nibbles
+  void *dst;        // decode: uint8 nibbles; encode: int32 codewords
+  int64_t rows, ntiles;
+  uint32_t d, g, gpr, lr, tr;
+  const void *tab;  // decode: spread tables (uint32[8192]); encode: parity (uint16[4096])
+  uint64_t *stats;
+};
+
+struct RegItems {
+  uint32_t r1[kRegGroups], q1[kRegGroups];  // row, 4-codeword group
+  uint32_t r2[kRegChunks], j2[kRegChunks];  // row, 16-byte nibble chunk
+  __device__ __forceinline__ RegItems(uint32_t lane, uint32_t gpr, uint32_t d16) {
+#pragma unroll
+    for (int i = 0; i < kRegGroups; ++i) {
+      const uint32_t f = lane + kWave * i;
+      r1[i] = f / gpr;
+      q1[i] = f - r1[i] * gpr;
+    }
+#pragma unroll
+    for (int i = 0; i < kRegChunks; ++i) {
+      const uint32_t v = lane + kWave * i;
+      r2[i] = v / d16;
+      j2[i] = v - r2[i] * d16;
+    }
+  }
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(uni(reinterpret_cast<const char *>(base))), 0,
+                                           (int)uni(bytes), 0x00020000);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRowsArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kRegWaves][kRegDecStage];
+  for (int i = threadIdx.x; i < 2048; i += kRegBlock)
+    reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
+  __syncthreads();
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  uint8_t *stage = stage_all[wave];
+  const uint32_t d16 = a.d / 16, groups = a.tr * a.gpr, chunks = a.tr * d16;
+  const RegItems it(lane, a.gpr, d16);
+  const int32_t *cw = reinterpret_cast<const int32_t *>(a.src);
+  uint8_t *nib = reinterpret_cast<uint8_t *>(a.dst);
+  uint32_t bits = 0, unc = 0;
+
+  int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
+  if (t >= a.ntiles) return;  // no workgroup barrier below
+  const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
+  u32x4 w[kRegGroups];
+  auto issue = [&](int64_t tt) {
+    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(cw + tt * a.tr * a.g, rows * a.g * 4u);
+#pragma unroll
+    for (int i = 0; i < kRegGroups; ++i) {
+      if (i * kWave >= (int)groups) break;  // uniform
+      w[i] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, it.r1[i] * a.g * 4u + 16u * it.q1[i], 0, 2));
+    }
+  };
+  issue(t);
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < kRegGroups; ++i) {
+      if (i * kWave >= (int)groups) break;  // uniform
+      const uint32_t q = it.q1[i];
+      uint32_t sp[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t c = w[i][k];
+        const uint32_t p = tab[c & 0xFFFu];
+        const uint32_t e = tab[4096 + (((c >> 12) ^ (p >> 20)) & 0xFFFu)];
+        sp[k] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
+        if (STATS && 4 * q + k < a.g) {  // past the tile: loads gave 0, count 0
+          bits += e >> 24 & 3u;
+          unc += e >> 26;
+        }
+      }
+      if (it.r1[i] < a.tr) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(stage + it.r1[i] * a.lr + 12 * q);
+        o[0] = sp[0] | sp[1] << 24;
+        o[1] = sp[1] >> 8 | sp[2] << 16;
+        o[2] = sp[2] >> 16 | sp[3] << 8;
+      }
+    }
+    wave_lds_sync();
+    const int64_t cur = t;
+    t += tstride;
+    const bool more = t < a.ntiles;
+    if (more) issue(t);
+    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
+    uint8_t *out = nib + cur * a.tr * a.d;
+#pragma unroll
+    for (int i = 0; i < kRegChunks; ++i) {
+      if (i * kWave >= (int)chunks) break;  // uniform
+      if (it.r2[i] < rows)
+        st_stream(reinterpret_cast<u32x4 *>(out + it.r2[i] * a.d) + it.j2[i],
+                  *reinterpret_cast<const u32x4 *>(stage + it.r2[i] * a.lr + 16 * it.j2[i]));
+    }
+    if (!more) break;
+    wave_lds_sync();
+  }
+  if (STATS) {
+    bits = wave_sum(bits);
+    unc = wave_sum(unc);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + ((blockIdx.x * kRegWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
+      if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRowsArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t par[4096];
+  __shared__ __attribute__((aligned(16))) uint8_t in_all[kRegWaves][kRegEncIn];
+  __shared__ __attribute__((aligned(16))) uint8_t out_all[kRegWaves][kRegEncOut];
+  for (int i = threadIdx.x; i < 512; i += kRegBlock)
+    reinterpret_cast<u32x4 *>(par)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  uint8_t *sin = in_all[wave];
+  uint32_t *sout = reinterpret_cast<uint32_t *>(out_all[wave]);
+  // the per-head zero padding: row bytes [d, lr) stay 0 (phase 1 writes [0, d))
+  for (uint32_t r = 0; r < a.tr; ++r)
+    for (uint32_t b = a.d + lane; b < a.lr; b += kWave) sin[r * a.lr + b] = 0;
+  __syncthreads();
+  const uint32_t d16 = a.d / 16, groups = a.tr * a.gpr, chunks = a.tr * d16;
+  const RegItems it(lane, a.gpr, d16);
+  const uint8_t *nib = reinterpret_cast<const uint8_t *>(a.src);
+  uint32_t *cw = reinterpret_cast<uint32_t *>(a.dst);
+
+  int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
+  if (t >= a.ntiles) return;
+  const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
+  u32x4 v[kRegChunks];
+  auto issue = [&](int64_t tt) {
+    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + tt * a.tr * a.d, rows * a.d);
+#pragma unroll
+    for (int i = 0; i < kRegChunks; ++i) {
+      if (i * kWave >= (int)chunks) break;  // uniform
+      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (lane + kWave * i), 0, 2));
+    }
+  };
+  issue(t);
+  for (;;) {
+    // ---- phase 1: land the nibble rows (chunk = lane + 64 i of the contiguous tile)
+#pragma unroll
+    for (int i = 0; i < kRegChunks; ++i) {
+      if (i * kWave >= (int)chunks) break;  // uniform
+      if (it.r2[i] < a.tr) *reinterpret_cast<u32x4 *>(sin + it.r2[i] * a.lr + 16 * it.j2[i]) = v[i];
+    }
+    wave_lds_sync();
+    const int64_t cur = t;
+    t += tstride;
+    const bool more = t < a.ntiles;
+    if (more) issue(t);
+    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
+    // ---- phase 2: 4 codewords per lane into the LDS codeword tile
+#pragma unroll
+    for (int i = 0; i < kRegGroups; ++i) {
+      if (i * kWave >= (int)groups) break;  // uniform
+      const uint32_t r = it.r1[i], q = it.q1[i];
+      if (r < rows) {
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(sin + r * a.lr + 12 * q);
+        uint32_t dd[4];
+        golay_unpack4(s[0], s[1], s[2], dd);
+        uint32_t *o = sout + r * a.g + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (4 * q + k < a.g) o[k] = dd[k] | (uint32_t)par[dd[k]] << 12;
+      }
+    }
+    wave_lds_sync();
+    // ---- phase 3: the tile's codewords, contiguous, as 16-byte stores
+    const uint32_t nw = rows * a.g;  // words
+    uint32_t *out = cw + cur * a.tr * a.g;
+    for (uint32_t k = lane; k < nw / 4; k += kWave)
+      st_stream(reinterpret_cast<u32x4 *>(out) + k, reinterpret_cast<const u32x4 *>(sout)[k]);
+    for (uint32_t k = nw / 4 * 4 + lane; k < nw; k += kWave) st_stream(out + k, sout[k]);  // last tile's tail
+    if (!more) break;
+    wave_lds_sync();
+  }
+}
+
+// tile geometry of the register-tile row kernels (0 rows: not applicable)
+struct RegGeom {
+  uint32_t gpr, lr, tr;
+};
+inline RegGeom reg_geom(int64_t d, int64_t g, bool encode) {
+  RegGeom r{0, 0, 0};
+  if (d % 16 != 0 || g < 16 || d > kTiledMaxD) return r;
+  r.gpr = (uint32_t)cdiv(g, 4);
+  r.lr = (12 * r.gpr + 15) / 16 * 16;
+  int64_t tr = std::min<int64_t>({(int64_t)(encode ? kRegEncIn : kRegDecStage) / r.lr,
+                                  (int64_t)kWave * kRegGroups / r.gpr, (int64_t)kWave * kRegChunks / (d / 16)});
+  if (encode) {
+    tr = std::min<int64_t>(tr, kRegEncOut / (4 * g));
+    const int64_t m = 4 / gcd_i((int)(g % 4), 4);  // tiles stay 16-byte aligned: tr * g % 4 == 0
+    tr = tr / m * m;
+  }
+  r.tr = (uint32_t)std::max<int64_t>(tr, 0);
+  return r;
+}
+
 }  // namespace kvecc
 
 using namespace kvecc;
@@ -538,6 +776,14 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
   const uint16_t *par = golay_parity_table_dev();
   if (!par) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
+  const RegGeom rg = reg_geom(d, g, true);
+  if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 16)) {
+    RegRowsArgs a{nibbles, codewords, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
+                  par, nullptr};
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
+    KVECC_LAUNCH(golay_encode_rows_reg_kernel, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
+    return check_launch("golay_encode_rows");
+  }
   if (row_tiled(d, g, false)) {
     const RowTile tl = row_tile(d, g);
     const bool a16 = aligned(nibbles, 16) && aligned(codewords, 16);
@@ -562,6 +808,19 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
   const uint16_t *cor = golay_correct_table_dev();
   if (!par || !cor) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
+  const RegGeom rg = reg_geom(d, g, false);
+  if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 4)) {
+    const uint32_t *atab = golay_attn_table_dev();
+    if (!atab) return KVECC_EHIP;
+    RegRowsArgs a{codewords, nibbles, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
+                  atab, stats};
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
+    if (stats)
+      KVECC_LAUNCH(golay_decode_rows_reg_kernel<true>, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
+    else
+      KVECC_LAUNCH(golay_decode_rows_reg_kernel<false>, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
+    return check_launch("golay_decode_rows");
+  }
   if (row_tiled(d, g, true)) {
     const RowTile tl = row_tile(d, g);
     const bool a16 = aligned(nibbles, 16) && aligned(codewords, 16);

@@ -90,6 +90,21 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a wave-uniform value the compiler cannot prove uniform (it came through a
+// vector load): readfirstlane, so buffer descriptors built from it live in
+// SGPRs instead of a waterfall loop around every buffer load
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ const char *uni(const char *p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  return reinterpret_cast<const char *>((uint64_t)uni((uint32_t)v) | (uint64_t)uni((uint32_t)(v >> 32)) << 32);
+}
+
+// a wave-uniform load through the scalar cache (s_load: counted by lgkmcnt, so
+// it does not wait behind the wave's outstanding vector stores like a vector load)
+__device__ __forceinline__ int32_t ld_scalar(const int32_t *p) {
+  return *(const __attribute__((address_space(4))) int32_t *)uni(reinterpret_cast<const char *>(p));
+}
+
 // element conversions of the fused kernels (fp32 / fp16 / bf16, RNE on the way out)
 template <typename T>
 __device__ __forceinline__ float to_f32(T v);

@@ -230,22 +230,45 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 }
 
 // ---- Golay read through wave tiles (the fused decode the headline names) -------
-// A wave owns a tile: up to `tr` consecutive token rows of one (side, sequence,
-// head, block) -- contiguous codewords in the cache, a contiguous run of the
-// [hkv, ctx, d] output.  Phase 1: each lane takes groups of 4 codewords of a
-// row (one 16-byte buffer load; packed: 12 bytes), decodes them through the
+// A wave owns a tile: up to `tr` (<= 64) consecutive token rows of one (side,
+// sequence, head, block) -- contiguous codewords in the cache, a contiguous run
+// of the [hkv, ctx, d] output.  Phase 1: each lane takes groups of 4 codewords
+// of a row (one 16-byte buffer load; packed: 12 bytes), decodes them through the
 // spread tables in LDS (2 lookups + a v_bitop3 per codeword, nibbles one per
 // byte, the error count in byte 3 of the correction entry) and writes 12
 // nibble bytes to the wave's LDS tile (rows `lr` bytes apart).  Phase 2: each
 // lane takes 8 consecutive values of a row (two LDS dwords), dequantizes
-// (q - 8) * scale in fp32 and writes them with one 16-byte store (fp16/bf16).
-// The next tile's loads are issued before phase 2 (register prefetch).  HBM
+// (q - 8) * scale in fp32 and writes them with one non-temporal 16-byte store
+// (fp16/bf16).  The next tile's codewords AND row scales (lane r holds row r's
+// scale, handed to phase 2 by ds_bpermute) are loaded before phase 2, so no
+// dependent global load sits inside a tile.  Every lane's (row, group) and
+// (row, 8-value chunk) items are the same for every tile: computed once.  HBM
 // traffic is the algorithm's: 4 B (3 B packed) per codeword in, d * sizeof(TO)
 // per row out, 4 B of scale per row.
-constexpr int kTileBlock = 512;                    // 8 waves per workgroup
+#ifndef KVECC_SHIM_TILE_NT
+#define KVECC_SHIM_TILE_NT 1     // non-temporal output stores and codeword loads
+#endif
+// workgroups per CU (LDS: 32 KiB table + a 2.25 KiB tile per wave); 2 beat 3
+// by 6-12 % at [8,4096,32,128] (tools/exp/run_shim_read.py)
+#ifndef KVECC_SHIM_TILE_PER_CU
+#define KVECC_SHIM_TILE_PER_CU 2
+#endif
+#ifndef KVECC_SHIM_TILE_BLOCK
+#define KVECC_SHIM_TILE_BLOCK 512
+#endif
+#ifndef KVECC_SHIM_TILE_NODECODE
+#define KVECC_SHIM_TILE_NODECODE 0
+#endif
+#ifndef KVECC_SHIM_TILE_TPI
+#define KVECC_SHIM_TILE_TPI 1
+#endif
+constexpr int kTileBlock = KVECC_SHIM_TILE_BLOCK;  // 8 waves per workgroup
+constexpr int kTileTPI = KVECC_SHIM_TILE_TPI;      // tiles in flight per wave
 constexpr int kTileWaves = kTileBlock / kWave;
 constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
 constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
+constexpr int kTileChunks = 5;                     // 8-value output chunks per lane per tile (max)
+constexpr int kTileAux = KVECC_SHIM_TILE_NT ? 2 : 0;  // buffer-load cache policy: nt
 
 struct ShimTileArgs {
   const void *cache[2];
@@ -257,7 +280,7 @@ struct ShimTileArgs {
   uint32_t tstride, hkv, d, g, layers, bs, layer, ctx;
   uint32_t gpr;           // 4-codeword groups per row: ceil(g / 4)
   uint32_t lr;            // LDS bytes per staged row: 12 * gpr
-  uint32_t tr;            // rows per tile
+  uint32_t tr;            // rows per tile (<= 64)
   uint32_t tpb;           // tiles per block: ceil(bs / tr)
   uint32_t nlb;           // logical blocks covering ctx
   uint32_t units;         // 2 * batch * hkv * nlb * tpb
@@ -282,55 +305,98 @@ __device__ __forceinline__ ShimTile shim_tile(const ShimTileArgs &a, uint32_t u)
   const uint32_t b = t.bh / a.hkv, h = t.bh - b * a.hkv;
   t.pos0 = lb * a.bs + ch * a.tr;
   t.rows = t.pos0 < a.ctx ? min(min(a.tr, a.bs - ch * a.tr), a.ctx - t.pos0) : 0u;
-  const int32_t blk = a.table[(int64_t)b * a.tstride + lb];
+  const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + lb);
   t.row0 = blk < 0 ? -1 : (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + ch * a.tr;
   return t;
 }
 
+// per-lane items, identical for every tile
+struct TileItems {
+  uint32_t r1[kTileGroups], q1[kTileGroups];  // phase 1: row, 4-codeword group
+  uint32_t r2[kTileChunks], j2[kTileChunks];  // phase 2: row, 8-value chunk
+};
+
+// the tile's codewords and its rows' scales, into registers.  Buffer
+// descriptors cover exactly the tile's bytes: past them (rows >= t.rows, a
+// missing block, a row's last group running into the next row) loads return 0,
+// which decodes to 0 with no error count; the overrun codeword is masked
+// out of the statistics and never reaches the output.
+// the tile's codewords (raw: packed rows' 3 dwords are unpacked where used, so
+// nothing waits on the loads here) and its rows' scales, into registers.
+// Buffer descriptors cover exactly the tile's bytes: past them (rows >=
+// t.rows, a missing block, a row's last group running into the next row)
+// loads return 0, which decodes to 0 with no error count; the overrun
+// codeword is masked out of the statistics and never reaches the output.
 template <bool PACKED>
 __device__ __forceinline__ void tile_issue(const ShimTileArgs &a, const ShimTile &t, uint32_t lane,
-                                           u32x4 (&w)[kTileGroups]) {
-  // buffer descriptor over exactly the tile's bytes: a row's last group reads
-  // past its row (the next row's first codeword, or 0 past the tile), ignored
-  const char *base = reinterpret_cast<const char *>(a.cache[t.side]) + (t.row0 < 0 ? 0 : t.row0) * (int64_t)a.rowb;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<char *>(base), 0, t.row0 < 0 ? 0 : (int)(t.rows * a.rowb), 0x00020000);
+                                           const TileItems &it, u32x4 (&w)[kTileGroups], float &scale) {
+  const bool live = t.row0 >= 0;
+  const int64_t row0 = live ? t.row0 : 0;
+  const uint32_t side = uni(t.side);
+  const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + row0 * (int64_t)a.rowb);
+  const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + row0));
+  const uint32_t nrows = uni(live ? t.rows : 0u);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.rowb), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ss =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+  scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
   const uint32_t groups = a.tr * a.gpr;
 #pragma unroll
   for (int i = 0; i < kTileGroups; ++i) {
     if (i * kWave >= (int)groups) break;  // uniform
-    const uint32_t f = lane + kWave * i;
-    const uint32_t r = f / a.gpr, q = f - r * a.gpr;
-    const uint32_t off = (r < t.rows ? r : 0u) * a.rowb + (PACKED ? 12u : 16u) * q;
-    if (PACKED) {  // 4 three-byte codewords from 3 dwords
-      const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
-      w[i] = u32x4{v[0], __builtin_amdgcn_alignbyte(v[1], v[0], 3), __builtin_amdgcn_alignbyte(v[2], v[1], 2),
-                   v[2] >> 8};
+    const uint32_t off = it.r1[i] * a.rowb + (PACKED ? 12u : 16u) * it.q1[i];
+    if (PACKED) {  // 4 three-byte codewords in 3 dwords
+      const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, kTileAux);
+      w[i] = u32x4{v[0], v[1], v[2], 0u};
     } else {
-      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kTileAux));
     }
+  }
+}
+
+// codeword k of group w (packed: from its 3 raw dwords)
+template <bool PACKED>
+__device__ __forceinline__ uint32_t tile_cw(const u32x4 &w, int k) {
+  if (!PACKED) return w[k];
+  switch (k) {
+    case 0: return w[0];
+    case 1: return __builtin_amdgcn_alignbyte(w[1], w[0], 3);
+    case 2: return __builtin_amdgcn_alignbyte(w[2], w[1], 2);
+    default: return w[2] >> 8;
   }
 }
 
 template <typename TO>
 __device__ __forceinline__ void store8(TO *dst, const float (&v)[8]) {
   if constexpr (sizeof(TO) == 4) {
-    reinterpret_cast<float4 *>(dst)[0] = float4{v[0], v[1], v[2], v[3]};
-    reinterpret_cast<float4 *>(dst)[1] = float4{v[4], v[5], v[6], v[7]};
+    const u32x4 lo{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+    const u32x4 hi{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
+    if (KVECC_SHIM_TILE_NT) {
+      st_stream(reinterpret_cast<u32x4 *>(dst), lo);
+      st_stream(reinterpret_cast<u32x4 *>(dst) + 1, hi);
+    } else {
+      reinterpret_cast<u32x4 *>(dst)[0] = lo;
+      reinterpret_cast<u32x4 *>(dst)[1] = hi;
+    }
   } else {
     uint32_t p[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       p[k] = (uint32_t)__builtin_bit_cast(uint16_t, from_f32<TO>(v[2 * k])) |
              (uint32_t)__builtin_bit_cast(uint16_t, from_f32<TO>(v[2 * k + 1])) << 16;
-    *reinterpret_cast<u32x4 *>(dst) = u32x4{p[0], p[1], p[2], p[3]};
+    const u32x4 o{p[0], p[1], p[2], p[3]};
+    if (KVECC_SHIM_TILE_NT)
+      st_stream(reinterpret_cast<u32x4 *>(dst), o);
+    else
+      *reinterpret_cast<u32x4 *>(dst) = o;
   }
 }
 
 template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileTPI][kTileStage];
   {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(tab);
@@ -340,76 +406,128 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   __syncthreads();
   // wave-uniform from here on (readfirstlane: the compiler cannot prove it)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint8_t *stage = stage_all[wave];
   const uint32_t lane = threadIdx.x % kWave;
   const uint32_t nwaves = gridDim.x * kTileWaves;
   const uint32_t groups = a.tr * a.gpr;  // <= 64 * kTileGroups (host check)
   const uint32_t d8 = a.d / 8;
+  const uint32_t chunks = a.tr * d8;     // <= 64 * kTileChunks (host check)
+  TileItems it;
+#pragma unroll
+  for (int i = 0; i < kTileGroups; ++i) {
+    const uint32_t f = lane + kWave * i;
+    it.r1[i] = f / a.gpr;
+    it.q1[i] = f - it.r1[i] * a.gpr;
+  }
+#pragma unroll
+  for (int i = 0; i < kTileChunks; ++i) {
+    const uint32_t v = lane + kWave * i;
+    it.r2[i] = v / d8;
+    it.j2[i] = v - it.r2[i] * d8;
+  }
   uint32_t bits = 0, unc = 0;
 
+  // kTileTPI tiles per iteration: u, u + nwaves, ...; all their loads in flight
   uint32_t u = blockIdx.x * kTileWaves + wave;
   if (u >= a.units) return;  // no workgroup barrier below: waves retire independently
-  ShimTile cur = shim_tile(a, u);
-  u32x4 w[kTileGroups];
-  tile_issue<PACKED>(a, cur, lane, w);
-  for (;;) {
-    // ---- phase 1: decode 4 codewords per group into the LDS tile --------------
+  ShimTile cur[kTileTPI];
+  bool valid[kTileTPI];
+  u32x4 w[kTileTPI][kTileGroups];
+  float scale[kTileTPI];
+  auto fetch = [&](uint32_t u0) {
 #pragma unroll
-    for (int i = 0; i < kTileGroups; ++i) {
-      if (i * kWave >= (int)groups) break;  // uniform
-      const uint32_t f = lane + kWave * i;
-      const uint32_t r = f / a.gpr, q = f - r * a.gpr;
-      if (r < cur.rows) {
+    for (int k = 0; k < kTileTPI; ++k) {
+      valid[k] = u0 + k * nwaves < a.units;  // uniform
+      if (valid[k]) {
+        cur[k] = shim_tile(a, u0 + k * nwaves);
+        tile_issue<PACKED>(a, cur[k], lane, it, w[k], scale[k]);
+      }
+    }
+  };
+  fetch(u);
+  for (;;) {
+    // ---- phase 1: decode 4 codewords per group into the LDS tiles -------------
+#pragma unroll
+    for (int k = 0; k < kTileTPI; ++k) {
+      if (!valid[k]) continue;
+      uint8_t *stage = stage_all[wave][k];
+#pragma unroll
+      for (int i = 0; i < kTileGroups; ++i) {
+        if (i * kWave >= (int)groups) break;  // uniform
+        const uint32_t q = it.q1[i];
         uint32_t sp[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t cw = w[i][k];
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t cw = tile_cw<PACKED>(w[k][i], c);
+#if KVECC_SHIM_TILE_NODECODE  // memory-ceiling experiment: no table lookups (wrong values)
+          const uint32_t p = cw, e = 0;
+#else
           const uint32_t p = tab[cw & 0xFFFu];
           // syndrome = parity bits ^ parity(data): (cw >> 12 ^ p >> 20) & 0xFFF
           const uint32_t e = tab[4096 + (((cw >> 12) ^ (p >> 20)) & 0xFFFu)];
-          sp[k] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
-          if (STATS && cur.row0 >= 0 && 4 * q + k < a.g) {
-            const uint32_t c = e >> 24;  // 0-3 bits corrected, 4 = uncorrectable
-            bits += c & 3u;
-            unc += c >> 2;
+#endif
+          sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
+          if (STATS && 4 * q + c < a.g) {  // a row's last group runs into the next row
+            const uint32_t n = e >> 24;  // 0-3 bits corrected, 4 = uncorrectable
+            bits += n & 3u;
+            unc += n >> 2;
           }
         }
-        uint32_t *dst = reinterpret_cast<uint32_t *>(stage + r * a.lr + 12 * q);
-        dst[0] = sp[0] | sp[1] << 24;
-        dst[1] = sp[1] >> 8 | sp[2] << 16;
-        dst[2] = sp[2] >> 16 | sp[3] << 8;
+        if (it.r1[i] < a.tr) {  // groups past the tile's last row are never staged
+          uint32_t *dst = reinterpret_cast<uint32_t *>(stage + it.r1[i] * a.lr + 12 * q);
+          dst[0] = sp[0] | sp[1] << 24;
+          dst[1] = sp[1] >> 8 | sp[2] << 16;
+          dst[2] = sp[2] >> 16 | sp[3] << 8;
+        }
       }
     }
     wave_lds_sync();
-    // ---- prefetch the next tile's codewords ------------------------------------
-    const ShimTile t = cur;
-    u += nwaves;
-    const bool more = u < a.units;
-    if (more) {
-      cur = shim_tile(a, u);
-      tile_issue<PACKED>(a, cur, lane, w);
+    // ---- prefetch the next tiles' codewords and scales ---------------------------
+    ShimTile t[kTileTPI];
+    bool tv[kTileTPI];
+    float ts[kTileTPI];
+#pragma unroll
+    for (int k = 0; k < kTileTPI; ++k) {
+      t[k] = cur[k];
+      tv[k] = valid[k];
+      ts[k] = scale[k];
     }
+    u += kTileTPI * nwaves;
+    const bool more = u < a.units;
+    if (more) fetch(u);
     // ---- phase 2: dequantize 8 values per lane, 16-byte stores -----------------
-    const uint32_t tasks = t.rows * d8;
-    const float *sc = a.scales[t.side] + (t.row0 < 0 ? 0 : t.row0);
-    TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
-    for (uint32_t v = lane; v < tasks; v += kWave) {
-      const uint32_t r = v / d8, j = v - r * d8;
-      float o[8];
-      if (t.row0 >= 0) {
-        const float s = sc[r];
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + 8 * j);
-        const uint32_t lo = src[0], hi = src[1];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = ((float)(lo >> (8 * e) & 0xFFu) - 8.0f) * s;
-          o[4 + e] = ((float)(hi >> (8 * e) & 0xFFu) - 8.0f) * s;
+    for (int k = 0; k < kTileTPI; ++k) {
+      if (!tv[k]) continue;
+      const uint8_t *stage = stage_all[wave][k];
+      TO *out = reinterpret_cast<TO *>(a.out[t[k].side]) + ((int64_t)t[k].bh * a.ctx + t[k].pos0) * a.d;
+      if (t[k].row0 >= 0) {
+#pragma unroll
+        for (int i = 0; i < kTileChunks; ++i) {
+          if (i * kWave >= (int)chunks) break;  // uniform
+          const uint32_t r = it.r2[i], j = it.j2[i];
+          // every lane joins the bpermute (lanes past the tile read a harmless row)
+          const float s = __shfl(ts[k], (int)min(r, (uint32_t)kWave - 1u), kWave);
+          if (r < t[k].rows) {
+            float o[8];
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + 8 * j);
+            const uint32_t lo = src[0], hi = src[1];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              o[e] = ((float)(lo >> (8 * e) & 0xFFu) - 8.0f) * s;
+              o[4 + e] = ((float)(hi >> (8 * e) & 0xFFu) - 8.0f) * s;
+            }
+            store8<TO>(out + (int64_t)r * a.d + 8 * j, o);
+          }
         }
-      } else {
+      } else {  // no physical block: +0 (the product above would give -0)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = 0.0f;
+        for (int i = 0; i < kTileChunks; ++i) {
+          if (i * kWave >= (int)chunks) break;  // uniform
+          const uint32_t r = it.r2[i], j = it.j2[i];
+          const float o[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+          if (r < t[k].rows) store8<TO>(out + (int64_t)r * a.d + 8 * j, o);
+        }
       }
-      store8<TO>(out + (int64_t)r * a.d + 8 * j, o);
     }
     if (!more) break;
     wave_lds_sync();  // phase 2 reads done before the next phase 1 overwrites
@@ -486,7 +604,7 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
 
 template <typename TO>
 static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * 3);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * KVECC_SHIM_TILE_PER_CU);
   if (a.stats && packed)
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
   else if (a.stats)
@@ -645,7 +763,8 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
     a.ctx = (uint32_t)ctx;
     a.gpr = (uint32_t)gpr;
     a.lr = (uint32_t)lr;
-    a.tr = (uint32_t)std::min<int64_t>({block_size, kTileStage / lr, (int64_t)kWave * kTileGroups / gpr});
+    a.tr = (uint32_t)std::min<int64_t>({block_size, kTileStage / lr, (int64_t)kWave * kTileGroups / gpr,
+                                        (int64_t)kWave, (int64_t)kWave * kTileChunks / (d / 8)});
     a.tpb = (uint32_t)cdiv(block_size, a.tr);
     a.nlb = (uint32_t)cdiv(ctx, block_size);
     a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);

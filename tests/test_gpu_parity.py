@@ -513,7 +513,7 @@ def test_time_next_launch_stamps_one_kernel(gpu):
     assert start.elapsed_time(stop) == t1
 
 
-@pytest.mark.parametrize("d", [1, 2, 5, 46, 47, 64, 100, 127, 128, 129, 255, 256, 300, 511, 513])
+@pytest.mark.parametrize("d", [1, 2, 5, 46, 47, 48, 64, 96, 100, 127, 128, 129, 255, 256, 300, 511, 512, 513])
 @pytest.mark.parametrize("rows,offset", [(1, 0), (63, 0), (64, 0), (65, 1), (1000, 0), (1000, 3)])
 def test_golay_rows_vs_cpu_backend(gpu, d, rows, offset):
     """Per-head packing (ecc_shim.py:623-682): the wave-tiled LDS kernels (46 <= d <= 512:

@@ -1,0 +1,116 @@
+"""A/B of the fused shim read (kvecc_shim_read_batch, wave-tile Golay kernel)
+across library builds, interleaved in one process on the bench's workload:
+[B=8, L=4096, Hkv=32, D=128] K+V, block_size 16, BER 1e-2, fp16 out.
+
+usage: python tools/exp/run_shim_read.py [lib.so ...]   (product lib first)
+Prints per-lib median / min kernel time (events carried by the dispatch) and
+whether outputs + statistics equal the first lib's.
+"""
+import ctypes
+import os
+import statistics
+import sys
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd"))
+import torch  # noqa: E402
+
+from kvecc import _lib, ops  # noqa: E402
+
+B, L, H, D, BS, BER = 8, 4096, 32, 128, 16, 1e-2
+ROUNDS = int(os.environ.get("ROUNDS", "30"))
+
+
+def build_cache(dev, packed):
+    g = (D + 2) // 3
+    nlb = L // BS
+    nb = B * nlb
+    gen = torch.Generator().manual_seed(7)
+    caches, scales = [], []
+    for side in range(2):
+        x = torch.randint(0, 16, (nb, 1, H, BS, D), generator=gen, dtype=torch.uint8).to(dev)
+        cw = ops.golay_encode_rows(x).view(-1)
+        ops.inject_into(cw, cw, BER, 24, seed=42 + side)
+        cw = cw.view(nb, 1, H, BS * g)
+        if packed:
+            cw = torch.stack([(cw >> (8 * k)) & 0xFF for k in range(3)], -1).to(torch.uint8)
+            cw = cw.view(nb, 1, H, BS, 3 * g)
+            row = (3 * g + 3) // 4 * 4
+            pad = torch.zeros(nb, 1, H, BS, row, dtype=torch.uint8, device=dev)
+            pad[..., :3 * g] = cw
+            cw = pad.view(nb, 1, H, BS * row)
+        caches.append(cw.contiguous())
+        scales.append((torch.rand(nb, 1, H, BS, generator=gen) * 0.1 + 0.01).to(dev))
+    table = torch.randperm(nb, generator=gen).to(torch.int32).view(B, nlb).to(dev)
+    if os.environ.get("TABLE") == "seq":  # physical blocks in logical order
+        table = torch.arange(nb, dtype=torch.int32).view(B, nlb).to(dev)
+    # a few missing blocks, as the shim's tables can hold
+    table[1, 5] = -1
+    table[6, 200] = -1
+    return caches, scales, table
+
+
+def main():
+    dev = torch.device("cuda:0")
+    libs = sys.argv[1:] or [_lib.LIB_PATH]
+    handles = []
+    for p in libs:
+        h = ctypes.CDLL(os.path.abspath(p))
+        fn = h.kvecc_shim_read_batch
+        fn.argtypes = _lib.SIGNATURES["kvecc_shim_read_batch"]
+        fn.restype = ctypes.c_int
+        tn = h.kvecc_time_next_launch
+        tn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        handles.append((os.path.basename(p), fn, tn))
+    for packed in (False, True):
+        caches, scales, table = build_cache(dev, packed)
+        g = (D + 2) // 3
+        per = ((3 * g + 3) // 4 * 4) if packed else g
+        bs = caches[0].shape[-1] // per
+        codec = 4 if packed else 3
+        outs = [(torch.empty(B, H, L, D, dtype=torch.float16, device=dev),
+                 torch.empty(B, H, L, D, dtype=torch.float16, device=dev)) for _ in handles]
+        stats = [ops.new_stats(dev) for _ in handles]
+        times = [[] for _ in handles]
+        stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def call(i):
+            name, fn, tn = handles[i]
+            rc = fn(caches[0].data_ptr(), caches[1].data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(),
+                    table.data_ptr(), table.shape[1], B, L, H, D, 1, bs, 0, codec, 0,
+                    outs[i][0].data_ptr(), outs[i][1].data_ptr(), 1, stats[i].data_ptr(), stream)
+            assert rc == 0, (name, rc)
+
+        for i in range(len(handles)):
+            for _ in range(3):
+                call(i)
+        for s in stats:
+            s.zero_()
+        for i in range(len(handles)):
+            call(i)
+        torch.cuda.synchronize()
+        ref = outs[0]
+        for i, (name, _, _) in enumerate(handles):
+            same = torch.equal(outs[i][0], ref[0]) and torch.equal(outs[i][1], ref[1])
+            print(f"{'packed' if packed else 'int32'} {name}: outputs equal first={same} "
+                  f"stats={ops.read_stats(stats[i])}", flush=True)
+        for r in range(ROUNDS):
+            for i in range(len(handles)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                call(i)
+                e1.record()
+                times[i].append((e0, e1))
+        torch.cuda.synchronize()
+        nbytes = 2 * B * L * H * ((3 * g if packed else 4 * g) + 4 + 2 * D)
+        for i, (name, _, _) in enumerate(handles):
+            us = [a.elapsed_time(b) * 1e3 for a, b in times[i]]
+            med = statistics.median(us)
+            print(f"{'packed' if packed else 'int32'} {name}: median {med:.1f} us min {min(us):.1f} "
+                  f"({nbytes / med / 1e3:.0f} GB/s, {nbytes / med / 1e3 / 8000 * 100:.1f}% of 8 TB/s)",
+                  flush=True)
+        del caches, scales, outs
+
+
+if __name__ == "__main__":
+    main()
