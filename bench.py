@@ -69,6 +69,8 @@ def parse():
                          "step ~8 us; timing every step cost 7-9%% of throughput)")
     ap.add_argument("--no-fused", action="store_true",
                     help="skip the fused Golay read (shim_read_batch) measurement")
+    ap.add_argument("--no-rows", action="store_true",
+                    help="skip the per-head rows (golay_encode_rows / decode_rows) measurement")
     ap.add_argument("--dist", action="store_true",
                     help="create the RCCL process group even at world size 1 (exercises the "
                          "barrier and the stats/timing all-reduces on one GPU)")
@@ -170,6 +172,43 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
             "codewords_per_s": rows * g / (ms * 1e-3),
             "bytes_per_launch": rows * bytes_per_row,
             "bytes_per_token_row": bytes_per_row, "hbm_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
+            "write_share": 2 * D / bytes_per_row,
+            "ceiling_note": "write-heavy mix: non-temporal write-only streams peak at 4.8-5.3 TB/s and "
+                            "read-only at 6.1-6.9 TB/s on MI355X (profiles/r02/hbm_ceiling.log)",
+            "timing": f"HIP events carried by the dispatch, mean of {steps} launches"}
+
+
+def rows_bench(dev, x, noisy_rows, steps, warmup):
+    """Per-head Golay rows (the shim's and the config-5 sweep's layout,
+    ecc_shim.py:623-682): golay_encode_rows of the [8,4096,32,128] nibbles and
+    golay_decode_rows of its BER-1e-2 codewords, kernel time from events carried
+    by each dispatch.  Bytes/row: 128 nibble bytes + 43 * 4 codeword bytes."""
+    from kvecc import ops
+    rows, d = x.numel() // D, D
+    cw = torch.empty(rows, (D + 2) // 3, dtype=torch.int32, device=dev)
+    nib = torch.empty(rows, D, dtype=torch.uint8, device=dev)
+    st = ops.new_stats(dev)
+    xr = x.view(rows, D)
+    for _ in range(warmup):
+        ops.golay_encode_rows_into(xr, cw)
+        ops.golay_decode_rows_into(noisy_rows, nib, st)
+    ev = [ops.kernel_timer(dev) + ops.kernel_timer(dev) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ops.time_next_launch(ev[k][0], ev[k][1])
+        ops.golay_encode_rows_into(xr, cw)
+        ops.time_next_launch(ev[k][2], ev[k][3])
+        ops.golay_decode_rows_into(noisy_rows, nib, st)
+    torch.cuda.synchronize()
+    enc = sum(e[0].elapsed_time(e[1]) for e in ev) / steps
+    dec = sum(e[2].elapsed_time(e[3]) for e in ev) / steps
+    nbytes = rows * (D + 4 * ((D + 2) // 3))
+    return {"workload": "golay_encode_rows / golay_decode_rows, [8,4096,32,128] (43 codewords per head row)",
+            "kernels": ["golay_encode_rows_reg_kernel", "golay_decode_rows_reg_kernel"],
+            "kernel_ms": {"encode": enc, "decode": dec}, "bytes_per_launch": nbytes,
+            "hbm_gbs": {"encode": nbytes / (enc * 1e-3) / 1e9, "decode": nbytes / (dec * 1e-3) / 1e9},
+            "frac": {"encode": nbytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "decode": nbytes / (dec * 1e-3) / 1e9 / HBM_PEAK_GBS},
             "timing": f"HIP events carried by the dispatch, mean of {steps} launches"}
 
 
@@ -407,6 +446,14 @@ def main():
                   "hbm_gbs": {"encode": 4.5 * m / (p_enc * 1e-3) / 1e9,
                               "decode": 4.625 * m / (p_dec * 1e-3) / 1e9}}
 
+    rows = None
+    if not args.no_rows:
+        xr = torch.randint(0, 16, (B, L, H, D), generator=torch.Generator().manual_seed(rank),
+                           dtype=torch.uint8).to(dev)
+        noisy_rows = noisy.view(B * L * H, gsz)  # the same BER-1e-2 codewords, one row per head
+        rows = rows_bench(dev, xr, noisy_rows, max(args.steps, 10), args.warmup)
+        del xr
+
     fused = None
     if not args.no_fused:
         fused = fused_decode_bench(dev, max(args.steps, 10), args.warmup)
@@ -463,6 +510,7 @@ def main():
         "decode_stats": {"bits_corrected": bits, "uncorrectable": unc, "steps": args.steps},
         "inject": inject,
         "fused_golay_decode": fused,
+        "golay_rows": rows,
         "packed": packed,
         "cpu_baseline": cpu,
         "cpu_backend": host,

@@ -31,6 +31,8 @@
 // same as its initial max, so each accumulates weight 1 on the masked row
 // decode(0) - 8 = -8, attention_ecc.py:342,391-423), Golay 0
 // (reference_attention_ecc's torch.zeros, :806-807,885-886).
+#include <type_traits>
+
 #include "kvecc_internal.h"
 
 namespace kvecc {
@@ -78,6 +80,13 @@ constexpr int kGolayPackedVec = 4;
 #ifndef KVECC_ATTN_GOLAY_SPREAD
 #define KVECC_ATTN_GOLAY_SPREAD 1
 #endif
+// Hamming(8,4) decodes through a 256-entry LDS table of data(b) - 8: as int8
+// (ds_read_i8 + v_cvt_f32_i32; the 256 bytes are 64 dwords over 32 banks, so
+// random lookups conflict at most 2-way) or as fp32 (0; 256 dwords, ~3.5-way)
+#ifndef KVECC_ATTN_H84_LUT8
+#define KVECC_ATTN_H84_LUT8 1
+#endif
+typedef typename std::conditional<KVECC_ATTN_H84_LUT8 != 0, int8_t, float>::type h84_lut_t;
 constexpr bool is_golay(int codec) { return codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED; }
 
 struct AttnArgs {
@@ -173,12 +182,12 @@ struct Chunk {
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
   // correction tables (uncorrectable words keep their data, as golay_decode)
-  __device__ __forceinline__ void decode(const float *lut, const uint32_t *gtab, float *v) const {
+  __device__ __forceinline__ void decode(const h84_lut_t *lut, const uint32_t *gtab, float *v) const {
     if constexpr (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[4 * k + e] = lut[(w[k] >> (8 * e)) & 0xFFu];
+        for (int e = 0; e < 4; ++e) v[4 * k + e] = (float)lut[(w[k] >> (8 * e)) & 0xFFu];
       }
     } else {
 #pragma unroll
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   __shared__ float red_own[kSpread ? 1 : TP * W * E];  // per-group acc
   float *red = kSpread ? reinterpret_cast<float *>(gtab) : red_own;
   __shared__ float gml[2][TP];             // per-group running max / sum
-  __shared__ float lut[CODEC == KVECC_CODEC_H84 ? 256 : 1];  // H(8,4): codeword byte -> data - 8
+  __shared__ h84_lut_t lut[CODEC == KVECC_CODEC_H84 ? 256 : 1];  // H(8,4): codeword byte -> data - 8
 
   const int64_t bh = blockIdx.y;
   const int64_t b = bh / a.heads, h = bh % a.heads;
@@ -322,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   if (CODEC == KVECC_CODEC_H84 && threadIdx.x < 256) {
     uint32_t q, t, n1 = 0, n2 = 0;
     h84_decode4(threadIdx.x, q, t, n1, n2);
-    lut[threadIdx.x] = (float)(q & 0xFu) - 8.0f;
+    lut[threadIdx.x] = (h84_lut_t)((int)(q & 0xFu) - 8);
   }
   float qv[E];
   float qsum = 0.0f;  // sum of this lane's q (folds the decode's kOffset out of the K sums)

@@ -261,6 +261,36 @@ def golay_decode_rows(codewords: torch.Tensor, d: int, stats=None) -> torch.Tens
               _stream(codewords.device))
     return out
 
+def golay_encode_rows_into(nibbles: torch.Tensor, out: torch.Tensor) -> None:
+    """golay_encode_rows into a caller buffer: contiguous uint8 [..., D] nibbles ->
+    contiguous int32 [..., ceil(D/3)] codewords (asynchronous on the stream)."""
+    _check_gpu(nibbles)
+    d = nibbles.shape[-1]
+    g = (d + 2) // 3
+    if (nibbles.dtype != torch.uint8 or out.dtype != torch.int32 or not nibbles.is_contiguous()
+            or not out.is_contiguous() or out.shape[-1] != g or out.numel() * 3 < nibbles.numel()
+            or out.device != nibbles.device):
+        raise ValueError("golay_encode_rows_into: contiguous uint8 [..., D] -> int32 [..., ceil(D/3)]")
+    rows = nibbles.numel() // d if d else 0
+    _ensure_device(nibbles.device)
+    _lib.call("kvecc_golay_encode_rows", _ptr(nibbles), _ptr(out), rows, d, _stream(nibbles.device))
+
+
+def golay_decode_rows_into(codewords: torch.Tensor, out: torch.Tensor, stats=None) -> None:
+    """golay_decode_rows into a caller buffer: contiguous int32 [..., ceil(D/3)] ->
+    contiguous uint8 [..., D]; statistics accumulate into `stats` (asynchronous)."""
+    _check_gpu(codewords)
+    d = out.shape[-1]
+    g = (d + 2) // 3
+    if (codewords.dtype != torch.int32 or out.dtype != torch.uint8 or not codewords.is_contiguous()
+            or not out.is_contiguous() or codewords.shape[-1] != g or codewords.numel() // max(g, 1) * d != out.numel()
+            or out.device != codewords.device):
+        raise ValueError("golay_decode_rows_into: contiguous int32 [..., ceil(D/3)] -> uint8 [..., D]")
+    rows = codewords.numel() // g if g else 0
+    _ensure_device(codewords.device)
+    _lib.call("kvecc_golay_decode_rows", _ptr(codewords), _ptr(out), rows, d, _ptr(stats), _stream(codewords.device))
+
+
 
 # ============================================================================
 # Fault injection

@@ -290,3 +290,22 @@ def test_scale_rules(cpu, oracle, dtype):
     assert int((scales["div7"] != scales["mul_inv7"]).sum()) > 50
     with pytest.raises(ValueError):
         cpu.quantize_rows(x, scale_rule="div8")
+
+
+def test_golay_rows_into(cpu):
+    """The _into twins write the allocating calls' bits into caller buffers and
+    reject mismatched buffers."""
+    g = torch.Generator().manual_seed(11)
+    x = torch.randint(0, 16, (4, 6, 128), dtype=torch.uint8, generator=g)
+    cw = torch.empty(4, 6, 43, dtype=torch.int32)
+    cpu.golay_encode_rows_into(x, cw)
+    assert torch.equal(cw, cpu.golay_encode_rows(x))
+    noisy = cpu.inject_bit_errors_triton(cw, 0.05, 24, seed=3)
+    out, st, st2 = torch.empty_like(x), cpu.new_stats(), cpu.new_stats()
+    cpu.golay_decode_rows_into(noisy, out, st)
+    assert torch.equal(out, cpu.golay_decode_rows(noisy, 128, st2))
+    assert cpu.read_stats(st) == cpu.read_stats(st2)
+    with pytest.raises(ValueError):
+        cpu.golay_encode_rows_into(x, torch.empty(4, 6, 42, dtype=torch.int32))
+    with pytest.raises(ValueError):
+        cpu.golay_decode_rows_into(noisy, torch.empty(4, 6, 130, dtype=torch.uint8))

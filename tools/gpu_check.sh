@@ -4,7 +4,7 @@
 # in anything but success/test-failure (fault, abort, timeout) stops the script.
 # usage: tools/gpu_check.sh <tag> [steps...]   steps: test smoke bench dist prof pmc
 set -u
-TAG=${1:-r01}
+TAG=${1:-r02}
 shift || true
 STEPS=${@:-test smoke bench prof pmc}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
