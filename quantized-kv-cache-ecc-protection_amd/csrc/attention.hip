@@ -20,7 +20,8 @@
 // groups merge through LDS.  The split's (max, sum, acc[D]) go to a workspace
 // that a second small launch combines.  Query head h reads cache head
 // h / (H / Hkv) (the reference indexes cache head h, which only agrees without
-// GQA).  Numerics: fp32 throughout, expf.  The result differs from the
+// GQA).  Numerics: fp32 throughout, softmax as exp2 of log2(e)-scaled scores
+// (one v_exp_f32 per exponential).  The result differs from the
 // reference's sequential online softmax by fp32 summation order and, for Golay,
 // by the -8 fold: the kernel sums q*n and p*s*n over the raw nibbles and
 // subtracts 8*sum(q) / 8*sum(p*s) once per split (acc - 8*psum), which loses a
@@ -48,9 +49,16 @@ constexpr int kAttnMaxD = 256;
 #ifndef KVECC_ATTN_GOLAY_UNROLL
 #define KVECC_ATTN_GOLAY_UNROLL 2
 #endif
-constexpr int kUnroll = KVECC_ATTN_UNROLL;  // token rows in flight per lane group
+// Hamming(8,4): 2 rows in flight measured 56.9 / 57.1 us vs 60.3 / 60.0 at 4
+// (random / encoded caches, int8 table; tools/exp/run_attn.py)
+#ifndef KVECC_ATTN_H84_UNROLL
+#define KVECC_ATTN_H84_UNROLL 2
+#endif
+constexpr int kUnroll = KVECC_ATTN_UNROLL;  // token rows in flight per lane group (packed Golay)
 constexpr int kGolayUnroll = KVECC_ATTN_GOLAY_UNROLL;
-constexpr int kMaxUnroll = kUnroll > kGolayUnroll ? kUnroll : kGolayUnroll;
+constexpr int kH84Unroll = KVECC_ATTN_H84_UNROLL;
+constexpr int kMaxUnroll = kUnroll > kGolayUnroll ? (kUnroll > kH84Unroll ? kUnroll : kH84Unroll)
+                                                  : (kGolayUnroll > kH84Unroll ? kGolayUnroll : kH84Unroll);
 // codeword words per lane of a token row (A/B knobs: tools/exp/run_attn.py)
 #ifndef KVECC_ATTN_H84_VEC
 #define KVECC_ATTN_H84_VEC 4
@@ -87,6 +95,20 @@ constexpr int kGolayPackedVec = 4;
 #define KVECC_ATTN_H84_LUT8 1
 #endif
 typedef typename std::conditional<KVECC_ATTN_H84_LUT8 != 0, int8_t, float>::type h84_lut_t;
+// Softmax in base 2: the query is pre-scaled by sm_scale * log2(e), so every
+// exponential is one v_exp_f32 (exp2) instead of expf's ~10-instruction range
+// reduction; the split maxima in the workspace are in the same log2 units
+#ifndef KVECC_ATTN_EXP2
+#define KVECC_ATTN_EXP2 1
+#endif
+__device__ __forceinline__ float attn_exp(float x) {
+#if KVECC_ATTN_EXP2
+  return __builtin_amdgcn_exp2f(x);  // exp2(-inf) = 0
+#else
+  return expf(x);
+#endif
+}
+constexpr float kAttnLogScale = KVECC_ATTN_EXP2 ? 1.4426950408889634f : 1.0f;  // log2(e)
 constexpr bool is_golay(int codec) { return codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED; }
 
 struct AttnArgs {
@@ -262,7 +284,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
   // cache row of each token of the split (-1 = no block / past the split),
   // padded so the unrolled loop reads it without bounds checks
-  constexpr int U = CODEC == KVECC_CODEC_GOLAY ? kGolayUnroll : kUnroll;  // rows in flight
+  constexpr int U = CODEC == KVECC_CODEC_GOLAY ? kGolayUnroll : CODEC == KVECC_CODEC_H84 ? kH84Unroll : kUnroll;
   __shared__ int32_t rows[kMaxSplit + (kMaxUnroll - 1) * kBlock];
   // Golay tables copied from the device: the 32 KiB spread tables, or
   // parity[4096] then correct[4096] as uint16 (16 KiB).  With the spread
@@ -334,12 +356,13 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
     lut[threadIdx.x] = (h84_lut_t)((int)(q & 0xFu) - 8);
   }
   float qv[E];
+  const float qscale = a.sm_scale * kAttnLogScale;
   float qsum = 0.0f;  // sum of this lane's q (folds the decode's kOffset out of the K sums)
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int64_t di = (int64_t)c * E + e;
     qv[e] = (live && di < a.d)
-                ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h) * a.d + di]) * a.sm_scale
+                ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h) * a.d + di]) * qscale
                 : 0.0f;
     qsum += qv[e];
   }
@@ -397,14 +420,14 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       mn = fmaxf(mn, sc[u]);
     }
     if (mn == -INFINITY) continue;  // no valid row yet (uniform per group)
-    const float alpha = expf(m - mn);  // m = -inf -> 0
+    const float alpha = attn_exp(m - mn);  // m = -inf -> 0
     l *= alpha;
     psum *= alpha;
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] *= alpha;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float p = expf(sc[u] - mn);  // invalid rows: exp(-inf) = 0
+      const float p = attn_exp(sc[u] - mn);  // invalid rows: exp(-inf) = 0
       l += p;
       if (live) {
         float vv[E];
@@ -434,7 +457,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   for (int gi = 0; gi < TP; ++gi) M = fmaxf(M, gml[0][gi]);
   if (threadIdx.x < TP) {
     const float mg = gml[0][threadIdx.x];
-    gw[threadIdx.x] = mg == -INFINITY ? 0.0f : expf(mg - M);
+    gw[threadIdx.x] = mg == -INFINITY ? 0.0f : attn_exp(mg - M);
   }
   __syncthreads();
   for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
@@ -471,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) 
   float L = 0.0f;
   for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) {
     const float ms = ws[s * stride];
-    const float w = ms == -INFINITY ? 0.0f : expf(ms - mx);
+    const float w = ms == -INFINITY ? 0.0f : attn_exp(ms - mx);
     wt[s] = w;
     L += w * ws[s * stride + 1];
   }
@@ -556,13 +579,17 @@ static int launch_codec(int codec, const AttnArgs &a, int64_t batch, hipStream_t
 }
 
 // tokens per workgroup: the largest power of two <= kMaxSplit that still gives
-// >= 4 workgroups per CU (small batch*heads decode steps split finer)
+// >= KVECC_ATTN_WG_PER_CU workgroups per CU (small batch*heads decode steps
+// split finer)
+#ifndef KVECC_ATTN_WG_PER_CU
+#define KVECC_ATTN_WG_PER_CU 4
+#endif
 static int64_t choose_split(int64_t bh, int64_t max_context_len) {
   // longer splits amortise each workgroup's fixed work (table staging, the
   // group merge); measured best at 1024 for both codecs at [8,4096,32,128]
   const int64_t top = kMaxSplit;
   int64_t split = top;
-  const int64_t want = 4LL * cu_count();
+  const int64_t want = (int64_t)KVECC_ATTN_WG_PER_CU * cu_count();
   while (split > 32 && bh * cdiv(max_context_len, split) < want) split >>= 1;
   while (cdiv(max_context_len, split) > kMaxSplits && split < top) split <<= 1;
   return split;

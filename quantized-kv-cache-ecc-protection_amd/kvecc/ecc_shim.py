@@ -28,6 +28,7 @@ import torch.nn.functional as F
 
 from ._lib import golay_packed_row_bytes
 from .backends import get_codec_backend
+from .memory_layout import kv_cache_pair
 
 try:  # optional, as in the reference (:54)
     from transformers.models.llama.modeling_llama import LlamaRotaryEmbedding
@@ -160,8 +161,8 @@ class SimpleBlockManager:
                 codec, torch.uint8)
         self.codewords_per_head = self.values_per_head
         shape = (num_blocks, num_layers, num_kv_heads, self.codewords_per_head)
-        self.k_cache = torch.zeros(shape, dtype=self.cache_dtype, device=device)
-        self.v_cache = torch.zeros(shape, dtype=self.cache_dtype, device=device)
+        # one allocation, V skewed off K's HBM channels (memory_layout.kv_cache_pair)
+        self.k_cache, self.v_cache = kv_cache_pair(shape, self.cache_dtype, device)
         sshape = (num_blocks, num_layers, num_kv_heads, block_size)
         self.k_scales = torch.zeros(sshape, dtype=torch.float32, device=device)
         self.v_scales = torch.zeros(sshape, dtype=torch.float32, device=device)

@@ -14,6 +14,29 @@ import torch
 
 from .config import get_physical_dtype
 
+# V starts this many bytes past the 256-byte-rounded end of K (see kv_cache_pair)
+KV_SKEW_BYTES = 12800
+
+
+def kv_cache_pair(shape, dtype, device):
+    """Zeroed K and V caches of one shape as two views of ONE allocation, V
+    starting KV_SKEW_BYTES past K's 256-byte-rounded end.
+
+    Paged decode attention reads K row r and V row r together.  In two separate
+    equal-size allocations those rows sit exactly one allocation apart, which on
+    MI355X maps them onto the same HBM channels and banks: Hamming(8,4) / Golay /
+    packed Golay attention at [8,4096,32,128] ran 62.6 / 80.7 / 74.2 us with V
+    right after K against 56.1 / 74.2 / 71.5 us with a 12,800-byte skew
+    (tools/exp/attn_alias.py, profiles/r02/attention/kv_skew.log).  Both views
+    are contiguous and 256-byte aligned; nothing else about the layout changes."""
+    n = 1
+    for x in shape:
+        n *= int(x)
+    esz = torch.empty((), dtype=dtype).element_size()
+    v_off = ((n * esz + 255) // 256 * 256 + KV_SKEW_BYTES) // esz
+    buf = torch.zeros(v_off + n, dtype=dtype, device=device)
+    return buf[:n].view(shape), buf[v_off:v_off + n].view(shape)
+
 
 class ECCCacheConfig:
     def __init__(self, num_heads, head_size, num_layers, block_size=16, num_blocks=256,

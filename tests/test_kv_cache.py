@@ -80,3 +80,22 @@ def test_benchmark_harness(gpu):
     r = bh.benchmark_encode_inject_decode(codec="golay", n_elements=9_999, ber=0.01, warmup=2,
                                           repeat=5)
     assert r.latency_us > 0
+
+
+def test_kv_cache_pair_layout():
+    """K and V are contiguous, zeroed, 256-byte aligned views of one allocation,
+    V skewed past K (memory_layout.kv_cache_pair); SimpleBlockManager uses it."""
+    import torch
+    from kvecc.ecc_shim import SimpleBlockManager
+    from kvecc.memory_layout import KV_SKEW_BYTES, kv_cache_pair
+    for dtype, shape in ((torch.uint8, (5, 2, 3, 16 * 7)), (torch.int32, (4, 1, 2, 16 * 43))):
+        k, v = kv_cache_pair(shape, dtype, "cpu")
+        assert k.shape == v.shape == shape and k.dtype == v.dtype == dtype
+        assert k.is_contiguous() and v.is_contiguous()
+        assert not k.any() and not v.any()
+        gap = v.data_ptr() - k.data_ptr() - k.numel() * k.element_size()
+        assert gap >= KV_SKEW_BYTES and (v.data_ptr() - k.data_ptr()) % 256 == 0
+        k.fill_(1)
+        assert not v.any()  # disjoint
+    mgr = SimpleBlockManager(8, 16, 2, 4, 64, device="cpu", codec="golay")
+    assert mgr.v_cache.data_ptr() - mgr.k_cache.data_ptr() >= mgr.k_cache.numel() * 4 + KV_SKEW_BYTES

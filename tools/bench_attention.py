@@ -29,7 +29,9 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--ctx", type=int, default=4096)
     ap.add_argument("--bs", type=int, default=16)
-    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100,
+                    help="untimed calls first (a few ms of work: clocks ramp up on a cold GPU)")
     args = ap.parse_args()
     from kvecc import ops
     dev = torch.device("cuda:0")
@@ -39,13 +41,11 @@ def main():
     per = args.d if args.codec == "hamming84" else (args.d + 2) // 3
     if args.codec == "golay_packed":  # bytes per token row (KVECC_GOLAY_PACKED_ROW)
         per = (3 * per + 3) // 4 * 4
-    if args.codec != "golay":
-        kc = torch.randint(0, 256, (blocks, 1, args.kv_heads, args.bs * per), dtype=torch.uint8,
-                           device=dev, generator=g)
-    else:
-        kc = torch.randint(0, 1 << 24, (blocks, 1, args.kv_heads, args.bs * per),
-                           dtype=torch.int32, device=dev, generator=g)
-    vc = kc.clone()
+    from kvecc.memory_layout import kv_cache_pair  # K/V as SimpleBlockManager lays them out
+    kc, vc = kv_cache_pair((blocks, 1, args.kv_heads, args.bs * per),
+                           torch.int32 if args.codec == "golay" else torch.uint8, dev)
+    kc.random_(0, 1 << 24 if args.codec == "golay" else 256, generator=g)
+    vc.copy_(kc.roll(1, 0))
     ks = torch.rand(blocks, 1, args.kv_heads, args.bs, device=dev, generator=g)
     vs = torch.rand_like(ks)
     table = torch.randperm(blocks, device=dev, generator=g).to(torch.int32).view(args.batch, nb)
@@ -54,7 +54,7 @@ def main():
     out = torch.empty_like(q)
     call = lambda: ops.paged_attention_into(q, kc, vc, table, lens, ks, vs, out, 0, args.bs,  # noqa
                                             1 / math.sqrt(args.d), args.codec, args.ctx)
-    for _ in range(5):
+    for _ in range(args.warmup):
         call()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()

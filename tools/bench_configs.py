@@ -33,7 +33,7 @@ import torch  # noqa: E402
 PEAK = 8000.0  # GB/s
 
 
-def timed(fn, reps, warmup=3):
+def timed(fn, reps, warmup=10):
     for _ in range(warmup):
         fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -172,11 +172,10 @@ def extended(reps):
             per = (3 * per + 3) // 4 * 4
         nb = ctx // bs
         blocks = b * nb
-        if codec != "golay":
-            kc = torch.randint(0, 256, (blocks, 1, hq, bs * per), dtype=torch.uint8, device=dev)
-        else:
-            kc = torch.randint(0, 1 << 24, (blocks, 1, hq, bs * per), dtype=torch.int32, device=dev)
-        vc = kc.clone()
+        from kvecc.memory_layout import kv_cache_pair  # K/V as SimpleBlockManager lays them out
+        kc, vc = kv_cache_pair((blocks, 1, hq, bs * per), torch.int32 if codec == "golay" else torch.uint8, dev)
+        kc.random_(0, 1 << 24 if codec == "golay" else 256)
+        vc.copy_(kc.roll(1, 0))
         ks = torch.rand(blocks, 1, hq, bs, device=dev)
         vs = torch.rand_like(ks)
         table = torch.randperm(blocks, device=dev).to(torch.int32).view(b, nb)
