@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--event-every", type=int, default=10,
                     help="time the kernels of every k-th timed step (a timed dispatch costs the "
                          "step ~8 us; timing every step cost 7-9%% of throughput)")
+    ap.add_argument("--roofline-samples", type=int, default=30,
+                    help="extra encode/decode steps after the timed region whose kernels carry "
+                         "events, added to the roofline's kernel-time sample")
     ap.add_argument("--no-fused", action="store_true",
                     help="skip the fused Golay read (shim_read_batch) measurement")
     ap.add_argument("--no-rows", action="store_true",
@@ -332,7 +335,7 @@ def main():
 
     kernel_timing = args.timing == "kernel"
 
-    def step(ev=None):
+    def step(ev=None, st=stats):
         if ev is not None and kernel_timing:
             ops.time_next_launch(ev[0], ev[1])
         elif ev is not None:
@@ -342,7 +345,7 @@ def main():
             ops.time_next_launch(ev[2], ev[3])
         elif ev is not None:
             ev[1].record()
-        ops.golay_decode_into(noisy, out_trip, counts, stats)
+        ops.golay_decode_into(noisy, out_trip, counts, st)
         if ev is not None and not kernel_timing:
             ev[2].record()
 
@@ -374,6 +377,15 @@ def main():
 
     elapsed = t1 - t0
     timed = [events[k] for k in sampled]
+    if kernel_timing and args.roofline_samples > 0:
+        # more kernel-carried samples for the roofline, after the timed region
+        # (the throughput above is untouched; statistics go to a scratch buffer)
+        scratch = ops.new_stats(dev)
+        extra = [ops.kernel_timer(dev) + ops.kernel_timer(dev) for _ in range(args.roofline_samples)]
+        for ev in extra:
+            step(ev, scratch)
+        torch.cuda.synchronize()
+        timed = timed + extra
     if kernel_timing:
         enc_ms = sum(e[0].elapsed_time(e[1]) for e in timed) / len(timed)
         dec_ms = sum(e[2].elapsed_time(e[3]) for e in timed) / len(timed)
@@ -505,7 +517,9 @@ def main():
                      "frac": dec_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "golay_decode_kernel", "bytes_per_launch": DECODE_BYTES_PER_CW * m,
                      "timing": (f"HIP events carried by the kernel dispatches (hipExtLaunchKernel) "
-                                f"of every {args.event_every}th timed step" if kernel_timing else
+                                f"of every {args.event_every}th timed step and of "
+                                f"{args.roofline_samples} steps after the timed region "
+                                f"({len(timed)} samples)" if kernel_timing else
                                 f"hipEventRecord markers on every {args.event_every}th timed step")},
         "decode_stats": {"bits_corrected": bits, "uncorrectable": unc, "steps": args.steps},
         "inject": inject,
