@@ -689,6 +689,7 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
            l % block_size;
   };
   const int64_t per_side = hkv * ctx;
+  const std::vector<uint8_t> zero_row(golay ? 0 : (size_t)d, 0);  // a missing block's codewords
   std::vector<Acc2> acc(std::max(1, clamp_threads(threads, 2 * per_side, 1)));
   parallel_for(2 * per_side, threads, 1, [&](int64_t b, int64_t e, int t) {
     uint32_t n1 = 0, n2 = 0;
@@ -700,7 +701,7 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
       const int64_t slot = slot_of(l, h);
       void *out = side ? v_out : k_out;
       const int64_t o = (h * ctx + l) * d;
-      if (golay && block_table[l / block_size] < 0) {  // no physical block: zeros
+      if (block_table[l / block_size] < 0) {  // no physical block: zeros
         for (int64_t j = 0; j < d; ++j) store_y(out, out_dtype, o + j, 0.0f);
         continue;
       }
@@ -725,8 +726,10 @@ KVECC_API int kvecc_cpu_shim_read(const void *k_cache, const void *v_cache, cons
       }
       const uint8_t *base = reinterpret_cast<const uint8_t *>(side ? v_cache : k_cache);
       const uint8_t *c = base + slot * d;
-      const uint8_t *cl = base + slot_of(l > 0 ? l - 1 : 0, h) * d;
-      const uint8_t *cr = base + slot_of(l + 1 < ctx ? l + 1 : ctx - 1, h) * d;
+      // neighbours in a missing block read as zero codewords (the device kernels do the same)
+      const int64_t ll = l > 0 ? l - 1 : 0, lr = l + 1 < ctx ? l + 1 : ctx - 1;
+      const uint8_t *cl = block_table[ll / block_size] < 0 ? zero_row.data() : base + slot_of(ll, h) * d;
+      const uint8_t *cr = block_table[lr / block_size] < 0 ? zero_row.data() : base + slot_of(lr, h) * d;
       for (int64_t j = 0; j < d; ++j) {
         uint32_t q = c[j], type = 0;
         if (codec == KVECC_CODEC_H84) {

@@ -397,6 +397,10 @@ template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileTPI][kTileStage];
+  // row scales of the staged tiles: written in phase 1, read in phase 2 (a
+  // scale kept in a register across the next tile's prefetch made the compiler
+  // wait for that prefetch before phase 2)
+  __shared__ float scale_all[kTileWaves][kTileTPI][kWave];
   {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(tab);
@@ -450,6 +454,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     for (int k = 0; k < kTileTPI; ++k) {
       if (!valid[k]) continue;
       uint8_t *stage = stage_all[wave][k];
+      scale_all[wave][k][lane] = scale[k];
 #pragma unroll
       for (int i = 0; i < kTileGroups; ++i) {
         if (i * kWave >= (int)groups) break;  // uniform
@@ -484,12 +489,10 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     // ---- prefetch the next tiles' codewords and scales ---------------------------
     ShimTile t[kTileTPI];
     bool tv[kTileTPI];
-    float ts[kTileTPI];
 #pragma unroll
     for (int k = 0; k < kTileTPI; ++k) {
       t[k] = cur[k];
       tv[k] = valid[k];
-      ts[k] = scale[k];
     }
     u += kTileTPI * nwaves;
     const bool more = u < a.units;
@@ -505,9 +508,8 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
         for (int i = 0; i < kTileChunks; ++i) {
           if (i * kWave >= (int)chunks) break;  // uniform
           const uint32_t r = it.r2[i], j = it.j2[i];
-          // every lane joins the bpermute (lanes past the tile read a harmless row)
-          const float s = __shfl(ts[k], (int)min(r, (uint32_t)kWave - 1u), kWave);
           if (r < t[k].rows) {
+            const float s = scale_all[wave][k][r];
             float o[8];
             const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + 8 * j);
             const uint32_t lo = src[0], hi = src[1];
@@ -539,6 +541,168 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
       uint64_t *slot = a.stats + ((blockIdx.x * kTileWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
       if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
       if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+    }
+  }
+}
+
+// ---- byte codecs (raw INT4, H(7,4), H(8,4) [+ interpolation]) through wave tiles
+// The Golay tile scheme for one-byte codewords (d % 16 == 0): a wave owns the
+// `tr` rows of one (side, sequence, head, block).  Phase 1: each lane decodes
+// 16-byte chunks of codewords (16 values, SWAR through the v_perm tables) into
+// the wave's LDS tile as one byte per value, data | error type << 4; with
+// interpolation the tile also holds the decoded neighbour rows of positions
+// pos0 - 1 and pos0 + rows (clamped to the context, as the composed read
+// clamps), which live in other blocks.  Phase 2: each lane takes a 16-value
+// chunk of a row, interpolates double errors from the rows above and below
+// (decoded, not interpolated, neighbours), dequantizes and writes 16-byte
+// non-temporal stores.  A row in a missing block (table entry -1) reads as
+// zero codewords and outputs +0, as in the Golay kernel and the host twin.
+constexpr int kByteTileItems = 4;  // 16-value chunks per lane per phase (max)
+
+template <typename TO, int CODEC, bool INTERP, bool STATS>
+__global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ float scale_all[kTileWaves][kWave];  // row scales, staged like the rows
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  uint8_t *stage = stage_all[wave];
+  const uint32_t nwaves = gridDim.x * kTileWaves;
+  const uint32_t cpr = a.d / 16;       // 16-byte chunks per row
+  const uint32_t items = a.tr * cpr;   // <= 64 * kByteTileItems (host check)
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    ir[i] = f / cpr;
+    ic[i] = f - ir[i] * cpr;
+  }
+  uint32_t n1 = 0, n2 = 0;
+  uint32_t u = blockIdx.x * kTileWaves + wave;
+  if (u >= a.units) return;
+
+  ShimTile cur;
+  u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
+  float scale;
+  auto fetch = [&](uint32_t uu) {
+    cur = shim_tile(a, uu);
+    const bool live = cur.row0 >= 0;
+    const uint32_t side = uni(cur.side);
+    const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + (live ? cur.row0 : 0) * (int64_t)a.d);
+    const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + (live ? cur.row0 : 0)));
+    const uint32_t nrows = uni(live ? cur.rows : 0u);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.d), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ss =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+    scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;  // uniform
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
+    }
+    if (INTERP && cur.rows > 0) {  // neighbour rows: lanes [0, cpr) above, [cpr, 2 cpr) below
+      // both positions and their blocks are wave-uniform: scalar loads, so the
+      // halo does not wait behind the previous tile's stores
+      const bool below = lane >= cpr;
+      const uint32_t bh = uni(cur.bh), b = bh / a.hkv, h = bh - b * a.hkv;
+      const uint32_t pa = uni(cur.pos0 > 0 ? cur.pos0 - 1 : 0u), pb = uni(min(cur.pos0 + cur.rows, a.ctx - 1));
+      const int32_t ba = ld_scalar(a.table + (int64_t)b * a.tstride + pa / a.bs);
+      const int32_t bb = ld_scalar(a.table + (int64_t)b * a.tstride + pb / a.bs);
+      const uint32_t pos = below ? pb : pa;
+      const uint32_t lb = pos / a.bs;
+      const int32_t blk = below ? bb : ba;
+      hw = u32x4{0u, 0u, 0u, 0u};
+      if (lane < 2 * cpr && blk >= 0) {
+        const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - lb * a.bs);
+        hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[side]) + row * a.d) +
+                       (below ? lane - cpr : lane));
+      }
+    }
+  };
+  // 4 codewords -> data | type << 4 per byte (and the statistics)
+  auto dec = [&](uint32_t cw, bool count) -> uint32_t {
+    uint32_t q = cw, t = 0, s1 = 0, s2 = 0;
+    if (CODEC == KVECC_CODEC_H84) {
+      h84_decode4(cw, q, t, s1, s2);
+    } else if (CODEC == KVECC_CODEC_H74) {
+      h74_decode4(cw, q, t, s1);
+      t = 0;
+    }
+    if (STATS && count) {
+      n1 += s1;
+      n2 += s2;
+    }
+    return q | t << 4;
+  };
+  fetch(u);
+  for (;;) {
+    // ---- phase 1: decode into the LDS tile (row r at (r + INTERP) * d) --------
+    const uint32_t off0 = INTERP ? a.d : 0u;
+    scale_all[wave][lane] = scale;
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;  // uniform
+      const bool real = ir[i] < cur.rows;  // rows past the tile loaded 0: no statistics
+      const u32x4 d4{dec(w[i].x, real), dec(w[i].y, real), dec(w[i].z, real), dec(w[i].w, real)};
+      // (with interpolation, rows past the tile's end would overwrite the row below)
+      if (ir[i] < (INTERP ? cur.rows : a.tr)) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
+    }
+    if (INTERP && lane < 2 * cpr) {  // neighbours: row 0 above, row rows + 1 below
+      const u32x4 d4{dec(hw.x, false), dec(hw.y, false), dec(hw.z, false), dec(hw.w, false)};
+      const uint32_t r = lane >= cpr ? cur.rows + 1 : 0u;
+      *reinterpret_cast<u32x4 *>(stage + r * a.d + 16 * (lane >= cpr ? lane - cpr : lane)) = d4;
+    }
+    wave_lds_sync();
+    const ShimTile t = cur;
+    u += nwaves;
+    const bool more = u < a.units;
+    if (more) fetch(u);
+    // ---- phase 2: interpolate, dequantize, 16 values per lane -------------------
+    TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;  // uniform
+      const uint32_t r = ir[i], c = ic[i];
+      if (r >= t.rows) continue;
+      const float s = scale_all[wave][r];
+      const uint8_t *row = stage + off0 + r * a.d + 16 * c;
+      u32x4 v = *reinterpret_cast<const u32x4 *>(row);
+      u32x4 q4;
+      if (INTERP) {
+        const u32x4 up = *reinterpret_cast<const u32x4 *>(row - a.d);
+        const u32x4 dn = *reinterpret_cast<const u32x4 *>(row + a.d);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          q4[k] = interp_word(v[k] & 0x0F0F0F0Fu, up[k] & 0x0F0F0F0Fu, dn[k] & 0x0F0F0F0Fu,
+                              (v[k] >> 4) & 0x03030303u);
+      } else if (CODEC == KVECC_CODEC_NONE) {
+        q4 = v;  // raw bytes as stored (the composed read does not mask them)
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q4[k] = v[k] & 0x0F0F0F0Fu;
+      }
+      TO *dst = out + (int64_t)r * a.d + 16 * c;
+#pragma unroll
+      for (int k = 0; k < 4; k += 2) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = t.row0 >= 0 ? ((float)(q4[k] >> (8 * e) & 0xFFu) - 8.0f) * s : 0.0f;
+          o[4 + e] = t.row0 >= 0 ? ((float)(q4[k + 1] >> (8 * e) & 0xFFu) - 8.0f) * s : 0.0f;
+        }
+        store8<TO>(dst + 4 * k, o);
+      }
+    }
+    if (!more) break;
+    wave_lds_sync();
+  }
+  if (STATS) {
+    n1 = wave_sum(n1);
+    n2 = wave_sum(n2);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + ((blockIdx.x * kTileWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+      if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
     }
   }
 }
@@ -613,6 +777,27 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
   else
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
+}
+
+template <typename TO, int CODEC, bool INTERP>
+static void launch_bytes_tiles_s(const ShimTileArgs &a, unsigned grid, hipStream_t st) {
+  if (a.stats)
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
+  else
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
+}
+
+template <typename TO>
+static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * KVECC_SHIM_TILE_PER_CU);
+  if (codec == KVECC_CODEC_H84 && interp)
+    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, true>(a, grid, st);
+  else if (codec == KVECC_CODEC_H84)
+    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, false>(a, grid, st);
+  else if (codec == KVECC_CODEC_H74)
+    launch_bytes_tiles_s<TO, KVECC_CODEC_H74, false>(a, grid, st);
+  else
+    launch_bytes_tiles_s<TO, KVECC_CODEC_NONE, false>(a, grid, st);
 }
 
 }  // namespace kvecc
@@ -776,6 +961,40 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
       default: launch_read_tiles<__hip_bfloat16>(pk, a, st); break;
     }
     return check_launch("shim_read");
+  }
+  if (!golay && d % 16 == 0 && (!interp || d <= kWave * 16 / 2) && aligned(k_cache, 16) && aligned(v_cache, 16) && aligned(k_out, 16) && aligned(v_out, 16) &&
+      2 * batch * hkv * cdiv(ctx, block_size) * block_size <= 0x7FFFFFFFLL) {
+    // byte codecs: the wave-tile kernel, all sequences in one launch
+    ShimTileArgs a{};
+    a.cache[0] = k_cache;
+    a.cache[1] = v_cache;
+    a.scales[0] = k_scales;
+    a.scales[1] = v_scales;
+    a.out[0] = k_out;
+    a.out[1] = v_out;
+    a.table = block_table;
+    a.stats = stats;
+    a.tstride = (uint32_t)tstride;
+    a.hkv = (uint32_t)hkv;
+    a.d = a.g = a.lr = a.rowb = (uint32_t)d;
+    a.layers = (uint32_t)num_layers;
+    a.bs = (uint32_t)block_size;
+    a.layer = (uint32_t)layer;
+    a.ctx = (uint32_t)ctx;
+    const int64_t cpr = d / 16;
+    a.tr = (uint32_t)std::min<int64_t>({block_size, (int64_t)kTileStage / d - (interp ? 2 : 0), (int64_t)kWave,
+                                        (int64_t)kWave * kByteTileItems / cpr});
+    if (a.tr >= 1) {
+      a.tpb = (uint32_t)cdiv(block_size, a.tr);
+      a.nlb = (uint32_t)cdiv(ctx, block_size);
+      a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+      switch (out_dtype) {
+        case KVECC_F32: launch_bytes_tiles<float>(codec, interp, a, st); break;
+        case KVECC_F16: launch_bytes_tiles<__half>(codec, interp, a, st); break;
+        default: launch_bytes_tiles<__hip_bfloat16>(codec, interp, a, st); break;
+      }
+      return check_launch("shim_read");
+    }
   }
   const int64_t osz = out_dtype == KVECC_F32 ? 4 : 2;
   for (int64_t b = 0; b < batch; ++b) {  // one launch per sequence

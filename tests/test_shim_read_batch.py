@@ -123,6 +123,17 @@ def test_cpu_batch_read_vs_oracle(oracle, codec, batch, ctx, hkv, d, bs, dtype):
     assert cpu_ops.read_stats(st) == [sk[0] + sv[0], sk[1] + sv[1]]
 
 
+def test_cpu_missing_byte_block_reads_zero():
+    """Byte codecs: a -1 block reads as +0 rows; as an interpolation neighbour
+    its codewords read as 0 (decode(0) = 0)."""
+    from kvecc import cpu_ops
+    kc, vc, ks, vs, table = make_cache("hamming84", 1, 40, 2, 64, 16, seed=4)
+    table[0, 1] = -1
+    k, _ = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 40, 64, 1, "hamming84", torch.float32, interp=True)
+    assert torch.equal(k[0, :, 16:32], torch.zeros(2, 16, 64))
+    assert bool(torch.isfinite(k).all())
+
+
 def test_cpu_missing_golay_block_reads_zero(oracle):
     from kvecc import cpu_ops
     kc, vc, ks, vs, table = make_cache("golay", 2, 40, 2, 64, 16, seed=4)
@@ -135,7 +146,12 @@ def test_cpu_missing_golay_block_reads_zero(oracle):
 
 GPU_CASES = CPU_CASES + [("golay", 4, 257, 4, 128, 16), ("golay_packed", 3, 100, 8, 64, 32),
                          ("golay", 2, 50, 2, 256, 8), ("golay", 1, 3, 1, 8, 16),
-                         ("golay_packed", 2, 64, 2, 512, 2), ("golay", 2, 31, 2, 96, 5)]
+                         ("golay_packed", 2, 64, 2, 512, 2), ("golay", 2, 31, 2, 96, 5),
+                         # byte codecs: wave tiles for d % 16 == 0, per-sequence kernels otherwise
+                         ("hamming84", 4, 257, 4, 128, 16), ("hamming74", 2, 100, 3, 64, 32),
+                         ("int4", 2, 50, 2, 256, 8), ("hamming84", 1, 3, 1, 16, 16),
+                         ("hamming84", 2, 64, 2, 512, 2), ("hamming84", 2, 31, 2, 48, 5),
+                         ("hamming84", 2, 20, 2, 36, 4), ("hamming74", 1, 70, 2, 128, 128)]
 
 
 @pytest.mark.gpu
@@ -153,16 +169,47 @@ def test_hip_batch_read_vs_cpu(gpu, codec, batch, ctx, hkv, d, bs, dtype):
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
 
 
+INTERP_CASES = [(3, 70, 2, 64, 16), (2, 33, 2, 128, 16), (1, 1, 1, 16, 16), (2, 100, 3, 512, 4),
+                (2, 45, 2, 32, 7), (1, 17, 2, 128, 64), (2, 40, 2, 36, 8)]
+
+
 @pytest.mark.gpu
-def test_hip_batch_read_interp_vs_cpu(gpu):
+@pytest.mark.parametrize("batch,ctx,hkv,d,bs", INTERP_CASES)
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_hip_batch_read_interp_vs_cpu(gpu, batch, ctx, hkv, d, bs, dtype):
+    """H(8,4) with double-error interpolation: neighbours across block and tile
+    boundaries, context ends clamped, partial blocks, statistics."""
     from kvecc import cpu_ops, ops
-    kc, vc, ks, vs, table = make_cache("hamming84", 3, 70, 2, 64, 16, seed=9)
-    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 70, 64, 1, "hamming84", torch.float16,
-                                     interp=True)
+    kc, vc, ks, vs, table = make_cache("hamming84", batch, ctx, hkv, d, bs, seed=9 + ctx)
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 1, "hamming84", dtype,
+                                     interp=True, stats=st)
     t = lambda x: x.to(gpu)  # noqa: E731
-    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), 70, 64, 1, "hamming84",
-                               torch.float16, interp=True)
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 1, "hamming84",
+                               dtype, interp=True, stats=gst)
     assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,interp", [("hamming84", False), ("hamming84", True), ("hamming74", False),
+                                          ("int4", False)])
+def test_hip_missing_byte_block_reads_zero(gpu, codec, interp):
+    """A -1 block (never produced by the shim) reads as +0 rows, and as zero
+    codewords where it is an interpolation neighbour -- the same on both backends."""
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache(codec, 2, 40, 2, 64, 16, seed=4)
+    table[1, 1] = -1
+    table[0, 0] = -1
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 40, 64, 1, codec, torch.float16, stats=st,
+                                     interp=interp)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), 40, 64, 1, codec, torch.float16,
+                               stats=gst, interp=interp)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert torch.equal(k[1, :, 16:32].cpu(), torch.zeros(2, 16, 64, dtype=torch.float16))
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
 
 
 @pytest.mark.gpu
@@ -183,19 +230,22 @@ def test_hip_missing_golay_block_reads_zero(gpu, codec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("codec", ["golay", "golay_packed"])
+@pytest.mark.parametrize("codec", ["golay", "golay_packed", "hamming84", "hamming84+interp"])
 def test_hip_batch_read_full_size(gpu, codec):
     """[B=8, L=4096, Hkv=32, D=128] (the bench's fused-decode workload), fp16,
     bit-exact against the host twin, statistics included."""
     from kvecc import cpu_ops, ops
     batch, ctx, hkv, d, bs = 8, 4096, 32, 128, 16
+    interp = codec.endswith("+interp")
+    codec = codec.split("+")[0]
     kc, vc, ks, vs, table = make_cache(codec, batch, ctx, hkv, d, bs, layers=1, seed=1, spare=0)
     st = cpu_ops.new_stats()
-    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 0, codec, torch.float16, stats=st)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 0, codec, torch.float16, stats=st,
+                                     interp=interp)
     gst = ops.new_stats(gpu)
     t = lambda x: x.to(gpu)  # noqa: E731
     k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 0, codec, torch.float16,
-                               stats=gst)
+                               stats=gst, interp=interp)
     assert torch.equal(k.cpu(), ek)
     assert torch.equal(v.cpu(), ev)
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
