@@ -569,12 +569,19 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
   const uint32_t nwaves = gridDim.x * kTileWaves;
   const uint32_t cpr = a.d / 16;       // 16-byte chunks per row
   const uint32_t items = a.tr * cpr;   // <= 64 * kByteTileItems (host check)
-  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];          // phase 1: row, 16-value chunk
+  uint32_t i2r[2 * kByteTileItems], i2c[2 * kByteTileItems];  // phase 2: row, 8-value chunk
 #pragma unroll
   for (int i = 0; i < kByteTileItems; ++i) {
     const uint32_t f = lane + kWave * i;
     ir[i] = f / cpr;
     ic[i] = f - ir[i] * cpr;
+  }
+#pragma unroll
+  for (int i = 0; i < 2 * kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    i2r[i] = f / (2 * cpr);
+    i2c[i] = f - i2r[i] * (2 * cpr);
   }
   uint32_t n1 = 0, n2 = 0;
   uint32_t u = blockIdx.x * kTileWaves + wave;
@@ -657,41 +664,43 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     u += nwaves;
     const bool more = u < a.units;
     if (more) fetch(u);
-    // ---- phase 2: interpolate, dequantize, 16 values per lane -------------------
+    // ---- phase 2: interpolate, dequantize; 8 values per lane, so each
+    // wave-instruction stores 1 KiB of contiguous fp16 output --------------------
     TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
 #pragma unroll
-    for (int i = 0; i < kByteTileItems; ++i) {
-      if (i * kWave >= (int)items) break;  // uniform
-      const uint32_t r = ir[i], c = ic[i];
+    for (int i = 0; i < 2 * kByteTileItems; ++i) {
+      if (i * kWave >= (int)(2 * items)) break;  // uniform
+      const uint32_t r = i2r[i], c = i2c[i];
       if (r >= t.rows) continue;
       const float s = scale_all[wave][r];
-      const uint8_t *row = stage + off0 + r * a.d + 16 * c;
-      u32x4 v = *reinterpret_cast<const u32x4 *>(row);
-      u32x4 q4;
+      const uint8_t *row = stage + off0 + r * a.d + 8 * c;
+      const u32x2 v = *reinterpret_cast<const u32x2 *>(row);
+      u32x2 q2;
       if (INTERP) {
-        const u32x4 up = *reinterpret_cast<const u32x4 *>(row - a.d);
-        const u32x4 dn = *reinterpret_cast<const u32x4 *>(row + a.d);
+        const u32x2 up = *reinterpret_cast<const u32x2 *>(row - a.d);
+        const u32x2 dn = *reinterpret_cast<const u32x2 *>(row + a.d);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          q4[k] = interp_word(v[k] & 0x0F0F0F0Fu, up[k] & 0x0F0F0F0Fu, dn[k] & 0x0F0F0F0Fu,
+        for (int k = 0; k < 2; ++k)
+          q2[k] = interp_word(v[k] & 0x0F0F0F0Fu, up[k] & 0x0F0F0F0Fu, dn[k] & 0x0F0F0F0Fu,
                               (v[k] >> 4) & 0x03030303u);
       } else if (CODEC == KVECC_CODEC_NONE) {
-        q4 = v;  // raw bytes as stored (the composed read does not mask them)
+        q2 = v;  // raw bytes as stored (the composed read does not mask them)
       } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q4[k] = v[k] & 0x0F0F0F0Fu;
+        for (int k = 0; k < 2; ++k) q2[k] = v[k] & 0x0F0F0F0Fu;
       }
-      TO *dst = out + (int64_t)r * a.d + 16 * c;
-#pragma unroll
-      for (int k = 0; k < 4; k += 2) {
-        float o[8];
+      float o[8];
+      if (t.row0 >= 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          o[e] = t.row0 >= 0 ? ((float)(q4[k] >> (8 * e) & 0xFFu) - 8.0f) * s : 0.0f;
-          o[4 + e] = t.row0 >= 0 ? ((float)(q4[k + 1] >> (8 * e) & 0xFFu) - 8.0f) * s : 0.0f;
+          o[e] = ((float)(q2[0] >> (8 * e) & 0xFFu) - 8.0f) * s;
+          o[4 + e] = ((float)(q2[1] >> (8 * e) & 0xFFu) - 8.0f) * s;
         }
-        store8<TO>(dst + 4 * k, o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0.0f;
       }
+      store8<TO>(out + (int64_t)r * a.d + 8 * c, o);
     }
     if (!more) break;
     wave_lds_sync();
