@@ -181,6 +181,56 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
             "timing": f"HIP events carried by the dispatch, mean of {steps} launches"}
 
 
+def fused_h84_bench(dev, steps, warmup):
+    """The shim's fused read for its default codec, Hamming(8,4) (ecc_shim.py:990-1071):
+    gather -> SECDED decode (-> double-error interpolation along the context) ->
+    dequantize -> fp16 over [B=8, L=4096, Hkv=32, D=128] K+V, block 16, BER 1e-3.
+    Bytes per token row and side: 128 codeword bytes + 4 B scale in, 256 B out
+    (interpolation's neighbour rows come from the wave's LDS tile, except the
+    two halo rows per 16-row tile)."""
+    from kvecc import ops
+    bs = 16
+    nlb = L // bs
+    nb = B * nlb
+    gen = torch.Generator().manual_seed(11)
+    caches, scales = [], []
+    for side in range(2):
+        x = torch.randint(0, 16, (nb * H * bs * D,), generator=gen, dtype=torch.uint8).to(dev)
+        cw = ops.hamming84_encode(x)
+        ops.inject_into(cw, cw, 1e-3, 8, seed=SEED + side)
+        caches.append(cw.view(nb, 1, H, bs * D))
+        scales.append((torch.rand(nb, 1, H, bs, generator=gen) * 0.1 + 0.01).to(dev))
+        del x
+    table = torch.randperm(nb, generator=gen).to(torch.int32).view(B, nlb).to(dev)
+    outs = (torch.empty(B, H, L, D, dtype=torch.float16, device=dev),
+            torch.empty(B, H, L, D, dtype=torch.float16, device=dev))
+    st = ops.new_stats(dev)
+    res = {}
+    for interp in (False, True):
+        def call():
+            ops.shim_read_batch(caches[0], caches[1], scales[0], scales[1], table, L, D, 0, "hamming84",
+                                torch.float16, stats=st, interp=interp, out=outs)
+        for _ in range(warmup):
+            call()
+        evs = [ops.kernel_timer(dev) for _ in range(steps)]
+        torch.cuda.synchronize()
+        for k in range(steps):
+            ops.time_next_launch(*evs[k])
+            call()
+        torch.cuda.synchronize()
+        ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
+        nbytes = 2 * B * L * H * (D + 4 + 2 * D)
+        res["interp" if interp else "plain"] = {
+            "kernel_ms": ms, "values_per_s": 2 * B * L * H * D / (ms * 1e-3),
+            "bytes_per_launch": nbytes, "hbm_gbs": nbytes / (ms * 1e-3) / 1e9,
+            "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    res.update({"workload": "shim_read_batch hamming84 -> fp16, [B=8,L=4096,Hkv=32,D=128] K+V, block_size 16, "
+                            "BER 1e-3; plain and with double-error interpolation",
+                "kernel": "shim_read_bytes_tiles_kernel", "bytes_per_token_row": D + 4 + 2 * D,
+                "timing": f"HIP events carried by the dispatch, mean of {steps} launches"})
+    return res
+
+
 def rows_bench(dev, x, noisy_rows, steps, warmup):
     """Per-head Golay rows (the shim's and the config-5 sweep's layout,
     ecc_shim.py:623-682): golay_encode_rows of the [8,4096,32,128] nibbles and
@@ -470,6 +520,7 @@ def main():
     if not args.no_fused:
         fused = fused_decode_bench(dev, max(args.steps, 10), args.warmup)
         fused["packed"] = fused_decode_bench(dev, max(args.steps, 10), args.warmup, packed=True)
+        fused["hamming84"] = fused_h84_bench(dev, max(args.steps, 10), args.warmup)
 
     if rank != 0:
         if dist is not None:

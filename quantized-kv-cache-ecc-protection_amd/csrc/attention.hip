@@ -277,8 +277,18 @@ __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
   if (E % 2) acc[E - 1] = fmaf(p, v[E - 1], acc[E - 1]);
 }
 
+// minimum waves per SIMD the register allocation must allow (0: no bound)
+#ifndef KVECC_ATTN_MIN_WAVES
+#define KVECC_ATTN_MIN_WAVES 0
+#endif
+#if KVECC_ATTN_MIN_WAVES
+#define KVECC_ATTN_BOUNDS __launch_bounds__(kBlock, KVECC_ATTN_MIN_WAVES)
+#else
+#define KVECC_ATTN_BOUNDS __launch_bounds__(kBlock)
+#endif
+
 template <typename T, int CODEC, int VEC, int W, bool BUF>
-__global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
+__global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)

@@ -105,6 +105,18 @@ __device__ __forceinline__ int32_t ld_scalar(const int32_t *p) {
   return *(const __attribute__((address_space(4))) int32_t *)uni(reinterpret_cast<const char *>(p));
 }
 
+// dequantization (n - 8) * s, rounded to fp32 as its own operation.  Left to
+// itself the compiler may contract the product with a following fp16/bf16
+// conversion into v_fma_mix*_f16, which rounds the exact product once, while
+// the reference (and the host twin) round to fp32 first: 1 ulp apart.
+// (Neither __fmul_rn nor `#pragma clang fp contract(off)` stops that combine;
+// an empty asm on the fp32 product does.)
+__device__ __forceinline__ float dequant1(uint32_t n, float s) {
+  float x = ((float)n - 8.0f) * s;
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // element conversions of the fused kernels (fp32 / fp16 / bf16, RNE on the way out)
 template <typename T>
 __device__ __forceinline__ float to_f32(T v);

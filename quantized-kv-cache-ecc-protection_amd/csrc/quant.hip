@@ -184,7 +184,7 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_kernel(const uint8_t *_
       if (zero_doubles && t == 2) q = 0;
       n1 += t == 1;
       n2 += t == 2;
-      o.v[k] = from_f32<TO>(((float)q - 8.0f) * s);
+      o.v[k] = from_f32<TO>(dequant1(q, s));
     }
     *reinterpret_cast<Vec<TO, VEC> *>(out + i * VEC) = o;
   }
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_wide_kernel(const uint3
         q &= ~(dbl * 0xFFu);
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[4 * k + e] = from_f32<TO>(((float)(q >> (8 * e) & 0xFFu) - 8.0f) * s);
+      for (int e = 0; e < 4; ++e) o[4 * k + e] = from_f32<TO>(dequant1(q >> (8 * e) & 0xFFu, s));
     }
     u32x4 b;
     __builtin_memcpy(&b, o, 16);

@@ -148,7 +148,7 @@ struct ShimReadArgs {
 template <typename TO>
 __device__ __forceinline__ void dequant4(TO *o, uint32_t q, float s) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) o[k] = from_f32<TO>(((float)(q >> (8 * k) & 0xFFu) - 8.0f) * s);
+  for (int k = 0; k < 4; ++k) o[k] = from_f32<TO>(dequant1(q >> (8 * k) & 0xFFu, s));
 }
 
 __device__ __forceinline__ uint32_t ld_word(const uint8_t *base, int64_t slot, uint32_t d, uint32_t c) {
@@ -222,9 +222,9 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
     bits += cnt & 3u;
     unc += cnt >> 2;
     const float s = a.scales[side][slot];
-    o[0] = from_f32<TO>(((float)(dw & 0xFu) - 8.0f) * s);
-    if (left > 1) o[1] = from_f32<TO>(((float)(dw >> 4 & 0xFu) - 8.0f) * s);
-    if (left > 2) o[2] = from_f32<TO>(((float)(dw >> 8) - 8.0f) * s);
+    o[0] = from_f32<TO>(dequant1(dw & 0xFu, s));
+    if (left > 1) o[1] = from_f32<TO>(dequant1(dw >> 4 & 0xFu, s));
+    if (left > 2) o[2] = from_f32<TO>(dequant1(dw >> 8, s));
   }
   if (STATS) flush_stats2(a.stats, bits, unc);
 }
@@ -313,7 +313,7 @@ __device__ __forceinline__ ShimTile shim_tile(const ShimTileArgs &a, uint32_t u)
 // per-lane items, identical for every tile
 struct TileItems {
   uint32_t r1[kTileGroups], q1[kTileGroups];  // phase 1: row, 4-codeword group
-  uint32_t r2[kTileChunks], j2[kTileChunks];  // phase 2: row, 8-value chunk
+  uint32_t r2[2 * kTileChunks], j2[2 * kTileChunks];  // phase 2: row, VPL-value chunk
 };
 
 // the tile's codewords and its rows' scales, into registers.  Buffer
@@ -393,6 +393,30 @@ __device__ __forceinline__ void store8(TO *dst, const float (&v)[8]) {
   }
 }
 
+// values per lane per output item: one 16-byte store (fp16/bf16: 8, fp32: 4),
+// so each wave-instruction writes 1 KiB contiguous (32-byte lane strides, two
+// stores per lane, halved the store rate)
+template <typename TO>
+constexpr int kVpl = 16 / (int)sizeof(TO);
+
+// VPL dequantized values (nibble bytes n: (n - 8) * s, or +0) as one 16-byte store
+template <typename TO>
+__device__ __forceinline__ void dequant_store(TO *dst, const uint32_t *nb, float s, bool zero) {
+  constexpr int V = kVpl<TO>;
+  float o[8];
+#pragma unroll
+  for (int e = 0; e < V; ++e) o[e] = zero ? 0.0f : dequant1(nb[e / 4] >> (8 * (e % 4)) & 0xFFu, s);
+  if constexpr (V == 4) {
+    const u32x4 v{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
+    if (KVECC_SHIM_TILE_NT)
+      st_stream(reinterpret_cast<u32x4 *>(dst), v);
+    else
+      *reinterpret_cast<u32x4 *>(dst) = v;
+  } else {
+    store8<TO>(dst, o);
+  }
+}
+
 template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
@@ -413,8 +437,9 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   const uint32_t lane = threadIdx.x % kWave;
   const uint32_t nwaves = gridDim.x * kTileWaves;
   const uint32_t groups = a.tr * a.gpr;  // <= 64 * kTileGroups (host check)
-  const uint32_t d8 = a.d / 8;
-  const uint32_t chunks = a.tr * d8;     // <= 64 * kTileChunks (host check)
+  constexpr int V = kVpl<TO>, NC = kTileChunks * 8 / V;  // output chunks per lane (max)
+  const uint32_t dv = a.d / V;
+  const uint32_t chunks = a.tr * dv;     // <= 64 * NC (host check: tr * d / 8 <= 64 * kTileChunks)
   TileItems it;
 #pragma unroll
   for (int i = 0; i < kTileGroups; ++i) {
@@ -423,10 +448,10 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     it.q1[i] = f - it.r1[i] * a.gpr;
   }
 #pragma unroll
-  for (int i = 0; i < kTileChunks; ++i) {
+  for (int i = 0; i < NC; ++i) {
     const uint32_t v = lane + kWave * i;
-    it.r2[i] = v / d8;
-    it.j2[i] = v - it.r2[i] * d8;
+    it.r2[i] = v / dv;
+    it.j2[i] = v - it.r2[i] * dv;
   }
   uint32_t bits = 0, unc = 0;
 
@@ -503,31 +528,17 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
       if (!tv[k]) continue;
       const uint8_t *stage = stage_all[wave][k];
       TO *out = reinterpret_cast<TO *>(a.out[t[k].side]) + ((int64_t)t[k].bh * a.ctx + t[k].pos0) * a.d;
-      if (t[k].row0 >= 0) {
+      const bool dead = t[k].row0 < 0;  // no physical block: +0 (the product would give -0)
 #pragma unroll
-        for (int i = 0; i < kTileChunks; ++i) {
-          if (i * kWave >= (int)chunks) break;  // uniform
-          const uint32_t r = it.r2[i], j = it.j2[i];
-          if (r < t[k].rows) {
-            const float s = scale_all[wave][k][r];
-            float o[8];
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + 8 * j);
-            const uint32_t lo = src[0], hi = src[1];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              o[e] = ((float)(lo >> (8 * e) & 0xFFu) - 8.0f) * s;
-              o[4 + e] = ((float)(hi >> (8 * e) & 0xFFu) - 8.0f) * s;
-            }
-            store8<TO>(out + (int64_t)r * a.d + 8 * j, o);
-          }
-        }
-      } else {  // no physical block: +0 (the product above would give -0)
-#pragma unroll
-        for (int i = 0; i < kTileChunks; ++i) {
-          if (i * kWave >= (int)chunks) break;  // uniform
-          const uint32_t r = it.r2[i], j = it.j2[i];
-          const float o[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-          if (r < t[k].rows) store8<TO>(out + (int64_t)r * a.d + 8 * j, o);
+      for (int i = 0; i < NC; ++i) {
+        if (i * kWave >= (int)chunks) break;  // uniform
+        const uint32_t r = it.r2[i], j = it.j2[i];
+        if (r < t[k].rows) {
+          uint32_t nb[2];
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + V * j);
+          nb[0] = src[0];
+          nb[1] = V == 8 ? src[1] : 0u;
+          dequant_store<TO>(out + (int64_t)r * a.d + V * j, nb, scale_all[wave][k][r], dead);
         }
       }
     }
@@ -570,7 +581,8 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
   const uint32_t cpr = a.d / 16;       // 16-byte chunks per row
   const uint32_t items = a.tr * cpr;   // <= 64 * kByteTileItems (host check)
   uint32_t ir[kByteTileItems], ic[kByteTileItems];          // phase 1: row, 16-value chunk
-  uint32_t i2r[2 * kByteTileItems], i2c[2 * kByteTileItems];  // phase 2: row, 8-value chunk
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;  // phase 2: VPL-value chunks
+  uint32_t i2r[NI2], i2c[NI2];                              // phase 2: row, chunk
 #pragma unroll
   for (int i = 0; i < kByteTileItems; ++i) {
     const uint32_t f = lane + kWave * i;
@@ -578,10 +590,10 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     ic[i] = f - ir[i] * cpr;
   }
 #pragma unroll
-  for (int i = 0; i < 2 * kByteTileItems; ++i) {
+  for (int i = 0; i < NI2; ++i) {
     const uint32_t f = lane + kWave * i;
-    i2r[i] = f / (2 * cpr);
-    i2c[i] = f - i2r[i] * (2 * cpr);
+    i2r[i] = f / (cpr * 16 / V);
+    i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
   uint32_t n1 = 0, n2 = 0;
   uint32_t u = blockIdx.x * kTileWaves + wave;
@@ -664,43 +676,28 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     u += nwaves;
     const bool more = u < a.units;
     if (more) fetch(u);
-    // ---- phase 2: interpolate, dequantize; 8 values per lane, so each
-    // wave-instruction stores 1 KiB of contiguous fp16 output --------------------
+    // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
+    // wave-instruction stores 1 KiB contiguous ------------------------------------
     TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
 #pragma unroll
-    for (int i = 0; i < 2 * kByteTileItems; ++i) {
-      if (i * kWave >= (int)(2 * items)) break;  // uniform
+    for (int i = 0; i < NI2; ++i) {
+      if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
       const uint32_t r = i2r[i], c = i2c[i];
       if (r >= t.rows) continue;
-      const float s = scale_all[wave][r];
-      const uint8_t *row = stage + off0 + r * a.d + 8 * c;
-      const u32x2 v = *reinterpret_cast<const u32x2 *>(row);
-      u32x2 q2;
-      if (INTERP) {
-        const u32x2 up = *reinterpret_cast<const u32x2 *>(row - a.d);
-        const u32x2 dn = *reinterpret_cast<const u32x2 *>(row + a.d);
+      const uint8_t *row = stage + off0 + r * a.d + V * c;
+      uint32_t q[2] = {0u, 0u};
 #pragma unroll
-        for (int k = 0; k < 2; ++k)
-          q2[k] = interp_word(v[k] & 0x0F0F0F0Fu, up[k] & 0x0F0F0F0Fu, dn[k] & 0x0F0F0F0Fu,
-                              (v[k] >> 4) & 0x03030303u);
-      } else if (CODEC == KVECC_CODEC_NONE) {
-        q2 = v;  // raw bytes as stored (the composed read does not mask them)
-      } else {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) q2[k] = v[k] & 0x0F0F0F0Fu;
-      }
-      float o[8];
-      if (t.row0 >= 0) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = ((float)(q2[0] >> (8 * e) & 0xFFu) - 8.0f) * s;
-          o[4 + e] = ((float)(q2[1] >> (8 * e) & 0xFFu) - 8.0f) * s;
+      for (int k = 0; k < V / 4; ++k) {
+        const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+        if (INTERP) {
+          const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+          const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+          q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+        } else {
+          q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
         }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = 0.0f;
       }
-      store8<TO>(out + (int64_t)r * a.d + 8 * c, o);
+      dequant_store<TO>(out + (int64_t)r * a.d + V * c, q, scale_all[wave][r], t.row0 < 0);
     }
     if (!more) break;
     wave_lds_sync();

@@ -16,7 +16,8 @@ gen = torch.Generator().manual_seed(7)
 x = torch.randint(0, 16, (2, nb, 1, H, BS * D), generator=gen, dtype=torch.uint8).to(dev)
 sc = (torch.rand(2, nb, 1, H, BS, generator=gen) * 0.1 + 0.01).to(dev)
 table = torch.randperm(nb, generator=gen).to(torch.int32).view(B, nlb).to(dev)
-outs = (torch.empty(B, H, L, D, dtype=torch.float16, device=dev), torch.empty(B, H, L, D, dtype=torch.float16, device=dev))
+ODT = torch.float32 if os.environ.get("OUT") == "fp32" else torch.float16
+outs = (torch.empty(B, H, L, D, dtype=ODT, device=dev), torch.empty(B, H, L, D, dtype=ODT, device=dev))
 st = ops.new_stats(dev)
 for codec, interp in (("hamming84", False), ("hamming84", True), ("hamming74", False), ("int4", False)):
     enc = {"hamming84": ops.hamming84_encode, "hamming74": ops.hamming74_encode, "int4": lambda t: t.clone()}[codec]
@@ -25,7 +26,7 @@ for codec, interp in (("hamming84", False), ("hamming84", True), ("hamming74", F
         for s in range(2):
             cf = c[s].view(-1)
             ops.inject_into(cf, cf, 1e-3, 8 if codec == "hamming84" else 7, seed=42 + s)
-    call = lambda: ops.shim_read_batch(c[0], c[1], sc[0], sc[1], table, L, D, 0, codec, torch.float16,
+    call = lambda: ops.shim_read_batch(c[0], c[1], sc[0], sc[1], table, L, D, 0, codec, ODT,
                                        stats=st, interp=interp, out=outs)
     for _ in range(20): call()
     ts = []
@@ -34,5 +35,5 @@ for codec, interp in (("hamming84", False), ("hamming84", True), ("hamming74", F
         a.record(); call(); b.record(); torch.cuda.synchronize()
         ts.append(a.elapsed_time(b) * 1e3)
     med = statistics.median(ts)
-    nbytes = 2 * B * L * H * (D + 4 + 2 * D)
-    print(f"{codec:9s} interp={interp!s:5s}: {med:7.1f} us ({nbytes / med / 1e3:.0f} GB/s, {nbytes / med / 8e4:.1f}% of 8 TB/s)", flush=True)
+    nbytes = 2 * B * L * H * (D + 4 + outs[0].element_size() * D)
+    print(f"{str(ODT)[6:]:8s} {codec:9s} interp={interp!s:5s}: {med:7.1f} us ({nbytes / med / 1e3:.0f} GB/s, {nbytes / med / 8e4:.1f}% of 8 TB/s)", flush=True)

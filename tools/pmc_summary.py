@@ -27,10 +27,14 @@ ALGO = {"golay_decode_kernel": 8 * M, "golay_encode_kernel": 7 * M,
         "golay_encode_rows_reg_kernel": 300 * (M // 43), "golay_decode_rows_reg_kernel": 300 * (M // 43),
         # fused shim read, K+V token rows: int32 (172 + 4 + 256 B) then packed (129 + 4 + 256 B)
         "shim_read_golay_tiles_kernel[int32]": 432 * 2 * (M // 43),
-        "shim_read_golay_tiles_kernel[packed]": 389 * 2 * (M // 43)}
+        "shim_read_golay_tiles_kernel[packed]": 389 * 2 * (M // 43),
+        # fused shim read, Hamming(8,4) K+V token rows: 128 + 4 + 256 B
+        "shim_read_bytes_tiles_kernel[h84]": 388 * 2 * (M // 43),
+        "shim_read_bytes_tiles_kernel[h84+interp]": 388 * 2 * (M // 43)}
 # kernels the bench launches in two configurations under one (truncated) name:
 # the first half of the launches is the first configuration
-SPLIT = {"shim_read_golay_tiles_kernel": ("[int32]", "[packed]")}
+SPLIT = {"shim_read_golay_tiles_kernel": ("[int32]", "[packed]"),
+         "shim_read_bytes_tiles_kernel": ("[h84]", "[h84+interp]")}
 
 
 def counters(path):
