@@ -74,6 +74,9 @@ def parse():
                     help="skip the fused Golay read (shim_read_batch) measurement")
     ap.add_argument("--no-rows", action="store_true",
                     help="skip the per-head rows (golay_encode_rows / decode_rows) measurement")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend for N > 1 (nccl = RCCL; gloo only to rehearse several "
+                         "ranks on one GPU)")
     ap.add_argument("--dist", action="store_true",
                     help="create the RCCL process group even at world size 1 (exercises the "
                          "barrier and the stats/timing all-reduces on one GPU)")
@@ -347,8 +350,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one GPU per rank; --backend gloo lets several ranks share one device to
+    # rehearse the multi-rank path on a 1-GPU box (RCCL refuses that)
+    ngpu = torch.cuda.device_count()
+    local_dev = local % ngpu if args.backend == "gloo" and ngpu else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     dist = None
     if world > 1 or args.dist:
         import torch.distributed as dist
@@ -357,7 +364,10 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29511")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     import kvecc
     from kvecc import ops
@@ -445,6 +455,8 @@ def main():
     tt = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
     st = ops.stats_totals(stats)
     if dist is not None:
+        if args.backend == "gloo":  # gloo reduces host tensors
+            tt, st = tt.cpu(), st.cpu()
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(st, op=dist.ReduceOp.SUM)     # the single stats all-reduce
     elapsed, enc_ms, dec_ms = tt.tolist()

@@ -253,6 +253,21 @@ __global__ __launch_bounds__(256) void write_only(u32x4 *__restrict__ d, int64_t
   }
 }
 
+// write-only through buffer stores with a cache-policy immediate (gfx950: sc0 = 1, nt = 2, sc1 = 16)
+template <int AUX>
+__global__ __launch_bounds__(256) void write_only_pol(u32x4 *__restrict__ d, int64_t n) {
+  u32x4 v;
+  v.x = v.y = v.z = v.w = threadIdx.x;
+  for (int64_t b = (int64_t)blockIdx.x * 1024; b < n; b += (int64_t)gridDim.x * 1024) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char *>(d + b), 0, (int)(min<int64_t>(1024, n - b) * 16), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                             rs, (uint32_t)(u * 256 + threadIdx.x) * 16u, 0, AUX);
+  }
+}
+
 extern "C" __attribute__((visibility("default"))) int exp_ceiling(const void *s, void *d, int64_t bytes, int variant,
                                                                   int grid, void *stream) {
   int64_t n = bytes / 16;
@@ -269,6 +284,12 @@ extern "C" __attribute__((visibility("default"))) int exp_ceiling(const void *s,
     case 6: hipLaunchKernelGGL((read_only<false>), dim3(grid), dim3(256), 0, st, S, n, reinterpret_cast<uint32_t *>(d)); break;
     case 7: hipLaunchKernelGGL((write_only<true>), dim3(grid), dim3(256), 0, st, D, n); break;
     case 8: hipLaunchKernelGGL((write_only<false>), dim3(grid), dim3(256), 0, st, D, n); break;
+    case 9: hipLaunchKernelGGL((write_only_pol<0>), dim3(grid), dim3(256), 0, st, D, n); break;
+    case 10: hipLaunchKernelGGL((write_only_pol<2>), dim3(grid), dim3(256), 0, st, D, n); break;
+    case 11: hipLaunchKernelGGL((write_only_pol<16>), dim3(grid), dim3(256), 0, st, D, n); break;
+    case 12: hipLaunchKernelGGL((write_only_pol<17>), dim3(grid), dim3(256), 0, st, D, n); break;
+    case 13: hipLaunchKernelGGL((write_only_pol<18>), dim3(grid), dim3(256), 0, st, D, n); break;
+    case 14: hipLaunchKernelGGL((write_only_pol<1>), dim3(grid), dim3(256), 0, st, D, n); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
