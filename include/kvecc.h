@@ -175,6 +175,12 @@ KVECC_API int kvecc_interpolate_auto(const uint8_t *q, const uint8_t *err, uint8
 /* *flag = (any x[i] == value) ? 1 : 0 (device int32, overwritten). */
 KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int32_t *flag,
                                  void *stream);
+/* stats[0] += number of positions i < n with a[i] != b[i] (device buffers;
+ * sharded statistics buffer as the codecs use).  The codec-level sweep's
+ * residual-error count, `(decoded != truth).sum()` in the reference's Monte
+ * Carlo (evaluation/experiments/monte_carlo.py:75-395), as one HBM pass. */
+KVECC_API int kvecc_count_ne_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint64_t *stats,
+                                void *stream);
 
 /* ---- Fused quantize / encode and decode / dequantize ----------------------- */
 /* fused_kernels.py:18-160 (H84), :163-269 (H74), and the shim's torch path
@@ -353,6 +359,8 @@ KVECC_API int kvecc_cpu_inject_rows_u8(const uint8_t *in, uint8_t *out, int64_t 
 KVECC_API int kvecc_cpu_inject_rows_i32(const int32_t *in, int32_t *out, int64_t rows,
                                         int64_t row_len, int n_bits, int64_t seed_base, float ber,
                                         uint64_t *stats, int threads);
+KVECC_API int kvecc_cpu_count_ne_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint64_t *stats,
+                                    int threads);
 KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
                                     int64_t outer, int64_t len, int64_t inner, int threads);
 KVECC_API int kvecc_cpu_quantize_encode_rows(const void *x, int x_dtype, int codec,

@@ -512,6 +512,21 @@ KVECC_API int kvecc_cpu_inject_rows_i32(const int32_t *in, int32_t *out, int64_t
                                   "cpu_inject_rows_i32");
 }
 
+KVECC_API int kvecc_cpu_count_ne_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint64_t *stats,
+                                    int threads) {
+  if (n < 0) return set_error(KVECC_EINVAL, "cpu_count_ne_u8: negative n");
+  if (n == 0) return KVECC_OK;
+  if (!a || !b || !stats) return set_error(KVECC_EINVAL, "cpu_count_ne_u8: null pointer");
+  std::vector<Acc2> acc(std::max(1, clamp_threads(threads, n, 1 << 16)));
+  parallel_for(n, threads, 1 << 16, [&](int64_t lo, int64_t hi, int t) {
+    uint64_t c = 0;
+    for (int64_t i = lo; i < hi; ++i) c += a[i] != b[i];
+    acc[t].a += c;
+  });
+  add_stats(stats, acc, 1);
+  return KVECC_OK;
+}
+
 KVECC_API int kvecc_cpu_interpolate(const uint8_t *q, const uint8_t *err, uint8_t *out,
                                     int64_t outer, int64_t len, int64_t inner, int threads) {
   if (outer < 0 || len < 0 || inner < 0) return set_error(KVECC_EINVAL, "cpu_interpolate: negative size");

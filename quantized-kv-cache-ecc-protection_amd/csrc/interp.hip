@@ -287,6 +287,47 @@ __global__ __launch_bounds__(kBlock) void any_equal_kernel(const uint8_t *__rest
   if (__syncthreads_or(hit) && threadIdx.x == 0) *flag = 1;
 }
 
+// bytes of a that differ from b: four 16-byte non-temporal loads of each in
+// flight per lane; per word, the nonzero bytes of a ^ b are folded to bit 0 of
+// each byte and counted with one popcount
+__device__ __forceinline__ uint32_t ne_bytes(uint32_t x) {
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return __builtin_popcount(x & 0x01010101u);
+}
+
+__global__ __launch_bounds__(kBlock) void count_ne_kernel(const uint8_t *__restrict__ a,
+                                                          const uint8_t *__restrict__ b, int64_t n,
+                                                          uint64_t *__restrict__ stats) {
+  constexpr int kU = 4;
+  uint32_t cnt = 0;
+  const bool vec = (reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) % 16 == 0;
+  const int64_t nvec = vec ? n / 16 : 0;
+  const u32x4 *av = reinterpret_cast<const u32x4 *>(a), *bv = reinterpret_cast<const u32x4 *>(b);
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (; i + (kU - 1) * stride < nvec; i += kU * stride) {
+    u32x4 x[kU], y[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      x[u] = ld_stream(av + i + u * stride);
+      y[u] = ld_stream(bv + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      cnt += ne_bytes(x[u].x ^ y[u].x) + ne_bytes(x[u].y ^ y[u].y) + ne_bytes(x[u].z ^ y[u].z) +
+             ne_bytes(x[u].w ^ y[u].w);
+  }
+  for (; i < nvec; i += stride) {
+    const u32x4 x = ld_stream(av + i), y = ld_stream(bv + i);
+    cnt += ne_bytes(x.x ^ y.x) + ne_bytes(x.y ^ y.y) + ne_bytes(x.z ^ y.z) + ne_bytes(x.w ^ y.w);
+  }
+  for (int64_t j = nvec * 16 + (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += stride)
+    cnt += a[j] != b[j];
+  flush_stats2(stats, cnt, 0u);
+}
+
 template <bool RECORD>
 static void launch_interp(const uint8_t *q, const uint8_t *err, uint8_t *out, int64_t outer,
                           int64_t len, int64_t inner, const int32_t *gate, int32_t *flags,
@@ -343,6 +384,16 @@ KVECC_API int kvecc_interpolate_auto(const uint8_t *q, const uint8_t *err, uint8
   KVECC_LAUNCH(interp_fixup_kernel, dim3(64), dim3(kBlock), 0, st, q, out, total, flags, epoch,
                aligned(q, 16) && aligned(out, 16));
   return check_launch("interpolate_auto");
+}
+
+KVECC_API int kvecc_count_ne_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint64_t *stats,
+                                void *stream) {
+  if (n < 0) return set_error(KVECC_EINVAL, "count_ne_u8: negative n");
+  if (n == 0) return KVECC_OK;
+  if (!a || !b || !stats) return set_error(KVECC_EINVAL, "count_ne_u8: null pointer");
+  KVECC_LAUNCH(count_ne_kernel, dim3(grid_for(n, (int64_t)kBlock * 64, 8)), dim3(kBlock), 0,
+               as_stream(stream), a, b, n, stats);
+  return check_launch("count_ne_u8");
 }
 
 KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int32_t *flag,

@@ -46,6 +46,7 @@ SIGNATURES = {
     "kvecc_inject_rows_i32": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _vp],
     "kvecc_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "kvecc_any_equal_u8": [_vp, _i64, _u8, _vp, _vp],
+    "kvecc_count_ne_u8": [_vp, _vp, _i64, _vp, _vp],
     "kvecc_interpolate_auto": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp],
     "kvecc_quantize_encode_rows": [_vp, _int, _int, _int, _vp, _vp, _i64, _i64, _vp],
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
@@ -80,6 +81,7 @@ SIGNATURES = {
     "kvecc_cpu_inject_rows_i32": [_vp, _vp, _i64, _i64, _int, _i64, _f32, _vp, _int],
     "kvecc_cpu_inject_u8": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
     "kvecc_cpu_inject_i32": [_vp, _vp, _vp, _i64, _int, _i64, _f32, _i64, _i64, _vp, _int],
+    "kvecc_cpu_count_ne_u8": [_vp, _vp, _i64, _vp, _int],
     "kvecc_cpu_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _int],
     "kvecc_cpu_quantize_encode_rows": [_vp, _int, _int, _int, _vp, _vp, _i64, _i64, _int],
     "kvecc_cpu_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _int],

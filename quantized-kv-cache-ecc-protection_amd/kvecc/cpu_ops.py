@@ -340,6 +340,15 @@ def _seq_layout(shape, seq_dim):
     return layout(shape, seq_dim)
 
 
+def count_ne_into(a, b, stats):
+    """Host twin of ops.count_ne_into: stats[0] += count of positions where a != b."""
+    if a.dtype != torch.uint8 or b.dtype != torch.uint8 or a.numel() != b.numel():
+        raise ValueError("count_ne_into: two uint8 tensors of one size")
+    a, b = a.contiguous(), b.contiguous()
+    _lib.call("kvecc_cpu_count_ne_u8", _ptr(a), _ptr(b), a.numel(), _ptr(stats), NUM_THREADS)
+    return stats
+
+
 def any_equal(x, value, flag=None):
     """int32 flag [1] = any(x == value) (host twin of ops.any_equal)."""
     if flag is None:

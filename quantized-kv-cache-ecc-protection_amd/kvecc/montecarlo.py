@@ -92,8 +92,32 @@ def shard_bounds(batch, rank, world):
     return b0, b0 + base + (1 if rank < extra else 0)
 
 
+class _TrialBuffers:
+    """One trial's device buffers (HipShard keeps two, for the stream pipeline)."""
+
+    def __init__(self, ops, shape, g, dev):
+        sb, l, h, d = shape
+        self.cw8 = torch.empty(shape, dtype=torch.uint8, device=dev)
+        self.cw32 = torch.empty((sb, l, h, g), dtype=torch.int32, device=dev)
+        self.dec = torch.empty(shape, dtype=torch.uint8, device=dev)
+        self.et = torch.empty(shape, dtype=torch.uint8, device=dev)
+        self.itp = torch.empty(shape, dtype=torch.uint8, device=dev)
+        self.st_inj = ops.new_stats(dev)
+        self.st_dec = ops.new_stats(dev)
+        self.st_cmp = ops.new_stats(dev)  # residual mismatches (kvecc_count_ne_u8)
+        self.ready = torch.cuda.Event()   # encode + inject done
+        self.free = torch.cuda.Event()    # decode + count done: the buffers may be rewritten
+        self.free.record()
+
+
 class HipShard:
-    """One rank's shard of the sweep on an MI355X (kvecc HIP kernels)."""
+    """One rank's shard of the sweep on an MI355X (kvecc HIP kernels).
+
+    Trials are pipelined over two HIP streams: trial k's encode + injection
+    (VALU-bound Philox, ~1.65 ms at [8,4096,32,128]) runs on one stream while
+    trial k-1's decode, interpolation and residual count (HBM-bound) run on the
+    other, in two alternating buffer sets ordered by events.  The counters are
+    the same as a serial run's; finish() drains the pipeline."""
 
     def __init__(self, cfg: MonteCarloConfig, rank: int, world: int, device):
         from . import ops
@@ -115,50 +139,83 @@ class HipShard:
         if self.sb:
             ops.inject_into(self.x.view(-1), self.x.view(-1), 0.5, 4, cfg.data_seed,
                             global_n=self.n_total, offset0=self.off)
-        self.cw8 = torch.empty_like(self.x)
-        self.dec = torch.empty_like(self.x)
-        self.et = torch.empty_like(self.x)
-        self.itp = torch.empty_like(self.x)
-        self.cw32 = torch.empty((self.sb, l, h, self.g), dtype=torch.int32, device=self.dev)
-        self.st_inj = ops.new_stats(self.dev)
-        self.st_dec = ops.new_stats(self.dev)
+        with torch.cuda.device(self.dev):
+            self.bufs = [_TrialBuffers(ops, shape, self.g, self.dev) for _ in range(2)]
+            self.s_inj = torch.cuda.Stream(self.dev)
+            self.s_dec = torch.cuda.Stream(self.dev)
+        self.k = 0
+        self.pending = None
 
     def run_trial(self, codec, ber, seed, row):
-        """Accumulate this shard's 5 counters of one trial into `row` (device int64[5])."""
+        """Queue one trial; its 5 counters land in `row` (device int64[5]) once
+        the pipeline has run it (finish() or the next trial)."""
         ops = self.ops
         if self.sb == 0:
             return row
-        self.st_inj.zero_()
-        self.st_dec.zero_()
+        caller = torch.cuda.current_stream(self.dev)
+        buf = self.bufs[self.k % 2]
+        self.k += 1
         x = self.x.view(-1)
-        if codec == "golay":
-            cw = ops.golay_encode_rows(self.x)
-            flat = cw.view(-1)
-            ops.inject_into(flat, flat, ber, 24, seed, stats=self.st_inj, global_n=self.m_total,
-                            offset0=self.m_off)
-            out = ops.golay_decode_rows(cw, self.cfg.shape[3], stats=self.st_dec)
-        else:
-            enc = ops.hamming74_encode_into if codec == "hamming74" else ops.hamming84_encode_into
-            enc(x, self.cw8.view(-1))
-            c = self.cw8.view(-1)
-            ops.inject_into(c, c, ber, N_BITS[codec], seed, stats=self.st_inj,
-                            global_n=self.n_total, offset0=self.off)
-            if codec == "hamming74":
-                ops.hamming74_decode_into(c, self.dec.view(-1), None, self.st_dec)
-                out = self.dec
+        with torch.cuda.stream(self.s_inj):
+            self.s_inj.wait_stream(caller)
+            self.s_inj.wait_event(buf.free)
+            buf.st_inj.zero_()
+            if codec == "golay":
+                ops.golay_encode_rows_into(self.x, buf.cw32)
+                flat = buf.cw32.view(-1)
+                ops.inject_into(flat, flat, ber, 24, seed, stats=buf.st_inj, global_n=self.m_total,
+                                offset0=self.m_off)
             else:
-                ops.hamming84_decode_into(c, self.dec.view(-1), self.et.view(-1), self.st_dec)
-                out = self.dec
+                enc = ops.hamming74_encode_into if codec == "hamming74" else ops.hamming84_encode_into
+                c = buf.cw8.view(-1)
+                enc(x, c)
+                ops.inject_into(c, c, ber, N_BITS[codec], seed, stats=buf.st_inj,
+                                global_n=self.n_total, offset0=self.off)
+            buf.ready.record(self.s_inj)
+        self._drain()
+        self.pending = (codec, buf, row, caller)
+        return row
+
+    def _drain(self):
+        """Decode, interpolate and count the pending trial on the decode stream."""
+        if self.pending is None:
+            return
+        ops = self.ops
+        codec, buf, row, caller = self.pending
+        self.pending = None
+        x = self.x.view(-1)
+        with torch.cuda.stream(self.s_dec):
+            self.s_dec.wait_stream(caller)  # the caller's row buffer exists
+            self.s_dec.wait_event(buf.ready)
+            buf.st_dec.zero_()
+            buf.st_cmp.zero_()
+            if codec == "golay":
+                ops.golay_decode_rows_into(buf.cw32, buf.dec, buf.st_dec)
+                out = buf.dec
+            elif codec == "hamming74":
+                ops.hamming74_decode_into(buf.cw8.view(-1), buf.dec.view(-1), None, buf.st_dec)
+                out = buf.dec
+            else:
+                ops.hamming84_decode_into(buf.cw8.view(-1), buf.dec.view(-1), buf.et.view(-1), buf.st_dec)
+                out = buf.dec
                 if codec == "hamming84_interp":
                     _, l, h, d = self.cfg.shape
                     # temporal neighbours along L, each (b, h, d) column a sequence
-                    ops.interpolate_into(self.dec.view(-1), self.et.view(-1), self.itp.view(-1),
+                    ops.interpolate_into(buf.dec.view(-1), buf.et.view(-1), buf.itp.view(-1),
                                          self.sb, l, h * d)
-                    out = self.itp
-        row[0:2] += ops.stats_totals(self.st_inj, 2)
-        row[2:4] += ops.stats_totals(self.st_dec, 2)
-        row[4] += (out != self.x).sum()
-        return row
+                    out = buf.itp
+            ops.count_ne_into(out.view(-1), x, buf.st_cmp)  # one pass, no bool tensor
+            row[0:2] += ops.stats_totals(buf.st_inj, 2)
+            row[2:4] += ops.stats_totals(buf.st_dec, 2)
+            row[4:5] += ops.stats_totals(buf.st_cmp, 1)
+            buf.free.record(self.s_dec)
+
+    def finish(self):
+        """Drain the pipeline; the caller's stream then waits for every queued trial."""
+        self._drain()
+        caller = torch.cuda.current_stream(self.dev)
+        caller.wait_stream(self.s_inj)
+        caller.wait_stream(self.s_dec)
 
 
 def _load_done(path):
@@ -190,6 +247,8 @@ def run_sweep(cfg: MonteCarloConfig, shard, dist=None, rank=0):
     t0 = time.perf_counter()
     for i, (codec, ber, seed) in enumerate(todo):
         shard.run_trial(codec, ber, seed, table[i])
+    if hasattr(shard, "finish"):  # pipelined shards
+        shard.finish()
     if shard.dev.type == "cuda":
         torch.cuda.synchronize(shard.dev)
     elapsed = time.perf_counter() - t0

@@ -412,6 +412,15 @@ def interpolate_into(q, err, out, outer, length, inner, gate=None):
     return out
 
 
+def count_ne_into(a, b, stats):
+    """stats[0] += count of positions where uint8 a != b (same shapes, one device); no sync."""
+    if a.dtype != torch.uint8 or b.dtype != torch.uint8 or a.numel() != b.numel() or a.device != b.device:
+        raise ValueError("count_ne_into: two uint8 tensors of one size on one device")
+    a, b = a.contiguous(), b.contiguous()
+    _lib.call("kvecc_count_ne_u8", _ptr(a), _ptr(b), a.numel(), _ptr(stats), _stream(a.device))
+    return stats
+
+
 def any_equal(x, value, flag=None):
     """Device int32 flag = any(x == value), no host sync."""
     if flag is None:

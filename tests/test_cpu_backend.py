@@ -309,3 +309,20 @@ def test_golay_rows_into(cpu):
         cpu.golay_encode_rows_into(x, torch.empty(4, 6, 42, dtype=torch.int32))
     with pytest.raises(ValueError):
         cpu.golay_decode_rows_into(noisy, torch.empty(4, 6, 130, dtype=torch.uint8))
+
+
+def test_count_ne_into(cpu):
+    """kvecc_cpu_count_ne_u8: mismatching byte count added to stats[0]."""
+    g = torch.Generator().manual_seed(12)
+    for n in (0, 1, 15, 16, 17, 100003):
+        a = torch.randint(0, 16, (n,), dtype=torch.uint8, generator=g)
+        b = a.clone()
+        if n:
+            idx = torch.randint(0, n, (max(1, n // 7),), generator=g)
+            b[idx] ^= 0x5
+        st = cpu.new_stats()
+        cpu.count_ne_into(a, b, st)
+        cpu.count_ne_into(a, a, st)
+        assert cpu.read_stats(st, 1)[0] == int((a != b).sum())
+    with pytest.raises(ValueError):
+        cpu.count_ne_into(a, b[:-1], cpu.new_stats())

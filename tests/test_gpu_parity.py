@@ -567,3 +567,19 @@ def test_interp_auto_in_a_hip_graph(gpu):
             assert int(out.max()) == 15
         else:
             assert torch.equal(out, q)
+
+
+@pytest.mark.parametrize("n,offset", [(1, 0), (15, 0), (16, 0), (1 << 20, 0), ((1 << 20) + 37, 3),
+                                      (134217728 + 5, 0)])
+def test_count_ne_vs_torch(gpu, n, offset):
+    """kvecc_count_ne_u8 (the sweep's residual count) equals (a != b).sum():
+    vector and tail paths, unaligned buffers, a [8,4096,32,128]-sized input."""
+    from kvecc import ops
+    g = torch.Generator(device=gpu).manual_seed(n)
+    a = torch.randint(0, 256, (n + offset,), dtype=torch.uint8, device=gpu, generator=g)[offset:]
+    b = a.clone()
+    flips = torch.randint(0, n, (max(1, n // 100),), device=gpu, generator=g)
+    b[flips] ^= 0x40
+    st = ops.new_stats(gpu)
+    ops.count_ne_into(a, b, st)
+    assert ops.read_stats(st, 1)[0] == int((a != b).sum())

@@ -159,8 +159,28 @@ def test_hip_shard_matches_oracle_shard(gpu):
             a = torch.zeros(5, dtype=torch.int64, device=gpu)
             b = torch.zeros(5, dtype=torch.int64)
             hip.run_trial(codec, ber, seed, a)
+            hip.finish()  # the HIP shard pipelines trials over two streams
             ora.run_trial(codec, ber, seed, b)
             assert a.cpu().tolist() == b.tolist(), (codec, ber, world, rank)
+
+
+@pytest.mark.gpu
+def test_hip_shard_pipeline_equals_oracle(gpu):
+    """Trials queued back to back (encode + injection of trial k on one stream,
+    decode + count of trial k-1 on the other, two alternating buffer sets)
+    give every trial the oracle's counters."""
+    cfg = mc.MonteCarloConfig(shape=(2, 96, 4, 128), bers=(1e-3, 0.03), seeds=(42, 7))
+    hip = mc.HipShard(cfg, 0, 1, gpu)
+    ora = OracleShard(cfg, 0, 1)
+    trials = cfg.trials()
+    rows = torch.zeros(len(trials), 5, dtype=torch.int64, device=gpu)
+    for i, t in enumerate(trials):
+        hip.run_trial(*t, rows[i])
+    hip.finish()
+    for i, t in enumerate(trials):
+        b = torch.zeros(5, dtype=torch.int64)
+        ora.run_trial(*t, b)
+        assert rows[i].cpu().tolist() == b.tolist(), t
 
 
 def test_seed_aliases_config5():
