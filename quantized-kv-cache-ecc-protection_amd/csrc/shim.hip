@@ -20,6 +20,7 @@
 // with P = D (uint8) or ceil(D/3) (int32 Golay); scales fp32 [blocks, layers,
 // Hkv, bs]; logical block b of the sequence is physical block table[b].
 #include <algorithm>
+#include <type_traits>
 
 #include "kvecc_internal.h"
 
@@ -568,7 +569,30 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 // (decoded, not interpolated, neighbours), dequantizes and writes 16-byte
 // non-temporal stores.  A row in a missing block (table entry -1) reads as
 // zero codewords and outputs +0, as in the Golay kernel and the host twin.
-constexpr int kByteTileItems = 4;  // 16-value chunks per lane per phase (max)
+constexpr int kByteTileItems = 4;
+// memory/VALU-ceiling experiments for the interpolating read (wrong values;
+// A/B: tools/exp/run_shim_read_interp.py): no neighbour-row loads / no
+// interpolation arithmetic
+#ifndef KVECC_SHIM_INTERP_NOHALO
+#define KVECC_SHIM_INTERP_NOHALO 0
+#endif
+#ifndef KVECC_SHIM_INTERP_NOVALU
+#define KVECC_SHIM_INTERP_NOVALU 0
+#endif
+// Interpolation only changes a double error's value.  A tile whose decode saw
+// no double (a wave ballot in phase 1) dequantizes without the interpolation
+// arithmetic and the neighbour-row reads (SKIP; at BER 1e-3 ~95 % of tiles).
+// [8,4096,32,128] K+V fp16, per launch: 204 -> 177 us at BER 0, 199 -> 176 us
+// at 1e-3, 201 -> 206 us at 1e-2 (profiles/r02/interp_read/).  LAZY loads the
+// neighbour rows only when a double sits in the tile's first or last row
+// (synchronously, and from then on the wave prefetches them): 161 us at BER 0,
+// but 188 us at 1e-3 and 221 us at 1e-2, so it stays off.
+#ifndef KVECC_SHIM_INTERP_LAZY
+#define KVECC_SHIM_INTERP_LAZY 0
+#endif
+#ifndef KVECC_SHIM_INTERP_SKIP
+#define KVECC_SHIM_INTERP_SKIP 1
+#endif
 
 template <typename TO, int CODEC, bool INTERP, bool STATS>
 __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
@@ -602,6 +626,30 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
   ShimTile cur;
   u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
   float scale;
+  bool eager = !KVECC_SHIM_INTERP_LAZY;  // prefetch neighbour rows (sticky once a tile needed them)
+  bool has_hw = false;                   // hw holds the current tile's neighbour rows
+  // neighbour rows of tile c: lanes [0, cpr) row pos0 - 1 (pos0 itself at the
+  // context's start), [cpr, 2 cpr) row pos0 + rows (the last row at its end)
+  auto load_halo = [&](const ShimTile &c) -> u32x4 {
+    // both positions and their blocks are wave-uniform: scalar loads, so the
+    // halo does not wait behind the previous tile's stores
+    const uint32_t side = uni(c.side);
+    const bool below = lane >= cpr;
+    const uint32_t bh = uni(c.bh), b = bh / a.hkv, h = bh - b * a.hkv;
+    const uint32_t pa = uni(c.pos0 > 0 ? c.pos0 - 1 : 0u), pb = uni(min(c.pos0 + c.rows, a.ctx - 1));
+    const int32_t ba = ld_scalar(a.table + (int64_t)b * a.tstride + pa / a.bs);
+    const int32_t bb = ld_scalar(a.table + (int64_t)b * a.tstride + pb / a.bs);
+    const uint32_t pos = below ? pb : pa;
+    const uint32_t lb = pos / a.bs;
+    const int32_t blk = below ? bb : ba;
+    u32x4 r{0u, 0u, 0u, 0u};
+    if (lane < 2 * cpr && blk >= 0) {
+      const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - lb * a.bs);
+      r = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[side]) + row * a.d) +
+                    (below ? lane - cpr : lane));
+    }
+    return r;
+  };
   auto fetch = [&](uint32_t uu) {
     cur = shim_tile(a, uu);
     const bool live = cur.row0 >= 0;
@@ -619,27 +667,12 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
       if (i * kWave >= (int)items) break;  // uniform
       w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
     }
-    if (INTERP && cur.rows > 0) {  // neighbour rows: lanes [0, cpr) above, [cpr, 2 cpr) below
-      // both positions and their blocks are wave-uniform: scalar loads, so the
-      // halo does not wait behind the previous tile's stores
-      const bool below = lane >= cpr;
-      const uint32_t bh = uni(cur.bh), b = bh / a.hkv, h = bh - b * a.hkv;
-      const uint32_t pa = uni(cur.pos0 > 0 ? cur.pos0 - 1 : 0u), pb = uni(min(cur.pos0 + cur.rows, a.ctx - 1));
-      const int32_t ba = ld_scalar(a.table + (int64_t)b * a.tstride + pa / a.bs);
-      const int32_t bb = ld_scalar(a.table + (int64_t)b * a.tstride + pb / a.bs);
-      const uint32_t pos = below ? pb : pa;
-      const uint32_t lb = pos / a.bs;
-      const int32_t blk = below ? bb : ba;
-      hw = u32x4{0u, 0u, 0u, 0u};
-      if (lane < 2 * cpr && blk >= 0) {
-        const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - lb * a.bs);
-        hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[side]) + row * a.d) +
-                       (below ? lane - cpr : lane));
-      }
-    }
+    has_hw = INTERP && !KVECC_SHIM_INTERP_NOHALO && eager && cur.rows > 0;
+    if (has_hw) hw = load_halo(cur);
   };
-  // 4 codewords -> data | type << 4 per byte (and the statistics)
-  auto dec = [&](uint32_t cw, bool count) -> uint32_t {
+  // 4 codewords -> data | type << 4 per byte (and the statistics); `dbl`
+  // collects the words' double errors
+  auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
     uint32_t q = cw, t = 0, s1 = 0, s2 = 0;
     if (CODEC == KVECC_CODEC_H84) {
       h84_decode4(cw, q, t, s1, s2);
@@ -647,9 +680,12 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
       h74_decode4(cw, q, t, s1);
       t = 0;
     }
-    if (STATS && count) {
-      n1 += s1;
-      n2 += s2;
+    if (count) {
+      if (STATS) {
+        n1 += s1;
+        n2 += s2;
+      }
+      dbl |= s2;
     }
     return q | t << 4;
   };
@@ -658,16 +694,31 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     // ---- phase 1: decode into the LDS tile (row r at (r + INTERP) * d) --------
     const uint32_t off0 = INTERP ? a.d : 0u;
     scale_all[wave][lane] = scale;
+    bool dbl_any = false, dbl_edge = false;  // this lane saw a double / one in the first or last row
 #pragma unroll
     for (int i = 0; i < kByteTileItems; ++i) {
       if (i * kWave >= (int)items) break;  // uniform
       const bool real = ir[i] < cur.rows;  // rows past the tile loaded 0: no statistics
-      const u32x4 d4{dec(w[i].x, real), dec(w[i].y, real), dec(w[i].z, real), dec(w[i].w, real)};
+      uint32_t dbl = 0;
+      const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
+                     dec(w[i].w, real, dbl)};
+      dbl_any |= dbl != 0;
+      dbl_edge |= dbl != 0 && (ir[i] == 0 || ir[i] + 1 == cur.rows);
       // (with interpolation, rows past the tile's end would overwrite the row below)
       if (ir[i] < (INTERP ? cur.rows : a.tr)) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
     }
-    if (INTERP && lane < 2 * cpr) {  // neighbours: row 0 above, row rows + 1 below
-      const u32x4 d4{dec(hw.x, false), dec(hw.y, false), dec(hw.z, false), dec(hw.w, false)};
+    // wave-uniform: interpolate this tile at all / does it need its neighbour rows
+    const bool tile_dbl = INTERP && (!KVECC_SHIM_INTERP_SKIP || __builtin_amdgcn_ballot_w64(dbl_any) != 0);
+    if (INTERP && KVECC_SHIM_INTERP_LAZY && !KVECC_SHIM_INTERP_NOHALO && !has_hw &&
+        __builtin_amdgcn_ballot_w64(dbl_edge) != 0) {
+      hw = load_halo(cur);  // waits here; later tiles prefetch theirs
+      has_hw = true;
+      eager = true;
+    }
+    if (INTERP && has_hw && lane < 2 * cpr) {  // neighbours: row 0 above, row rows + 1 below
+      uint32_t none = 0;
+      const u32x4 d4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none),
+                     dec(hw.w, false, none)};
       const uint32_t r = lane >= cpr ? cur.rows + 1 : 0u;
       *reinterpret_cast<u32x4 *>(stage + r * a.d + 16 * (lane >= cpr ? lane - cpr : lane)) = d4;
     }
@@ -679,26 +730,34 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
     // wave-instruction stores 1 KiB contiguous ------------------------------------
     TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
+    // one straight-line body per case (a branch per item serialised its LDS reads)
+    auto phase2 = [&](auto interp_c) {
+      constexpr bool IP = decltype(interp_c)::value;
 #pragma unroll
-    for (int i = 0; i < NI2; ++i) {
-      if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
-      const uint32_t r = i2r[i], c = i2c[i];
-      if (r >= t.rows) continue;
-      const uint8_t *row = stage + off0 + r * a.d + V * c;
-      uint32_t q[2] = {0u, 0u};
+      for (int i = 0; i < NI2; ++i) {
+        if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
+        const uint32_t r = i2r[i], c = i2c[i];
+        if (r >= t.rows) continue;
+        const uint8_t *row = stage + off0 + r * a.d + V * c;
+        uint32_t q[2] = {0u, 0u};
 #pragma unroll
-      for (int k = 0; k < V / 4; ++k) {
-        const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
-        if (INTERP) {
-          const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
-          const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
-          q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
-        } else {
-          q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
+        for (int k = 0; k < V / 4; ++k) {
+          const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+          if (IP) {
+            const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+            const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+            q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+          } else {
+            q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
+          }
         }
+        dequant_store<TO>(out + (int64_t)r * a.d + V * c, q, scale_all[wave][r], t.row0 < 0);
       }
-      dequant_store<TO>(out + (int64_t)r * a.d + V * c, q, scale_all[wave][r], t.row0 < 0);
-    }
+    };
+    if (INTERP && !KVECC_SHIM_INTERP_NOVALU && tile_dbl)
+      phase2(std::integral_constant<bool, true>{});
+    else
+      phase2(std::integral_constant<bool, false>{});
     if (!more) break;
     wave_lds_sync();
   }

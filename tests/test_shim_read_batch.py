@@ -26,7 +26,7 @@ def _pack_golay(cache, g):
     return torch.from_numpy(out.reshape(*cache.shape[:-1], -1))
 
 
-def make_cache(codec, batch, ctx, hkv, d, bs, layers=2, seed=0, spare=3):
+def make_cache(codec, batch, ctx, hkv, d, bs, layers=2, seed=0, spare=3, ber=BER):
     """Random paged caches (cpu backend, oracle-pinned codecs) with BER-level errors.
     Returns caches, scales, block table [batch, max_blocks] (a random
     permutation of physical blocks) and the codeword count per row."""
@@ -42,13 +42,13 @@ def make_cache(codec, batch, ctx, hkv, d, bs, layers=2, seed=0, spare=3):
         x = vals[side]
         if golay:
             cw = cpu_ops.golay_encode_rows(x).reshape(nb, layers, hkv, bs * per)
-            cw = cpu_ops.inject_bit_errors_triton(cw, BER, 24, seed=seed + side)
+            cw = cpu_ops.inject_bit_errors_triton(cw, ber, 24, seed=seed + side)
             caches.append(_pack_golay(cw, per) if codec == "golay_packed" else cw)
         else:
             enc = {"hamming84": cpu_ops.hamming84_encode, "hamming74": cpu_ops.hamming74_encode,
                    "int4": lambda t: t}[codec](x).reshape(nb, layers, hkv, bs * d)
             if codec != "int4":
-                enc = cpu_ops.inject_bit_errors_triton(enc, BER, 8 if codec == "hamming84" else 7,
+                enc = cpu_ops.inject_bit_errors_triton(enc, ber, 8 if codec == "hamming84" else 7,
                                                        seed=seed + side)
             caches.append(enc)
     ks = torch.rand(nb, layers, hkv, bs, generator=g) * 0.5 + 0.01
@@ -187,6 +187,33 @@ def test_hip_batch_read_interp_vs_cpu(gpu, batch, ctx, hkv, d, bs, dtype):
     t = lambda x: x.to(gpu)  # noqa: E731
     k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 1, "hamming84",
                                dtype, interp=True, stats=gst)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
+# more tiles than waves in the grid (> 4096 on 256 CUs), several tiles per wave:
+# several tiles per block (bs 64 > 16 rows per tile), partial last blocks,
+# missing blocks (first, inner, last).  At low BER most tiles hold no double
+# error (no interpolation arithmetic, no neighbour rows) and a few need their
+# neighbour rows after the decode; at 2e-2 every wave soon prefetches them.
+MANY_TILE_CASES = [(4, 2001, 4, 32, 6, 2e-2), (3, 5000, 8, 128, 64, 2e-2), (2, 4099, 16, 64, 16, 1e-3),
+                   (3, 5000, 8, 128, 64, 1e-3), (4, 2001, 4, 32, 6, 3e-4), (2, 4099, 16, 128, 16, 0.0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,ctx,hkv,d,bs,ber", MANY_TILE_CASES)
+def test_hip_batch_read_interp_many_tiles(gpu, batch, ctx, hkv, d, bs, ber):
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache("hamming84", batch, ctx, hkv, d, bs, layers=1, seed=ctx, ber=ber)
+    table[0, 3] = -1
+    table[batch - 1, (ctx - 1) // bs] = -1  # the last block of a sequence
+    table[1, 0] = -1  # the first
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 0, "hamming84", torch.float16,
+                                     interp=True, stats=st)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 0, "hamming84", torch.float16,
+                               interp=True, stats=gst)
     assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
 
