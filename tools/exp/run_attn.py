@@ -9,7 +9,7 @@ import torch
 from kvecc import _lib, ops
 VP, I64 = ctypes.c_void_p, ctypes.c_int64
 libs = {"prod": _lib.load()}
-for name in ("v2", "v8", "v16", "buf", "nopk", "bufnopk", "u16", "g4", "u2", "u8", "gu1", "gu3", "gu4", "lutf", "expf", "r01", "w8", "w8u2", "w8v2", "h1", "h3", "h2f", "h2w8", "m5w5", "m6w6", "m8w8"):
+for name in ("prev", "v2", "v8", "v16", "buf", "nopk", "bufnopk", "u16", "g4", "u2", "u8", "gu1", "gu3", "gu4", "lutf", "expf", "r01", "w8", "w8u2", "w8v2", "h1", "h3", "h2f", "h2w8", "m5w5", "m6w6", "m8w8"):
     path = os.path.join(HERE, f"libattn_{name}.so")
     if os.path.exists(path):
         libs[name] = ctypes.CDLL(path)
@@ -20,7 +20,8 @@ for l in libs.values():
     l.kvecc_paged_attention_workspace.argtypes = [I64, I64, I64, I64]
     l.kvecc_paged_attention_workspace.restype = I64
 dev = torch.device("cuda:0")
-B, H, D, CTX, BS = 8, 32, 128, 4096, 16
+B, H, CTX, BS = 8, 32, 4096, 16
+D = int(os.environ.get("D", "128"))
 g = torch.Generator(device=dev).manual_seed(0)
 nb = CTX // BS
 blocks = B * nb
