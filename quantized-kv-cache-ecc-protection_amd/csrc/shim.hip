@@ -569,7 +569,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 // (decoded, not interpolated, neighbours), dequantizes and writes 16-byte
 // non-temporal stores.  A row in a missing block (table entry -1) reads as
 // zero codewords and outputs +0, as in the Golay kernel and the host twin.
-constexpr int kByteTileItems = 4;
+constexpr int kByteTileItems = 4;  // 16-value chunks per lane per phase (max)
 // memory/VALU-ceiling experiments for the interpolating read (wrong values;
 // A/B: tools/exp/run_shim_read_interp.py): no neighbour-row loads / no
 // interpolation arithmetic
