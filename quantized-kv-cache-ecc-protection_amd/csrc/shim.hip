@@ -448,11 +448,19 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     it.r1[i] = f / a.gpr;
     it.q1[i] = f - it.r1[i] * a.gpr;
   }
+  // fp32 output (NC = 10): the compiler keeps the phase-2 loop rolled, and
+  // per-lane item arrays indexed by its counter went to scratch (116 B, a
+  // vmcnt(0) wait per item); there the row is computed per item instead, by a
+  // reciprocal multiply exact for v < 2^32 / dv (v < 64 NC, dv = d / 4 >= 2)
+  constexpr bool kItemsInRegs = NC <= 8;
+  const uint32_t inv_dv = kItemsInRegs ? 0u : (uint32_t)(((1ull << 32) + dv - 1) / dv);
+  if (kItemsInRegs) {
 #pragma unroll
-  for (int i = 0; i < NC; ++i) {
-    const uint32_t v = lane + kWave * i;
-    it.r2[i] = v / dv;
-    it.j2[i] = v - it.r2[i] * dv;
+    for (int i = 0; i < NC; ++i) {
+      const uint32_t v = lane + kWave * i;
+      it.r2[i] = v / dv;
+      it.j2[i] = v - it.r2[i] * dv;
+    }
   }
   uint32_t bits = 0, unc = 0;
 
@@ -533,7 +541,15 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         if (i * kWave >= (int)chunks) break;  // uniform
-        const uint32_t r = it.r2[i], j = it.j2[i];
+        uint32_t r, j;
+        if (kItemsInRegs) {
+          r = it.r2[i];
+          j = it.j2[i];
+        } else {
+          const uint32_t v = lane + kWave * i;
+          r = __umulhi(v, inv_dv);
+          j = v - r * dv;
+        }
         if (r < t[k].rows) {
           uint32_t nb[2];
           const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + V * j);

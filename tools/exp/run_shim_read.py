@@ -19,6 +19,7 @@ from kvecc import _lib, ops  # noqa: E402
 
 B, L, H, D, BS, BER = 8, 4096, 32, 128, 16, 1e-2
 ROUNDS = int(os.environ.get("ROUNDS", "30"))
+ODT = torch.float32 if os.environ.get("OUT") == "fp32" else torch.float16
 
 
 def build_cache(dev, packed):
@@ -68,8 +69,8 @@ def main():
         per = ((3 * g + 3) // 4 * 4) if packed else g
         bs = caches[0].shape[-1] // per
         codec = 4 if packed else 3
-        outs = [(torch.empty(B, H, L, D, dtype=torch.float16, device=dev),
-                 torch.empty(B, H, L, D, dtype=torch.float16, device=dev)) for _ in handles]
+        outs = [(torch.empty(B, H, L, D, dtype=ODT, device=dev),
+                 torch.empty(B, H, L, D, dtype=ODT, device=dev)) for _ in handles]
         stats = [ops.new_stats(dev) for _ in handles]
         times = [[] for _ in handles]
         stream = torch.cuda.current_stream(dev).cuda_stream
@@ -78,7 +79,7 @@ def main():
             name, fn, tn = handles[i]
             rc = fn(caches[0].data_ptr(), caches[1].data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(),
                     table.data_ptr(), table.shape[1], B, L, H, D, 1, bs, 0, codec, 0,
-                    outs[i][0].data_ptr(), outs[i][1].data_ptr(), 1, stats[i].data_ptr(), stream)
+                    outs[i][0].data_ptr(), outs[i][1].data_ptr(), ops._DT[ODT], stats[i].data_ptr(), stream)
             assert rc == 0, (name, rc)
 
         for i in range(len(handles)):
@@ -102,7 +103,7 @@ def main():
                 e1.record()
                 times[i].append((e0, e1))
         torch.cuda.synchronize()
-        nbytes = 2 * B * L * H * ((3 * g if packed else 4 * g) + 4 + 2 * D)
+        nbytes = 2 * B * L * H * ((3 * g if packed else 4 * g) + 4 + ODT.itemsize * D)
         for i, (name, _, _) in enumerate(handles):
             us = [a.elapsed_time(b) * 1e3 for a, b in times[i]]
             med = statistics.median(us)
