@@ -34,7 +34,8 @@ def kernels(tmp_path_factory):
     fat = str(d / "fatbin.bin")
     subprocess.run([TOOLS[0], f"--dump-section=.hip_fatbin={fat}", LIB, str(d / "lib.stripped")], check=True)
     # one offload bundle per translation unit, concatenated in the section
-    blob = open(fat, "rb").read()
+    with open(fat, "rb") as f:
+        blob = f.read()
     magic = b"__CLANG_OFFLOAD_BUNDLE__"
     starts = [m.start() for m in re.finditer(re.escape(magic), blob)]
     notes = ""
