@@ -277,9 +277,10 @@ KVECC_API int kvecc_shim_read(const void *k_cache, const void *v_cache, const fl
  * table_stride >= ceil(ctx / block_size)); k_out / v_out are [batch, hkv, ctx,
  * d].  Golay caches with d % 8 == 0 take the wave-tile kernel (one launch for
  * every sequence and both sides; the fused decode BASELINE's north_star
- * measures); the other codecs launch once per sequence.  Golay: a negative
- * block id reads as zeros (no statistics); the byte codecs need valid blocks for
- * the first ctx tokens.  batch 1 is kvecc_shim_read. */
+ * measures); the other codecs launch once per sequence.  Every codec reads a
+ * negative block id as zero codewords: its rows output +0 (no statistics), and
+ * as an H84 interpolation neighbour its values read as decode(0) = 0.  batch 1
+ * is kvecc_shim_read. */
 KVECC_API int kvecc_shim_read_batch(const void *k_cache, const void *v_cache, const float *k_scales,
                                     const float *v_scales, const int32_t *block_table,
                                     int64_t table_stride, int64_t batch, int64_t ctx, int64_t hkv,

@@ -568,7 +568,7 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
         sp[k] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
         if (STATS && 4 * q + k < a.g) {  // past the tile: loads gave 0, count 0
           bits += e >> 24 & 3u;
-          unc += e >> 26;
+          unc += e >> 30;
         }
       }
       if (it.r1[i] < a.tr) {

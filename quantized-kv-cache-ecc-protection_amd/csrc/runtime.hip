@@ -132,8 +132,10 @@ static int ensure_tables(int d) {
   for (uint32_t i = 0; i < 4096; ++i) {
     host.attn[i] = spread12(i) | (uint32_t)host.par[i] << 20;
     // correction half: data bits of the error pattern spread one nibble per
-    // byte, the error count (0-3, 4 = uncorrectable) in byte 3
-    host.attn[4096 + i] = spread12(host.cor[i] & 0xFFFu) | (uint32_t)(host.cor[i] >> 12) << 24;
+    // byte; byte 3 = (bits corrected & 3) | uncorrectable << 6 (count 4 -> 0x40),
+    // so a sum of byte 3 over up to 21 codewords keeps both fields apart
+    const uint32_t n = host.cor[i] >> 12;  // 0-3 bits corrected, 4 = uncorrectable
+    host.attn[4096 + i] = spread12(host.cor[i] & 0xFFFu) | ((n & 3u) | (n >> 2) << 6) << 24;
   }
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");

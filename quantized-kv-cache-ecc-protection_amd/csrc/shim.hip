@@ -156,6 +156,14 @@ __device__ __forceinline__ uint32_t ld_word(const uint8_t *base, int64_t slot, u
   return *reinterpret_cast<const uint32_t *>(base + slot * d + 4 * c);
 }
 
+// codewords 4c..4c+3 of row `pos`, or 0 when its block is missing (table entry
+// -1): the tile kernels' and the host twin's reading of a missing block
+__device__ __forceinline__ uint32_t ld_word_or0(const ShimGeom &geo, const uint8_t *base, uint32_t pos, uint32_t h,
+                                                uint32_t c) {
+  if (geo.table[pos / geo.bs] < 0) return 0u;
+  return ld_word(base, geo.slot(pos, h), geo.d, c);
+}
+
 // byte codecs (raw INT4, H(7,4), H(8,4)): one lane per 4 codewords (d % 4 == 0)
 template <typename TO, int CODEC, bool INTERP, bool STATS>
 __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a) {
@@ -169,23 +177,28 @@ __global__ __launch_bounds__(kBlock) void shim_read_bytes_kernel(ShimReadArgs a)
     const uint32_t hl = t / c4, c = t - hl * c4;
     const uint32_t h = hl / a.ctx, l = hl - h * a.ctx;
     const uint8_t *base = reinterpret_cast<const uint8_t *>(a.cache[side]);
+    TO *o = reinterpret_cast<TO *>(a.out[side]) + ((int64_t)h * a.ctx + l) * geo.d + 4 * c;
+    if (geo.table[l / geo.bs] < 0) {  // no physical block: +0, as the tile kernels
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = from_f32<TO>(0.0f);
+      continue;
+    }
     const int64_t slot = geo.slot(l, h);
     const uint32_t w = ld_word(base, slot, geo.d, c);
     uint32_t q = w, type;
     if (CODEC == KVECC_CODEC_H84) {
       h84_decode4(w, q, type, n1, n2);
-      if (INTERP) {  // neighbours are the decoded (not interpolated) values
+      if (INTERP) {  // neighbours are the decoded (not interpolated) values; a missing one reads as 0
         const uint32_t lp = l > 0 ? l - 1 : 0, ln = l + 1 < a.ctx ? l + 1 : a.ctx - 1;
         uint32_t ql, qr, tt, u1 = 0, u2 = 0;
-        h84_decode4(ld_word(base, geo.slot(lp, h), geo.d, c), ql, tt, u1, u2);
-        h84_decode4(ld_word(base, geo.slot(ln, h), geo.d, c), qr, tt, u1, u2);
+        h84_decode4(ld_word_or0(geo, base, lp, h, c), ql, tt, u1, u2);
+        h84_decode4(ld_word_or0(geo, base, ln, h, c), qr, tt, u1, u2);
         q = interp_word(q, ql, qr, type);
       }
     } else if (CODEC == KVECC_CODEC_H74) {
       h74_decode4(w, q, type, n1);
     }
-    dequant4(reinterpret_cast<TO *>(a.out[side]) + ((int64_t)h * a.ctx + l) * geo.d + 4 * c, q,
-             a.scales[side][slot]);
+    dequant4(o, q, a.scales[side][slot]);
   }
   if (STATS) flush_stats2(a.stats, n1, n2);
 }
@@ -263,6 +276,24 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 #ifndef KVECC_SHIM_TILE_TPI
 #define KVECC_SHIM_TILE_TPI 1
 #endif
+// Work distribution.  CHUNK 0: a persistent grid of PER_CU workgroups per CU,
+// wave w taking tiles w, w + nwaves, ...  CHUNK P > 0: wave w takes the P
+// consecutive tiles [w P, w P + P), and the grid covers every tile once, so
+// workgroups retire and are replaced in dispatch order; LDS_PAD bytes of
+// dynamic LDS per workgroup cap the workgroups per CU.  (BYTES_*: the same for
+// the byte-codec kernel, which has no tables to stage per workgroup.)
+#ifndef KVECC_SHIM_TILE_CHUNK
+#define KVECC_SHIM_TILE_CHUNK 0
+#endif
+#ifndef KVECC_SHIM_TILE_LDS_PAD
+#define KVECC_SHIM_TILE_LDS_PAD 0
+#endif
+#ifndef KVECC_SHIM_BYTES_CHUNK
+#define KVECC_SHIM_BYTES_CHUNK KVECC_SHIM_TILE_CHUNK
+#endif
+#ifndef KVECC_SHIM_BYTES_LDS_PAD
+#define KVECC_SHIM_BYTES_LDS_PAD KVECC_SHIM_TILE_LDS_PAD
+#endif
 constexpr int kTileBlock = KVECC_SHIM_TILE_BLOCK;  // 8 waves per workgroup
 constexpr int kTileTPI = KVECC_SHIM_TILE_TPI;      // tiles in flight per wave
 constexpr int kTileWaves = kTileBlock / kWave;
@@ -314,7 +345,8 @@ __device__ __forceinline__ ShimTile shim_tile(const ShimTileArgs &a, uint32_t u)
 // per-lane items, identical for every tile
 struct TileItems {
   uint32_t r1[kTileGroups], q1[kTileGroups];  // phase 1: row, 4-codeword group
-  uint32_t r2[2 * kTileChunks], j2[2 * kTileChunks];  // phase 2: row, VPL-value chunk
+  uint32_t r2[2 * kTileChunks], j2[2 * kTileChunks];  // phase 2: row, the chunk's LDS byte offset
+  uint32_t o2[2 * kTileChunks];                       // phase 2: output byte offset in the tile
 };
 
 // the tile's codewords and its rows' scales, into registers.  Buffer
@@ -418,6 +450,66 @@ __device__ __forceinline__ void dequant_store(TO *dst, const uint32_t *nb, float
   }
 }
 
+// ---- fast dequantization -------------------------------------------------------
+// (n - 8) * s as fma(n, s, -8 s): -8 s is exact for |s| < 2^100, so the fma
+// rounds the exact (n - 8) s once, which is the reference's fp32 product bit
+// for bit; and s = 0 (a missing block's rows, which load scale 0, and rows
+// past a tile) gives +0 for every n, where the product gives -0 for n < 8.
+// Per 8 values: 8 v_cvt_f32_ubyte, 4 v_pk_fma_f32, 4 v_cvt_pk_{f16,bf16}_f32
+// (dequant1 + scalar conversions took ~4.5 VALU ops per value).  A tile with
+// a row scale outside that range (inf, NaN, huge) takes dequant_store instead.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ bool fast_scale(float s) { return __builtin_fabsf(s) < 0x1p100f; }
+
+// 4 nibble bytes -> 4 fp32 values, as two pairs
+__device__ __forceinline__ void dq4(uint32_t nb, float s, float m8s, f32x2 &lo, f32x2 &hi) {
+  const f32x2 ss = {s, s}, mm = {m8s, m8s};
+  const f32x2 a = {(float)(nb & 0xFFu), (float)(nb >> 8 & 0xFFu)};
+  const f32x2 b = {(float)(nb >> 16 & 0xFFu), (float)(nb >> 24)};
+  lo = __builtin_elementwise_fma(a, ss, mm);
+  hi = __builtin_elementwise_fma(b, ss, mm);
+  asm("" : "+v"(lo), "+v"(hi));  // rounded to fp32 here: no v_fma_mix contraction with the conversion
+}
+
+template <typename TO>
+__device__ __forceinline__ uint32_t pack2(f32x2 v) {
+  if constexpr (std::is_same<TO, __half>::value)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+  else
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
+// the 16 output bytes of VPL nibble bytes (fp16/bf16: nb[0..1], fp32: nb[0])
+template <typename TO>
+__device__ __forceinline__ u32x4 dq16(const uint32_t *nb, float s, float m8s) {
+  f32x2 v[4];
+  dq4(nb[0], s, m8s, v[0], v[1]);
+  if constexpr (sizeof(TO) == 4) {
+    return u32x4{__float_as_uint(v[0].x), __float_as_uint(v[0].y), __float_as_uint(v[1].x),
+                 __float_as_uint(v[1].y)};
+  } else {
+    dq4(nb[1], s, m8s, v[2], v[3]);
+    return u32x4{pack2<TO>(v[0]), pack2<TO>(v[1]), pack2<TO>(v[2]), pack2<TO>(v[3])};
+  }
+}
+
+// 16-byte store through a tile's output descriptor (offsets past it are dropped)
+__device__ __forceinline__ void tile_store(const __amdgpu_buffer_rsrc_t &os, uint32_t off, const u32x4 &v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), os,
+                                         off, 0, kTileAux);
+}
+
+// a tile's output rows [pos0, pos0 + rows) of [bh, ctx, d] as a buffer resource
+template <typename TO>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_out(const ShimTileArgs &a, const ShimTile &t) {
+  char *base = const_cast<char *>(uni(reinterpret_cast<const char *>(a.out[uni(t.side)]) +
+                                      ((int64_t)uni(t.bh) * a.ctx + uni(t.pos0)) * a.d * (int64_t)sizeof(TO)));
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)uni(t.rows * a.d * (uint32_t)sizeof(TO)), 0x00020000);
+}
+
 template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
@@ -454,29 +546,35 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   // reciprocal multiply exact for v < 2^32 / dv (v < 64 NC, dv = d / 4 >= 2)
   constexpr bool kItemsInRegs = NC <= 8;
   const uint32_t inv_dv = kItemsInRegs ? 0u : (uint32_t)(((1ull << 32) + dv - 1) / dv);
-  if (kItemsInRegs) {
+  if (kItemsInRegs) {  // r2: row, j2: the item's LDS byte offset in the tile
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
       const uint32_t v = lane + kWave * i;
       it.r2[i] = v / dv;
-      it.j2[i] = v - it.r2[i] * dv;
+      it.j2[i] = it.r2[i] * a.lr + V * (v - it.r2[i] * dv);
+      it.o2[i] = (it.r2[i] * a.d + V * (v - it.r2[i] * dv)) * (uint32_t)sizeof(TO);
     }
   }
   uint32_t bits = 0, unc = 0;
 
-  // kTileTPI tiles per iteration: u, u + nwaves, ...; all their loads in flight
-  uint32_t u = blockIdx.x * kTileWaves + wave;
-  if (u >= a.units) return;  // no workgroup barrier below: waves retire independently
+  // kTileTPI tiles per iteration: u, u + ustep, ...; all their loads in flight
+  constexpr uint32_t kChunk = KVECC_SHIM_TILE_CHUNK;
+  static_assert(kChunk == 0 || kTileTPI == 1, "chunked tiles take one tile per iteration");
+  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  uint32_t u = kChunk ? gw * kChunk : gw;
+  const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
+  const uint32_t ustep = kChunk ? 1u : nwaves;
+  if (u >= uend) return;  // no workgroup barrier below: waves retire independently
   ShimTile cur[kTileTPI];
-  bool valid[kTileTPI];
+  bool valid[kTileTPI], fast[kTileTPI];
   u32x4 w[kTileTPI][kTileGroups];
   float scale[kTileTPI];
   auto fetch = [&](uint32_t u0) {
 #pragma unroll
     for (int k = 0; k < kTileTPI; ++k) {
-      valid[k] = u0 + k * nwaves < a.units;  // uniform
+      valid[k] = u0 + k * ustep < uend;  // uniform
       if (valid[k]) {
-        cur[k] = shim_tile(a, u0 + k * nwaves);
+        cur[k] = shim_tile(a, u0 + k * ustep);
         tile_issue<PACKED>(a, cur[k], lane, it, w[k], scale[k]);
       }
     }
@@ -489,6 +587,11 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
       if (!valid[k]) continue;
       uint8_t *stage = stage_all[wave][k];
       scale_all[wave][k][lane] = scale[k];
+      // the fast dequantization holds for every row scale of the tile
+      fast[k] = __builtin_amdgcn_ballot_w64(!fast_scale(scale[k])) == 0;
+      // (n & 3) | uncorrectable << 6 per codeword (the correction table's byte
+      // 3), summed over the lane's <= 16 codewords of the tile: no carry
+      uint32_t cnt = 0;
 #pragma unroll
       for (int i = 0; i < kTileGroups; ++i) {
         if (i * kWave >= (int)groups) break;  // uniform
@@ -496,20 +599,20 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
         uint32_t sp[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const uint32_t cw = tile_cw<PACKED>(w[k][i], c);
+          uint32_t cw = tile_cw<PACKED>(w[k][i], c);
+          // a row's last group runs into the next row: that codeword decodes
+          // as 0 (no count), and its bytes land in the LDS row's padding
+          if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
 #if KVECC_SHIM_TILE_NODECODE  // memory-ceiling experiment: no table lookups (wrong values)
           const uint32_t p = cw, e = 0;
 #else
-          const uint32_t p = tab[cw & 0xFFFu];
-          // syndrome = parity bits ^ parity(data): (cw >> 12 ^ p >> 20) & 0xFFF
-          const uint32_t e = tab[4096 + (((cw >> 12) ^ (p >> 20)) & 0xFFFu)];
+          const char *tb = reinterpret_cast<const char *>(tab);
+          const uint32_t p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
+          // syndrome = parity bits ^ parity(data), as a byte offset: ((cw >> 12 ^ p >> 20) & 0xFFF) * 4
+          const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 16384 + (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
 #endif
           sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
-          if (STATS && 4 * q + c < a.g) {  // a row's last group runs into the next row
-            const uint32_t n = e >> 24;  // 0-3 bits corrected, 4 = uncorrectable
-            bits += n & 3u;
-            unc += n >> 2;
-          }
+          if (STATS) cnt += e >> 24;
         }
         if (it.r1[i] < a.tr) {  // groups past the tile's last row are never staged
           uint32_t *dst = reinterpret_cast<uint32_t *>(stage + it.r1[i] * a.lr + 12 * q);
@@ -518,44 +621,63 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
           dst[2] = sp[2] >> 16 | sp[3] << 8;
         }
       }
+      if (STATS) {
+        bits += cnt & 63u;
+        unc += cnt >> 6;
+      }
     }
     wave_lds_sync();
     // ---- prefetch the next tiles' codewords and scales ---------------------------
     ShimTile t[kTileTPI];
-    bool tv[kTileTPI];
+    bool tv[kTileTPI], tf[kTileTPI];
 #pragma unroll
     for (int k = 0; k < kTileTPI; ++k) {
       t[k] = cur[k];
       tv[k] = valid[k];
+      tf[k] = fast[k];
     }
-    u += kTileTPI * nwaves;
-    const bool more = u < a.units;
+    u += kTileTPI * ustep;
+    const bool more = u < uend;
     if (more) fetch(u);
-    // ---- phase 2: dequantize 8 values per lane, 16-byte stores -----------------
+    // ---- phase 2: dequantize VPL values per lane, one 16-byte store each -------
+    // (stores of rows past the tile fall outside its output descriptor: dropped)
 #pragma unroll
     for (int k = 0; k < kTileTPI; ++k) {
       if (!tv[k]) continue;
       const uint8_t *stage = stage_all[wave][k];
-      TO *out = reinterpret_cast<TO *>(a.out[t[k].side]) + ((int64_t)t[k].bh * a.ctx + t[k].pos0) * a.d;
-      const bool dead = t[k].row0 < 0;  // no physical block: +0 (the product would give -0)
+      const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t[k]);
+      if (tf[k]) {
 #pragma unroll
-      for (int i = 0; i < NC; ++i) {
-        if (i * kWave >= (int)chunks) break;  // uniform
-        uint32_t r, j;
-        if (kItemsInRegs) {
-          r = it.r2[i];
-          j = it.j2[i];
-        } else {
-          const uint32_t v = lane + kWave * i;
-          r = __umulhi(v, inv_dv);
-          j = v - r * dv;
+        for (int i = 0; i < NC; ++i) {
+          if (i * kWave >= (int)chunks) break;  // uniform
+          uint32_t r, l;
+          if (kItemsInRegs) {
+            r = it.r2[i];
+            l = it.j2[i];
+          } else {
+            const uint32_t v = lane + kWave * i;
+            r = __umulhi(v, inv_dv);
+            l = r * a.lr + V * (v - r * dv);
+          }
+          const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + l);
+          const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
+          const float s = scale_all[wave][k][r];
+          // output byte offset: (r d + V j) sizeof(TO), with V j = l - r lr
+          const uint32_t o = kItemsInRegs ? it.o2[i] : (r * a.d + l - r * a.lr) * (uint32_t)sizeof(TO);
+          tile_store(os, o, dq16<TO>(nb, s, s * -8.0f));
         }
-        if (r < t[k].rows) {
-          uint32_t nb[2];
-          const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + V * j);
-          nb[0] = src[0];
-          nb[1] = V == 8 ? src[1] : 0u;
-          dequant_store<TO>(out + (int64_t)r * a.d + V * j, nb, scale_all[wave][k][r], dead);
+      } else {  // a scale outside the fast form's range: the product, rounded to fp32
+        const bool dead = t[k].row0 < 0;  // no physical block: +0 (the product would give -0)
+        for (int i = 0; i < NC; ++i) {
+          if (i * kWave >= (int)chunks) break;  // uniform
+          const uint32_t v = lane + kWave * i;
+          const uint32_t r = v / dv, j = v - r * dv;
+          if (r < t[k].rows) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + V * j);
+            const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
+            TO *out = reinterpret_cast<TO *>(a.out[t[k].side]) + ((int64_t)t[k].bh * a.ctx + t[k].pos0) * a.d;
+            dequant_store<TO>(out + (int64_t)r * a.d + V * j, nb, scale_all[wave][k][r], dead);
+          }
         }
       }
     }
@@ -566,7 +688,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     bits = wave_sum(bits);
     unc = wave_sum(unc);
     if (lane == 0) {
-      uint64_t *slot = a.stats + ((blockIdx.x * kTileWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
       if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
       if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
     }
@@ -636,8 +758,12 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
   uint32_t n1 = 0, n2 = 0;
-  uint32_t u = blockIdx.x * kTileWaves + wave;
-  if (u >= a.units) return;
+  constexpr uint32_t kChunk = KVECC_SHIM_BYTES_CHUNK;
+  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  uint32_t u = kChunk ? gw * kChunk : gw;
+  const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
+  const uint32_t ustep = kChunk ? 1u : nwaves;
+  if (u >= uend) return;
 
   ShimTile cur;
   u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
@@ -745,8 +871,8 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     }
     wave_lds_sync();
     const ShimTile t = cur;
-    u += nwaves;
-    const bool more = u < a.units;
+    u += ustep;
+    const bool more = u < uend;
     if (more) fetch(u);
     // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
     // wave-instruction stores 1 KiB contiguous ------------------------------------
@@ -786,7 +912,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     n1 = wave_sum(n1);
     n2 = wave_sum(n2);
     if (lane == 0) {
-      uint64_t *slot = a.stats + ((blockIdx.x * kTileWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
       if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
       if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
     }
@@ -852,30 +978,40 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
   }
 }
 
+// workgroups for `units` tiles: one pass over every tile in chunks, or the
+// persistent grid
+static unsigned tile_grid(uint32_t units, uint32_t chunk) {
+  if (chunk) return (unsigned)cdiv(cdiv(units, chunk), kTileWaves);
+  return (unsigned)std::min<int64_t>(cdiv(units, kTileWaves), (int64_t)cu_count() * KVECC_SHIM_TILE_PER_CU);
+}
+
 template <typename TO>
 static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * KVECC_SHIM_TILE_PER_CU);
+  const unsigned grid = tile_grid(a.units, KVECC_SHIM_TILE_CHUNK);
+  constexpr unsigned pad = KVECC_SHIM_TILE_LDS_PAD;
   if (a.stats && packed)
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), pad, st, a);
   else if (a.stats)
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, false>), dim3(grid), dim3(kTileBlock), pad, st, a);
   else if (packed)
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, true>), dim3(grid), dim3(kTileBlock), pad, st, a);
   else
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), pad, st, a);
 }
 
 template <typename TO, int CODEC, bool INTERP>
 static void launch_bytes_tiles_s(const ShimTileArgs &a, unsigned grid, hipStream_t st) {
   if (a.stats)
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kTileBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kTileBlock),
+                 KVECC_SHIM_BYTES_LDS_PAD, st, a);
   else
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kTileBlock), 0, st, a);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kTileBlock),
+                 KVECC_SHIM_BYTES_LDS_PAD, st, a);
 }
 
 template <typename TO>
 static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * KVECC_SHIM_TILE_PER_CU);
+  const unsigned grid = tile_grid(a.units, KVECC_SHIM_BYTES_CHUNK);
   if (codec == KVECC_CODEC_H84 && interp)
     launch_bytes_tiles_s<TO, KVECC_CODEC_H84, true>(a, grid, st);
   else if (codec == KVECC_CODEC_H84)

@@ -223,7 +223,7 @@ def golay_encode_rows_into(nibbles: torch.Tensor, out: torch.Tensor) -> None:
     d = nibbles.shape[-1]
     g = (d + 2) // 3
     if (nibbles.dtype != torch.uint8 or out.dtype != torch.int32 or not nibbles.is_contiguous()
-            or not out.is_contiguous() or out.shape[-1] != g or out.numel() * 3 < nibbles.numel()
+            or not out.is_contiguous() or out.shape[-1] != g or out.shape[:-1] != nibbles.shape[:-1]
             or out.device != nibbles.device):
         raise ValueError("golay_encode_rows_into: contiguous uint8 [..., D] -> int32 [..., ceil(D/3)]")
     rows = nibbles.numel() // d if d else 0
@@ -515,17 +515,11 @@ def shim_read_batch(k_cache, v_cache, k_scales, v_scales, block_table, ctx, head
     for every sequence of a paged cache at once: block_table [B, max_blocks]
     int32 (row b = sequence b), caches [blocks, layers, hkv, block_size * P]
     -> (K, V) [B, hkv, ctx, head_dim] in out_dtype (kvecc_shim_read_batch)."""
-    nb, nl, hkv, row = k_cache.shape
-    per = {"golay": (head_dim + 2) // 3, "golay_packed": (3 * ((head_dim + 2) // 3) + 3) // 4 * 4}.get(
-        codec, head_dim)
-    if row % per:
-        raise ValueError(f"cache rows of {row} words do not hold whole token rows of {per}")
-    bs = row // per
-    if block_table.dim() != 2 or block_table.dtype != torch.int32 or not block_table.is_contiguous():
-        raise ValueError("block_table must be a contiguous int32 [B, max_blocks] tensor")
-    if block_table.shape[1] * bs < ctx:
-        raise ValueError(f"block_table covers {block_table.shape[1] * bs} tokens < ctx {ctx}")
-    batch = block_table.shape[0]
+    from .ops import _check_shim_read_args  # pure torch, device-agnostic
+    if k_cache.device.type != "cpu":
+        raise ValueError(f"the cpu backend reads host tensors, k_cache is on {k_cache.device}")
+    batch, nl, hkv, bs = _check_shim_read_args(k_cache, v_cache, k_scales, v_scales, block_table, ctx,
+                                               head_dim, layer, codec, out_dtype, stats, out)
     shape = (batch, hkv, ctx, head_dim)
     if out is None:
         out = (torch.empty(shape, dtype=out_dtype, device=k_cache.device),

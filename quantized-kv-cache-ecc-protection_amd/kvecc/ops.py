@@ -268,7 +268,7 @@ def golay_encode_rows_into(nibbles: torch.Tensor, out: torch.Tensor) -> None:
     d = nibbles.shape[-1]
     g = (d + 2) // 3
     if (nibbles.dtype != torch.uint8 or out.dtype != torch.int32 or not nibbles.is_contiguous()
-            or not out.is_contiguous() or out.shape[-1] != g or out.numel() * 3 < nibbles.numel()
+            or not out.is_contiguous() or out.shape[-1] != g or out.shape[:-1] != nibbles.shape[:-1]
             or out.device != nibbles.device):
         raise ValueError("golay_encode_rows_into: contiguous uint8 [..., D] -> int32 [..., ceil(D/3)]")
     rows = nibbles.numel() // d if d else 0
@@ -647,23 +647,73 @@ def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=
     return k_out, v_out
 
 
+_SHIM_CACHE_DT = {"int4": torch.uint8, "hamming74": torch.uint8, "hamming84": torch.uint8,
+                  "golay": torch.int32, "golay_packed": torch.uint8}
+
+
+def _check_shim_read_args(k_cache, v_cache, k_scales, v_scales, block_table, ctx, head_dim, layer, codec,
+                          out_dtype, stats, out):
+    """Validate a batched shim read (both backends): cache dtype per codec and
+    geometry, scales [blocks, layers, hkv, block_size] fp32, the block table,
+    a caller-supplied ``out`` pair ([B, hkv, ctx, head_dim], out_dtype,
+    contiguous), and one device for every tensor -- a mismatch raises
+    ValueError instead of reading or writing past an allocation.
+    Returns (batch, layers, hkv, block_size)."""
+    if codec not in _SHIM_CACHE_DT:
+        raise ValueError(f"shim codec {codec!r} (int4, hamming74, hamming84, golay or golay_packed)")
+    if out_dtype not in _DT:
+        raise ValueError(f"out_dtype must be fp32/fp16/bf16, got {out_dtype}")
+    if k_cache.dim() != 4 or k_cache.shape != v_cache.shape:
+        raise ValueError("k_cache / v_cache must share one [blocks, layers, kv_heads, row] shape")
+    nb, nl, hkv, row = k_cache.shape
+    for name, c in (("k_cache", k_cache), ("v_cache", v_cache)):
+        if c.dtype != _SHIM_CACHE_DT[codec]:
+            raise ValueError(f"{codec} {name} must be {_SHIM_CACHE_DT[codec]}, got {c.dtype}")
+    if head_dim < 1:
+        raise ValueError(f"head_dim must be positive, got {head_dim}")
+    per = {"golay": (head_dim + 2) // 3, "golay_packed": (3 * ((head_dim + 2) // 3) + 3) // 4 * 4}.get(
+        codec, head_dim)
+    if row % per:
+        raise ValueError(f"cache rows of {row} words do not hold whole token rows of {per}")
+    bs = row // per
+    if not 0 <= int(layer) < nl:
+        raise ValueError(f"layer {layer} outside the cache's {nl} layers")
+    if block_table.dim() != 2 or block_table.dtype != torch.int32:
+        raise ValueError("block_table must be a contiguous int32 [B, max_blocks] tensor")
+    if block_table.shape[1] * bs < ctx:
+        raise ValueError(f"block_table covers {block_table.shape[1] * bs} tokens < ctx {ctx}")
+    for name, sc in (("k_scales", k_scales), ("v_scales", v_scales)):
+        if sc.shape != (nb, nl, hkv, bs) or sc.dtype != torch.float32:
+            raise ValueError(f"{name} must be float32 [{nb}, {nl}, {hkv}, {bs}], got "
+                             f"{tuple(sc.shape)} {sc.dtype}")
+    batch = block_table.shape[0]
+    tensors = [("k_cache", k_cache), ("v_cache", v_cache), ("k_scales", k_scales), ("v_scales", v_scales),
+               ("block_table", block_table)]
+    if out is not None:
+        shape = (batch, hkv, ctx, head_dim)
+        for name, o in zip(("k_out", "v_out"), out):
+            if tuple(o.shape) != shape or o.dtype != out_dtype:
+                raise ValueError(f"{name} must be {out_dtype} {list(shape)}, got {o.dtype} {list(o.shape)}")
+            tensors.append((name, o))
+    for name, t in tensors:
+        if t.device != k_cache.device:
+            raise ValueError(f"{name} is on {t.device}, k_cache on {k_cache.device}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+    if stats is not None and stats.device != k_cache.device:
+        raise ValueError(f"stats is on {stats.device}, k_cache on {k_cache.device}")
+    return batch, nl, hkv, bs
+
+
 def shim_read_batch(k_cache, v_cache, k_scales, v_scales, block_table, ctx, head_dim, layer, codec,
                     out_dtype, stats=None, interp=False, out=None):
     """The shim's fused read (gather -> decode -> dequantize, ecc_shim.py:990-1071)
     for every sequence of a paged cache at once: block_table [B, max_blocks]
     int32 (row b = sequence b), caches [blocks, layers, hkv, block_size * P]
     -> (K, V) [B, hkv, ctx, head_dim] in out_dtype (kvecc_shim_read_batch)."""
-    nb, nl, hkv, row = k_cache.shape
-    per = {"golay": (head_dim + 2) // 3, "golay_packed": (3 * ((head_dim + 2) // 3) + 3) // 4 * 4}.get(
-        codec, head_dim)
-    if row % per:
-        raise ValueError(f"cache rows of {row} words do not hold whole token rows of {per}")
-    bs = row // per
-    if block_table.dim() != 2 or block_table.dtype != torch.int32 or not block_table.is_contiguous():
-        raise ValueError("block_table must be a contiguous int32 [B, max_blocks] tensor")
-    if block_table.shape[1] * bs < ctx:
-        raise ValueError(f"block_table covers {block_table.shape[1] * bs} tokens < ctx {ctx}")
-    batch = block_table.shape[0]
+    _check_gpu(k_cache)
+    batch, nl, hkv, bs = _check_shim_read_args(k_cache, v_cache, k_scales, v_scales, block_table, ctx,
+                                               head_dim, layer, codec, out_dtype, stats, out)
     shape = (batch, hkv, ctx, head_dim)
     if out is None:
         out = (torch.empty(shape, dtype=out_dtype, device=k_cache.device),

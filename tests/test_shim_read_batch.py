@@ -59,8 +59,14 @@ def make_cache(codec, batch, ctx, hkv, d, bs, layers=2, seed=0, spare=3, ber=BER
     return caches[0], caches[1], ks, vs, table
 
 
-def oracle_read(oracle, cache, scales, table, ctx, d, layer, codec, out_dtype):
-    """numpy restatement of the read for one side: [B, hkv, ctx, d] and (stat0, stat1)."""
+def oracle_read(oracle, cache, scales, table, ctx, d, layer, codec, out_dtype, interp=False):
+    """numpy restatement of the read for one side: [B, hkv, ctx, d] and (stat0, stat1).
+
+    interp (H84): the composed read of ecc_shim.py:1038-1059 per sequence --
+    decode the whole context, then oracle.interpolate_double_errors along ctx
+    (interpolation_triton.py:120-159, neighbours clamped to [0, ctx - 1]); a
+    missing (-1) block's rows read as zero codewords (decode(0) = 0, no error)
+    and output +0."""
     nb, layers, hkv, row = cache.shape
     golay = codec in ("golay", "golay_packed")
     g = (d + 2) // 3
@@ -88,6 +94,14 @@ def oracle_read(oracle, cache, scales, table, ctx, d, layer, codec, out_dtype):
             q = trip.reshape(*w.shape[:-1], 3 * g)[..., :d]
             st[0] += bits
             st[1] += unc
+        elif codec == "hamming84" and interp:
+            full = np.zeros((ctx, hkv, d), np.uint8)
+            full[pos[ok]] = rows  # missing rows: codeword 0
+            q, et, (c1, c2) = oracle.hamming84_decode(full.reshape(-1))
+            q = oracle.interpolate_double_errors(q.reshape(ctx, hkv, d), et.reshape(ctx, hkv, d), seq_dim=0)
+            q = q[pos[ok]]
+            st[0] += c1
+            st[1] += c2
         elif codec == "hamming84":
             q, _, (c1, c2) = oracle.hamming84_decode(rows.reshape(-1))
             q = q.reshape(rows.shape)
@@ -119,6 +133,46 @@ def test_cpu_batch_read_vs_oracle(oracle, codec, batch, ctx, hkv, d, bs, dtype):
     k, v = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 1, codec, dtype, stats=st)
     ek, sk = oracle_read(oracle, kc, ks, table, ctx, d, 1, codec, dtype)
     ev, sv = oracle_read(oracle, vc, vs, table, ctx, d, 1, codec, dtype)
+    assert torch.equal(k, ek) and torch.equal(v, ev)
+    assert cpu_ops.read_stats(st) == [sk[0] + sv[0], sk[1] + sv[1]]
+
+
+def _plant_doubles(cache, table, d, bs, layer, rows):
+    """Make every codeword of the listed (sequence, position) rows a double
+    error (two flipped data bits: SECDED DOUBLE_DETECTED) in-place."""
+    c = cache.view(cache.shape[0], cache.shape[1], cache.shape[2], bs, d)
+    for b, pos in rows:
+        blk = int(table[b, pos // bs])
+        if blk >= 0:
+            c[blk, layer, :, pos % bs, :] ^= 0x03
+
+
+# H(8,4) + interpolation against the oracle: doubles planted in the first and
+# last rows of 16-row tiles, at the context's ends and next to missing blocks.
+INTERP_CPU_CASES = [(2, 70, 2, 64, 16), (1, 40, 3, 32, 16), (2, 33, 2, 128, 8), (1, 1, 1, 16, 16),
+                    (2, 45, 2, 48, 7)]
+
+
+@pytest.mark.parametrize("batch,ctx,hkv,d,bs", INTERP_CPU_CASES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_cpu_batch_read_interp_vs_oracle(oracle, batch, ctx, hkv, d, bs, dtype):
+    from kvecc import cpu_ops
+    kc, vc, ks, vs, table = make_cache("hamming84", batch, ctx, hkv, d, bs, seed=ctx + 5, ber=3e-3)
+    rows = set()
+    for b in range(batch):
+        for pos in (0, ctx - 1, 15, 16, 31, 32, bs - 1, bs, 2 * bs - 1):
+            if 0 <= pos < ctx:
+                rows.add((b, pos))
+    for kv in (kc, vc):
+        _plant_doubles(kv, table, d, bs, 1, sorted(rows))
+    nlb = (ctx + bs - 1) // bs
+    if nlb > 2:  # a missing inner block: its neighbours interpolate against zeros
+        table[batch - 1, 1] = -1
+    st = cpu_ops.new_stats()
+    k, v = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 1, "hamming84", dtype, interp=True, stats=st)
+    ek, sk = oracle_read(oracle, kc, ks, table, ctx, d, 1, "hamming84", dtype, interp=True)
+    ev, sv = oracle_read(oracle, vc, vs, table, ctx, d, 1, "hamming84", dtype, interp=True)
+    assert sk[1] > 0  # doubles were decoded
     assert torch.equal(k, ek) and torch.equal(v, ev)
     assert cpu_ops.read_stats(st) == [sk[0] + sv[0], sk[1] + sv[1]]
 
@@ -219,23 +273,29 @@ def test_hip_batch_read_interp_many_tiles(gpu, batch, ctx, hkv, d, bs, ber):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("codec,interp", [("hamming84", False), ("hamming84", True), ("hamming74", False),
-                                          ("int4", False)])
-def test_hip_missing_byte_block_reads_zero(gpu, codec, interp):
+@pytest.mark.parametrize("codec,interp,d", [("hamming84", False, 64), ("hamming84", True, 64),
+                                            ("hamming74", False, 64), ("int4", False, 64),
+                                            # per-sequence kernels: d % 16 != 0, or interp with d > 512
+                                            ("hamming84", False, 36), ("hamming84", True, 48),
+                                            ("hamming74", False, 36), ("int4", False, 48),
+                                            ("hamming84", True, 528)])
+def test_hip_missing_byte_block_reads_zero(gpu, codec, interp, d):
     """A -1 block (never produced by the shim) reads as +0 rows, and as zero
-    codewords where it is an interpolation neighbour -- the same on both backends."""
+    codewords where it is an interpolation neighbour -- the same on both backends
+    and in both the wave-tile and the per-sequence kernels."""
     from kvecc import cpu_ops, ops
-    kc, vc, ks, vs, table = make_cache(codec, 2, 40, 2, 64, 16, seed=4)
+    kc, vc, ks, vs, table = make_cache(codec, 2, 40, 2, d, 16, seed=4)
     table[1, 1] = -1
     table[0, 0] = -1
     st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
-    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 40, 64, 1, codec, torch.float16, stats=st,
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, 40, d, 1, codec, torch.float16, stats=st,
                                      interp=interp)
     t = lambda x: x.to(gpu)  # noqa: E731
-    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), 40, 64, 1, codec, torch.float16,
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), 40, d, 1, codec, torch.float16,
                                stats=gst, interp=interp)
     assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
-    assert torch.equal(k[1, :, 16:32].cpu(), torch.zeros(2, 16, 64, dtype=torch.float16))
+    assert torch.equal(k[1, :, 16:32].cpu(), torch.zeros(2, 16, d, dtype=torch.float16))
+    assert torch.equal(k[0, :, 0:16].cpu(), torch.zeros(2, 16, d, dtype=torch.float16))
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
 
 
