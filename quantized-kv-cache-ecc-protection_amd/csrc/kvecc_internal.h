@@ -34,9 +34,21 @@ const uint16_t *golay_correct_table_dev();
 // byte, spread(x) = x&15 | (x>>4&15)<<8 | (x>>8&15)<<16, so a value converts
 // with one v_cvt_f32_ubyteN:
 //   [0, 4096)    spread(d) | parity(d) << 20
-//   [4096, 8192) spread(data error of syndrome s) | count(s) << 24
-//                (spread part 0 and count 4 when uncorrectable)
+//   [4096, 8192) spread(data error of syndrome s) | ((count(s) & 3) | unc << 6) << 24
+//                (count 0-3 bits corrected; uncorrectable: spread part 0, byte 3 = 0x40)
 const uint32_t *golay_attn_table_dev();
+// Work counters of the dynamically scheduled tile kernels (shim.hip): a ring of
+// kDynSlots slots per device, each kDynCounters counters kDynStride words apart,
+// zero between launches (each counter's last user resets it).  shim_dyn_slot() hands out the current device's slots round-robin,
+// so up to kDynSlots launches may be in flight at once.
+#ifndef KVECC_SHIM_DYN_COUNTERS
+#define KVECC_SHIM_DYN_COUNTERS 128
+#endif
+constexpr int kDynCounters = KVECC_SHIM_DYN_COUNTERS;
+constexpr int kDynStride = 64;  // uint32 words (256 B) between counters
+constexpr int kDynSlots = 64;
+constexpr int kDynSlotWords = kDynCounters * kDynStride;
+uint32_t *shim_dyn_slot();
 // host-side table builders (product copy, independent of the test oracle)
 void build_golay_parity_table(uint16_t *out4096);
 void build_golay_correct_table(uint16_t *out4096);

@@ -37,6 +37,8 @@ static int g_cu[kMaxDev];
 static std::atomic<uint16_t *> g_parity[kMaxDev];
 static std::atomic<uint16_t *> g_correct[kMaxDev];
 static std::atomic<uint32_t *> g_attn[kMaxDev];
+static std::atomic<uint32_t *> g_dyn[kMaxDev];  // kDynSlots work-counter slots, zeroed
+static std::atomic<uint32_t> g_dyn_next[kMaxDev];
 
 int current_device() {
   int d = 0;
@@ -141,10 +143,16 @@ static int ensure_tables(int d) {
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
   if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
   Host *buf = nullptr;
+  uint32_t *dyn = nullptr;
+  const size_t dyn_bytes = sizeof(uint32_t) * kDynSlots * kDynSlotWords;
   hipError_t e = hipMalloc(&buf, sizeof(Host));
   if (e == hipSuccess) e = hipMemcpy(buf, &host, sizeof(Host), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&dyn, dyn_bytes);
+  if (e == hipSuccess) e = hipMemset(dyn, 0, dyn_bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return set_error(KVECC_EHIP, "golay table upload: %s", hipGetErrorString(e));
+  g_dyn[d].store(dyn, std::memory_order_release);
   g_parity[d].store(buf->par, std::memory_order_release);
   g_correct[d].store(buf->cor, std::memory_order_release);
   g_attn[d].store(buf->attn, std::memory_order_release);  // last: the "built" flag
@@ -162,6 +170,13 @@ static const P *table_dev(std::atomic<P *> *tabs) {
 const uint16_t *golay_parity_table_dev() { return table_dev(g_parity); }
 const uint16_t *golay_correct_table_dev() { return table_dev(g_correct); }
 const uint32_t *golay_attn_table_dev() { return table_dev(g_attn); }
+
+uint32_t *shim_dyn_slot() {
+  const int d = current_device();
+  if (!table_dev(g_attn)) return nullptr;  // allocated with the tables
+  const uint32_t k = g_dyn_next[d].fetch_add(1, std::memory_order_relaxed) % kDynSlots;
+  return g_dyn[d].load(std::memory_order_acquire) + (size_t)k * kDynSlotWords;
+}
 
 }  // namespace kvecc
 

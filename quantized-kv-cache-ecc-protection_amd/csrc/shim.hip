@@ -294,6 +294,21 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 #ifndef KVECC_SHIM_BYTES_LDS_PAD
 #define KVECC_SHIM_BYTES_LDS_PAD KVECC_SHIM_TILE_LDS_PAD
 #endif
+// DYN (CHUNK 0): a wave takes its first DYN_STATIC tiles w, w + nwaves, ...
+// statically and the rest from work counters (kDynCounters per launch, counter
+// c handing out tiles base + k kDynCounters + c in turn), one atomic per tile,
+// issued a tile ahead.  With equal static shares the waves of one launch
+// finished 119-166 us apart at [8,4096,32,128] (mean 143 us;
+// tools/exp/run_wave_times.py): memory latency is not even across the chip.
+#ifndef KVECC_SHIM_TILE_DYN
+#define KVECC_SHIM_TILE_DYN 0
+#endif
+#ifndef KVECC_SHIM_DYN_PROBE
+#define KVECC_SHIM_DYN_PROBE 0
+#endif
+#ifndef KVECC_SHIM_TILE_DYN_STATIC
+#define KVECC_SHIM_TILE_DYN_STATIC 8
+#endif
 constexpr int kTileBlock = KVECC_SHIM_TILE_BLOCK;  // 8 waves per workgroup
 constexpr int kTileTPI = KVECC_SHIM_TILE_TPI;      // tiles in flight per wave
 constexpr int kTileWaves = kTileBlock / kWave;
@@ -317,6 +332,76 @@ struct ShimTileArgs {
   uint32_t nlb;           // logical blocks covering ctx
   uint32_t units;         // 2 * batch * hkv * nlb * tpb
   uint32_t rowb;          // bytes per cache row (4g int32, KVECC_GOLAY_PACKED_ROW(g) packed)
+  uint32_t *dyn;          // work-counter slot (shim_dyn_slot) of the dynamic schedule
+};
+
+// The dynamic tile schedule of one wave (KVECC_SHIM_TILE_DYN): its first tile
+// is gw, next() gives the following ones (>= units: none left).  Counter c
+// serves the W_c waves gw = c (mod kDynCounters) with its K_c tiles; every
+// such wave stops after its first failed grab, so the failed grabs return
+// K_c .. K_c + W_c - 1, and the wave that draws the last of them is the last
+// to touch the counter: it resets it to 0 for the next launch.  (A "done"
+// counter shared by all waves instead serialised their exits: ~40 us.)
+template <bool DYN>
+struct TileSchedule {
+  uint32_t gw, nwaves, units, cidx, sidx, gk, last_k;
+  uint32_t *ctr;
+  // a bijection of [0, nwaves) for power-of-two nwaves (probe 3 only)
+  __device__ __forceinline__ uint32_t perm(uint32_t w) const { return (w * 2654435761u) & (nwaves - 1); }
+  __device__ __forceinline__ uint32_t grab(uint32_t lane) {
+    // the offset is an opaque (per-lane) zero: with a provably uniform address
+    // the atomic optimizer rewrites the add into a broadcast of its result
+    // right after it, i.e. a vmcnt(0) wait for the round trip on every tile;
+    // here the wait comes only where next() reads the value, a tile later
+    uint32_t z;
+    asm("v_mov_b32 %0, 0" : "=v"(z));
+    uint32_t k = 0;
+    if (lane == 0) k = __hip_atomic_fetch_add(ctr + z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return k;  // lane 0's; next() broadcasts it when the tile is needed
+  }
+  __device__ __forceinline__ void init(const ShimTileArgs &a, uint32_t gw_, uint32_t nwaves_, uint32_t lane) {
+    gw = gw_;
+    nwaves = nwaves_;
+    units = a.units;
+    sidx = 1;
+    if (DYN || KVECC_SHIM_DYN_PROBE) {
+      cidx = gw % kDynCounters;
+      ctr = a.dyn + kDynStride * cidx;
+      const uint32_t base = KVECC_SHIM_TILE_DYN_STATIC * nwaves;
+      const uint32_t kc = units > base + cidx ? (units - base - cidx + kDynCounters - 1) / kDynCounters : 0u;
+      const uint32_t active = min(nwaves, units);  // waves with a first tile (gw < active)
+      const uint32_t wc = (active - cidx + kDynCounters - 1) / kDynCounters;  // >= 1: this wave
+      last_k = kc + wc - 1;
+      gk = grab(lane);
+    }
+  }
+  __device__ __forceinline__ uint32_t next(uint32_t cur, uint32_t lane) {
+#if KVECC_SHIM_DYN_PROBE == 1  // experiment: static schedule plus one atomic per tile on the counters
+    gk += grab(lane);
+    return cur + nwaves;
+#endif
+    if (!DYN) return cur + nwaves;
+#if KVECC_SHIM_DYN_PROBE == 3  // experiment: the static order with waves scrambled over tiles in each round
+    {
+      const uint32_t r = (cur - perm(gw)) / nwaves + 1;
+      return r * nwaves + perm(gw);
+    }
+#endif
+    constexpr uint32_t S = KVECC_SHIM_TILE_DYN_STATIC;
+    if (sidx < S) {
+      const uint32_t t = gw + sidx * nwaves;
+      ++sidx;
+      if (t < units) return t;
+      sidx = S;
+    }
+    const uint32_t k = __builtin_amdgcn_readfirstlane(gk);
+    const uint32_t t = S * nwaves + k * kDynCounters + cidx;
+    if (t < units)
+      gk = grab(lane);
+    else if (k == last_k && lane == 0)  // the counter's last user
+      __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t;
+  }
 };
 
 // a wave's tile: rows [row0, row0 + rows) of one cache side (wave-uniform)
@@ -400,78 +485,35 @@ __device__ __forceinline__ uint32_t tile_cw(const u32x4 &w, int k) {
   }
 }
 
-template <typename TO>
-__device__ __forceinline__ void store8(TO *dst, const float (&v)[8]) {
-  if constexpr (sizeof(TO) == 4) {
-    const u32x4 lo{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-    const u32x4 hi{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])};
-    if (KVECC_SHIM_TILE_NT) {
-      st_stream(reinterpret_cast<u32x4 *>(dst), lo);
-      st_stream(reinterpret_cast<u32x4 *>(dst) + 1, hi);
-    } else {
-      reinterpret_cast<u32x4 *>(dst)[0] = lo;
-      reinterpret_cast<u32x4 *>(dst)[1] = hi;
-    }
-  } else {
-    uint32_t p[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      p[k] = (uint32_t)__builtin_bit_cast(uint16_t, from_f32<TO>(v[2 * k])) |
-             (uint32_t)__builtin_bit_cast(uint16_t, from_f32<TO>(v[2 * k + 1])) << 16;
-    const u32x4 o{p[0], p[1], p[2], p[3]};
-    if (KVECC_SHIM_TILE_NT)
-      st_stream(reinterpret_cast<u32x4 *>(dst), o);
-    else
-      *reinterpret_cast<u32x4 *>(dst) = o;
-  }
-}
-
 // values per lane per output item: one 16-byte store (fp16/bf16: 8, fp32: 4),
 // so each wave-instruction writes 1 KiB contiguous (32-byte lane strides, two
 // stores per lane, halved the store rate)
 template <typename TO>
 constexpr int kVpl = 16 / (int)sizeof(TO);
 
-// VPL dequantized values (nibble bytes n: (n - 8) * s, or +0) as one 16-byte store
-template <typename TO>
-__device__ __forceinline__ void dequant_store(TO *dst, const uint32_t *nb, float s, bool zero) {
-  constexpr int V = kVpl<TO>;
-  float o[8];
-#pragma unroll
-  for (int e = 0; e < V; ++e) o[e] = zero ? 0.0f : dequant1(nb[e / 4] >> (8 * (e % 4)) & 0xFFu, s);
-  if constexpr (V == 4) {
-    const u32x4 v{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
-    if (KVECC_SHIM_TILE_NT)
-      st_stream(reinterpret_cast<u32x4 *>(dst), v);
-    else
-      *reinterpret_cast<u32x4 *>(dst) = v;
-  } else {
-    store8<TO>(dst, o);
-  }
-}
-
-// ---- fast dequantization -------------------------------------------------------
-// (n - 8) * s as fma(n, s, -8 s): -8 s is exact for |s| < 2^100, so the fma
-// rounds the exact (n - 8) s once, which is the reference's fp32 product bit
-// for bit; and s = 0 (a missing block's rows, which load scale 0, and rows
-// past a tile) gives +0 for every n, where the product gives -0 for n < 8.
-// Per 8 values: 8 v_cvt_f32_ubyte, 4 v_pk_fma_f32, 4 v_cvt_pk_{f16,bf16}_f32
-// (dequant1 + scalar conversions took ~4.5 VALU ops per value).  A tile with
-// a row scale outside that range (inf, NaN, huge) takes dequant_store instead.
+// ---- packed dequantization ----------------------------------------------------
+// (n - 8) * s exactly as the reference computes it (fp32 subtract, fp32 product,
+// then one RNE conversion), two values per instruction: per 8 values 8
+// v_cvt_f32_ubyte, 4 v_pk_add_f32, 4 v_pk_mul_f32, 4 v_cvt_pk_{f16,bf16}_f32
+// (dequant1 with scalar conversions took ~4.5 VALU ops per value, and its
+// volatile asm turned a `dead ? 0 : ...` per value into a branch per value).
+// A missing block's rows decode to n = 0 with scale 0 (their loads fall
+// outside the buffer descriptors); `dead` makes them n = 8, so they give
+// (8 - 8) * 0 = +0, where n = 0 would give -0.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ bool fast_scale(float s) { return __builtin_fabsf(s) < 0x1p100f; }
-
 // 4 nibble bytes -> 4 fp32 values, as two pairs
-__device__ __forceinline__ void dq4(uint32_t nb, float s, float m8s, f32x2 &lo, f32x2 &hi) {
-  const f32x2 ss = {s, s}, mm = {m8s, m8s};
+__device__ __forceinline__ void dq4(uint32_t nb, float s, f32x2 &lo, f32x2 &hi) {
+  const f32x2 ss = {s, s}, m8 = {-8.0f, -8.0f};
   const f32x2 a = {(float)(nb & 0xFFu), (float)(nb >> 8 & 0xFFu)};
   const f32x2 b = {(float)(nb >> 16 & 0xFFu), (float)(nb >> 24)};
-  lo = __builtin_elementwise_fma(a, ss, mm);
-  hi = __builtin_elementwise_fma(b, ss, mm);
-  asm("" : "+v"(lo), "+v"(hi));  // rounded to fp32 here: no v_fma_mix contraction with the conversion
+  f32x2 x = a + m8, y = b + m8;
+  asm("" : "+v"(x), "+v"(y));  // (n - 8) exactly, then the product: no fma contraction
+  lo = x * ss;
+  hi = y * ss;
+  asm("" : "+v"(lo), "+v"(hi));  // rounded to fp32 here: no v_fma_mix with the conversion
 }
 
 template <typename TO>
@@ -484,14 +526,15 @@ __device__ __forceinline__ uint32_t pack2(f32x2 v) {
 
 // the 16 output bytes of VPL nibble bytes (fp16/bf16: nb[0..1], fp32: nb[0])
 template <typename TO>
-__device__ __forceinline__ u32x4 dq16(const uint32_t *nb, float s, float m8s) {
+__device__ __forceinline__ u32x4 dq16(const uint32_t *nb, float s, bool dead) {
+  const uint32_t d8 = dead ? 0x08080808u : 0u;
   f32x2 v[4];
-  dq4(nb[0], s, m8s, v[0], v[1]);
+  dq4(nb[0] | d8, s, v[0], v[1]);
   if constexpr (sizeof(TO) == 4) {
     return u32x4{__float_as_uint(v[0].x), __float_as_uint(v[0].y), __float_as_uint(v[1].x),
                  __float_as_uint(v[1].y)};
   } else {
-    dq4(nb[1], s, m8s, v[2], v[3]);
+    dq4(nb[1] | d8, s, v[2], v[3]);
     return u32x4{pack2<TO>(v[0]), pack2<TO>(v[1]), pack2<TO>(v[2]), pack2<TO>(v[3])};
   }
 }
@@ -509,6 +552,18 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_out(const ShimTileArgs &a
                                       ((int64_t)uni(t.bh) * a.ctx + uni(t.pos0)) * a.d * (int64_t)sizeof(TO)));
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)uni(t.rows * a.d * (uint32_t)sizeof(TO)), 0x00020000);
 }
+
+// timing experiment (tools/exp/run_wave_times.py): each wave's first-tile start
+// and exit times (s_memrealtime, 100 MHz) into a buffer set by kvecc_exp_wave_times
+#ifndef KVECC_SHIM_WAVE_TIMES
+#define KVECC_SHIM_WAVE_TIMES 0
+#endif
+#if KVECC_SHIM_WAVE_TIMES
+__device__ uint64_t *g_wave_times;
+extern "C" __attribute__((visibility("default"))) int kvecc_exp_wave_times(void *buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_times), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
@@ -560,13 +615,23 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   // kTileTPI tiles per iteration: u, u + ustep, ...; all their loads in flight
   constexpr uint32_t kChunk = KVECC_SHIM_TILE_CHUNK;
   static_assert(kChunk == 0 || kTileTPI == 1, "chunked tiles take one tile per iteration");
+  constexpr bool kDyn = KVECC_SHIM_TILE_DYN && kChunk == 0 && kTileTPI == 1;
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
   uint32_t u = kChunk ? gw * kChunk : gw;
   const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
   const uint32_t ustep = kChunk ? 1u : nwaves;
   if (u >= uend) return;  // no workgroup barrier below: waves retire independently
+  TileSchedule<kDyn> sched;
+  sched.init(a, gw, nwaves, lane);
+#if KVECC_SHIM_DYN_PROBE == 3
+  u = sched.perm(gw);
+#endif
+#if KVECC_SHIM_WAVE_TIMES
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  uint32_t n_tiles = 0;
+#endif
   ShimTile cur[kTileTPI];
-  bool valid[kTileTPI], fast[kTileTPI];
+  bool valid[kTileTPI];
   u32x4 w[kTileTPI][kTileGroups];
   float scale[kTileTPI];
   auto fetch = [&](uint32_t u0) {
@@ -587,8 +652,6 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
       if (!valid[k]) continue;
       uint8_t *stage = stage_all[wave][k];
       scale_all[wave][k][lane] = scale[k];
-      // the fast dequantization holds for every row scale of the tile
-      fast[k] = __builtin_amdgcn_ballot_w64(!fast_scale(scale[k])) == 0;
       // (n & 3) | uncorrectable << 6 per codeword (the correction table's byte
       // 3), summed over the lane's <= 16 codewords of the tile: no carry
       uint32_t cnt = 0;
@@ -629,14 +692,16 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     wave_lds_sync();
     // ---- prefetch the next tiles' codewords and scales ---------------------------
     ShimTile t[kTileTPI];
-    bool tv[kTileTPI], tf[kTileTPI];
+    bool tv[kTileTPI];
 #pragma unroll
     for (int k = 0; k < kTileTPI; ++k) {
       t[k] = cur[k];
       tv[k] = valid[k];
-      tf[k] = fast[k];
     }
-    u += kTileTPI * ustep;
+#if KVECC_SHIM_WAVE_TIMES
+    ++n_tiles;
+#endif
+    u = kDyn ? sched.next(u, lane) : u + kTileTPI * ustep;
     const bool more = u < uend;
     if (more) fetch(u);
     // ---- phase 2: dequantize VPL values per lane, one 16-byte store each -------
@@ -646,44 +711,36 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
       if (!tv[k]) continue;
       const uint8_t *stage = stage_all[wave][k];
       const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t[k]);
-      if (tf[k]) {
+      const bool dead = t[k].row0 < 0;
 #pragma unroll
-        for (int i = 0; i < NC; ++i) {
-          if (i * kWave >= (int)chunks) break;  // uniform
-          uint32_t r, l;
-          if (kItemsInRegs) {
-            r = it.r2[i];
-            l = it.j2[i];
-          } else {
-            const uint32_t v = lane + kWave * i;
-            r = __umulhi(v, inv_dv);
-            l = r * a.lr + V * (v - r * dv);
-          }
-          const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + l);
-          const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
-          const float s = scale_all[wave][k][r];
-          // output byte offset: (r d + V j) sizeof(TO), with V j = l - r lr
-          const uint32_t o = kItemsInRegs ? it.o2[i] : (r * a.d + l - r * a.lr) * (uint32_t)sizeof(TO);
-          tile_store(os, o, dq16<TO>(nb, s, s * -8.0f));
-        }
-      } else {  // a scale outside the fast form's range: the product, rounded to fp32
-        const bool dead = t[k].row0 < 0;  // no physical block: +0 (the product would give -0)
-        for (int i = 0; i < NC; ++i) {
-          if (i * kWave >= (int)chunks) break;  // uniform
+      for (int i = 0; i < NC; ++i) {
+        if (i * kWave >= (int)chunks) break;  // uniform
+        uint32_t r, l;
+        if (kItemsInRegs) {
+          r = it.r2[i];
+          l = it.j2[i];
+        } else {
           const uint32_t v = lane + kWave * i;
-          const uint32_t r = v / dv, j = v - r * dv;
-          if (r < t[k].rows) {
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + r * a.lr + V * j);
-            const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
-            TO *out = reinterpret_cast<TO *>(a.out[t[k].side]) + ((int64_t)t[k].bh * a.ctx + t[k].pos0) * a.d;
-            dequant_store<TO>(out + (int64_t)r * a.d + V * j, nb, scale_all[wave][k][r], dead);
-          }
+          r = __umulhi(v, inv_dv);
+          l = r * a.lr + V * (v - r * dv);
         }
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + l);
+        const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
+        // output byte offset: (r d + V j) sizeof(TO), with V j = l - r lr
+        const uint32_t o = kItemsInRegs ? it.o2[i] : (r * a.d + l - r * a.lr) * (uint32_t)sizeof(TO);
+        tile_store(os, o, dq16<TO>(nb, scale_all[wave][k][r], dead));
       }
     }
     if (!more) break;
     wave_lds_sync();  // phase 2 reads done before the next phase 1 overwrites
   }
+#if KVECC_SHIM_WAVE_TIMES
+  if (lane == 0 && g_wave_times) {
+    g_wave_times[3 * gw] = t_start;
+    g_wave_times[3 * gw + 1] = __builtin_amdgcn_s_memrealtime();
+    g_wave_times[3 * gw + 2] = n_tiles;
+  }
+#endif
   if (STATS) {  // wave reduction, one atomic pair per wave
     bits = wave_sum(bits);
     unc = wave_sum(unc);
@@ -875,8 +932,10 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     const bool more = u < uend;
     if (more) fetch(u);
     // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
-    // wave-instruction stores 1 KiB contiguous ------------------------------------
-    TO *out = reinterpret_cast<TO *>(a.out[t.side]) + ((int64_t)t.bh * a.ctx + t.pos0) * a.d;
+    // wave-instruction stores 1 KiB contiguous (rows past the tile fall outside
+    // its output descriptor: dropped) -------------------------------------------
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
     // one straight-line body per case (a branch per item serialised its LDS reads)
     auto phase2 = [&](auto interp_c) {
       constexpr bool IP = decltype(interp_c)::value;
@@ -884,7 +943,6 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
       for (int i = 0; i < NI2; ++i) {
         if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
         const uint32_t r = i2r[i], c = i2c[i];
-        if (r >= t.rows) continue;
         const uint8_t *row = stage + off0 + r * a.d + V * c;
         uint32_t q[2] = {0u, 0u};
 #pragma unroll
@@ -898,7 +956,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
             q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
           }
         }
-        dequant_store<TO>(out + (int64_t)r * a.d + V * c, q, scale_all[wave][r], t.row0 < 0);
+        tile_store(os, (r * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
       }
     };
     if (INTERP && !KVECC_SHIM_INTERP_NOVALU && tile_dbl)
@@ -1176,6 +1234,8 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
     a.nlb = (uint32_t)cdiv(ctx, block_size);
     a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
     a.rowb = (uint32_t)(codec == KVECC_CODEC_GOLAY_PACKED ? KVECC_GOLAY_PACKED_ROW(g) : 4 * g);
+    a.dyn = shim_dyn_slot();
+    if (!a.dyn) return KVECC_EHIP;
     const bool pk = codec == KVECC_CODEC_GOLAY_PACKED;
     switch (out_dtype) {
       case KVECC_F32: launch_read_tiles<float>(pk, a, st); break;

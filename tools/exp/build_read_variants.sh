@@ -13,15 +13,13 @@ build() {  # name flags...
   local name=$1; shift
   $CC "$@" -o libread_$name.so $CSRC/shim.hip $CSRC/runtime.hip &
 }
-# (both kernels use at most 128 VGPRs: 16 waves per CU at most)
-# block 512: Golay 2 WG/CU (16 waves) with pad 8192; bytes 2 WG/CU with pad 40960
-for c in 1 2 4 8; do
-  build c${c}b512w16 -DKVECC_SHIM_TILE_CHUNK=$c -DKVECC_SHIM_TILE_LDS_PAD=8192 -DKVECC_SHIM_BYTES_LDS_PAD=40960
+# dynamic tile schedule: off, and DYN_STATIC static tiles per wave before the
+# counters; 2 or 3 workgroups per CU (VGPRs allow 3 since the packed dequantization)
+build nodyn -DKVECC_SHIM_TILE_DYN=0
+build nodyn_cu3 -DKVECC_SHIM_TILE_DYN=0 -DKVECC_SHIM_TILE_PER_CU=3
+for st in 8 16 24; do
+  build dyn$st -DKVECC_SHIM_TILE_DYN_STATIC=$st
 done
-# block 1024: 1 WG/CU (16 waves): Golay pad 12288, bytes pad 45056
-for c in 1 2 4; do
-  build c${c}b1024w16 -DKVECC_SHIM_TILE_BLOCK=1024 -DKVECC_SHIM_TILE_CHUNK=$c -DKVECC_SHIM_TILE_LDS_PAD=12288 \
-    -DKVECC_SHIM_BYTES_LDS_PAD=45056
-done
+build dyn16_cu3 -DKVECC_SHIM_TILE_DYN_STATIC=16 -DKVECC_SHIM_TILE_PER_CU=3
 wait
 ls -la libread_*.so
