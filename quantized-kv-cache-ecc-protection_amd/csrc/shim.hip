@@ -1205,7 +1205,8 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
   hipStream_t st = as_stream(stream);
   const int64_t g = golay ? (d + 2) / 3 : d;
   const int64_t gpr = cdiv(g, 4), lr = 12 * gpr;
-  if (golay && d % 8 == 0 && lr <= kTileStage && 2 * batch * hkv * cdiv(ctx, block_size) * block_size <= 0x7FFFFFFFLL) {
+  if (golay && d % 8 == 0 && lr <= kTileStage && aligned(k_out, 16) && aligned(v_out, 16) &&
+      2 * batch * hkv * cdiv(ctx, block_size) * block_size <= 0x7FFFFFFFLL) {
     // Golay: the wave-tile kernel, all sequences in one launch
     ShimTileArgs a;
     a.cache[0] = k_cache;

@@ -575,6 +575,8 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
                          k_scales.to(torch.float32).contiguous(),
                          v_scales.to(torch.float32).contiguous(), out, layer_idx, block_size,
                          sm_scale, codec)
+    if codec == "hamming84" and use_tiled and block_size >= block_m:
+        tiled_empty_to_zero(out, block_table, context_lens, block_size)
     return out
 
 
@@ -582,7 +584,7 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
 # Packed Golay storage (host twins of ops.golay_encode_packed / decode_packed)
 # ============================================================================
 
-from .ops import pack_nibbles, unpack_nibbles  # noqa: E402  (pure torch, device-agnostic)
+from .ops import pack_nibbles, tiled_empty_to_zero, unpack_nibbles  # noqa: E402  (pure torch)
 
 
 def golay_encode_packed(nibbles: torch.Tensor, m: int) -> torch.Tensor:

@@ -830,9 +830,12 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
     [B, max_blocks] int32; context_lens [B] int32.  -> [B, H, D] in query's
     dtype.  As in the reference: v_scales defaults to k_scales; the "golay"
     codec reproduces reference_attention_ecc (:783-909), which dequantizes K
-    and V with k_scales and returns fp32.  syndrome_table / use_tiled / block_m
-    are accepted for signature compatibility (the table lives on the device,
-    the kernel's geometry is fixed).
+    and V with k_scales and returns fp32.  syndrome_table is accepted for
+    signature compatibility (the table lives on the device).  use_tiled with
+    block_size >= block_m selects the reference's tiled kernel (:430-617, :693):
+    the same attention (one split kernel computes both), except that a context
+    with no valid token gives 0 there instead of the default kernel's -8.0
+    (tiled_empty_to_zero).
     """
     _check_gpu(query, "Query")
     if codec not in ("hamming84", "golay"):
@@ -860,7 +863,20 @@ def paged_attention_ecc(query, k_cache, v_cache, block_table, context_lens, k_sc
                          _conform(block_table, torch.int32), _conform(context_lens, torch.int32),
                          _conform(k_scales, torch.float32), _conform(v_scales, torch.float32),
                          out, layer_idx, block_size, sm_scale, codec)
+    if codec == "hamming84" and use_tiled and block_size >= block_m:
+        tiled_empty_to_zero(out, block_table, context_lens, block_size)
     return out
+
+
+def tiled_empty_to_zero(out, block_table, context_lens, block_size):
+    """The reference's tiled H84 kernel ends with ``l_i > 0 ? acc / l_i : 0``
+    (attention_ecc.py:614): a sequence with no valid token -- no block j with
+    j * block_size < context_len and block_table[b, j] >= 0 (:497-510) -- is 0,
+    where the default kernel's masked rows give -8.0.  In place on `out`."""
+    nb = block_table.shape[1]
+    start = torch.arange(nb, device=block_table.device, dtype=torch.int64) * block_size
+    valid = (start[None, :] < context_lens.to(torch.int64)[:, None]) & (block_table >= 0)
+    out.masked_fill_(~valid.any(dim=1)[:, None, None], 0.0)
 
 
 # ============================================================================

@@ -204,7 +204,9 @@ def _fixture(golden, manifest, name):
 
 
 FIXTURES = ["h84_basic", "h84_empty", "h84_holes", "h84_all_missing", "h84_d100",
-            "h84_vscales_none", "h84_fp16", "golay_basic", "golay_empty_holes", "golay_d100"]
+            "h84_vscales_none", "h84_fp16", "golay_basic", "golay_empty_holes", "golay_d100",
+            # use_tiled=True: the reference's tiled kernel (empty contexts give 0)
+            "h84_tiled_empty", "h84_tiled_holes", "h84_tiled_all_missing", "h84_tiled_small_block"]
 
 
 def test_fixture_inventory(manifest):
@@ -216,7 +218,9 @@ def _run_fixture(mod, meta, arr, dev=None):
     return mod.paged_attention_ecc(t(arr["q"]), t(arr["k_cache"]), t(arr["v_cache"]),
                                    t(arr["block_table"]), t(arr["context_lens"]), t(arr["k_scales"]),
                                    meta["layer"], meta["block_size"], codec=meta["codec"],
-                                   v_scales=t(arr["v_scales"]) if meta["v_scales"] else None).cpu()
+                                   v_scales=t(arr["v_scales"]) if meta["v_scales"] else None,
+                                   use_tiled=meta.get("use_tiled", False),
+                                   block_m=meta.get("block_m", 4)).cpu()
 
 
 def _assert_fixture(got, meta, arr):

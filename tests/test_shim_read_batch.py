@@ -336,3 +336,23 @@ def test_hip_batch_read_full_size(gpu, codec):
     assert torch.equal(k.cpu(), ek)
     assert torch.equal(v.cpu(), ev)
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["golay", "golay_packed"])
+def test_hip_golay_read_unaligned_out(gpu, codec):
+    """Outputs that start off a 16-byte boundary leave the wave-tile kernel
+    (16-byte buffer stores) for the per-sequence kernel: same values."""
+    from kvecc import cpu_ops, ops
+    batch, ctx, hkv, d, bs = 2, 40, 2, 64, 16
+    kc, vc, ks, vs, table = make_cache(codec, batch, ctx, hkv, d, bs, seed=12)
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, 1, codec, torch.float16, stats=st)
+    n = batch * hkv * ctx * d
+    bufs = [torch.empty(n + 1, dtype=torch.float16, device=gpu) for _ in range(2)]
+    out = tuple(b[1:].view(batch, hkv, ctx, d) for b in bufs)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, 1, codec, torch.float16,
+                               stats=gst, out=out)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)

@@ -318,6 +318,21 @@ def gen_attention(manifest):
          "f32", True),
         ("golay_d100", "golay", 1, 2, 100, 1, 0, 4, 4, [[1, 3, 0]], [12], "f32", True),
     ]
+    # use_tiled=True (:430-617, taken when block_size >= block_m, :693): the
+    # tiled kernel masks the normaliser with token_valid and returns 0 for a
+    # context with no valid token, where the default kernel gives -8.0.
+    # (Appended after the cases above, so their random inputs are unchanged.)
+    tiled = {"h84_tiled_empty": 4, "h84_tiled_holes": 4, "h84_tiled_all_missing": 2,
+             "h84_tiled_small_block": 4}
+    cases += [
+        ("h84_tiled_empty", "hamming84", 2, 2, 32, 1, 0, 4, 6, [[0, 1, -1, -1], [2, 3, -1, -1]], [0, 6],
+         "f32", True),
+        ("h84_tiled_holes", "hamming84", 2, 3, 32, 2, 0, 8, 8, [[-1, 3, 5, -1], [4, -1, 0, 2]], [30, 29],
+         "f32", True),
+        ("h84_tiled_all_missing", "hamming84", 1, 2, 16, 1, 0, 4, 3, [[-1, -1, -1]], [9], "f32", True),
+        # block_size 2 < block_m 4: the default kernel runs (empty -> -8.0)
+        ("h84_tiled_small_block", "hamming84", 2, 2, 16, 1, 0, 2, 4, [[-1, -1], [1, 3]], [3, 4], "f32", True),
+    ]
     for (name, codec, batch, heads, d, layers, layer, bs, nblocks, table, ctx, qdt,
          with_vs) in cases:
         per = d if codec == "hamming84" else (d + 2) // 3
@@ -337,13 +352,15 @@ def gen_attention(manifest):
         out = paged_attention_ecc(torch.from_numpy(q), torch.from_numpy(kc), torch.from_numpy(vc),
                                   torch.from_numpy(tab), torch.from_numpy(lens), torch.from_numpy(ks),
                                   layer, bs, codec=codec,
-                                  v_scales=torch.from_numpy(vs) if with_vs else None)
+                                  v_scales=torch.from_numpy(vs) if with_vs else None,
+                                  use_tiled=name in tiled, block_m=tiled.get(name, 4))
         for k, v in (("q", q), ("k_cache", kc), ("v_cache", vc), ("block_table", tab),
                      ("context_lens", lens), ("k_scales", ks), ("v_scales", vs),
                      ("out", out.numpy())):
             arrays[f"{name}_{k}"] = v
         params.append({"name": name, "codec": codec, "layer": layer, "block_size": bs,
-                       "v_scales": with_vs, "q_dtype": qdt, "out_dtype": str(out.dtype)})
+                       "v_scales": with_vs, "q_dtype": qdt, "out_dtype": str(out.dtype),
+                       "use_tiled": name in tiled, "block_m": tiled.get(name, 4)})
         print(f"    {name}: out {tuple(out.shape)} {out.dtype}, "
               f"range [{float(out.min()):.4f}, {float(out.max()):.4f}]")
     _save("attention", manifest, {"cases": params}, **arrays)
