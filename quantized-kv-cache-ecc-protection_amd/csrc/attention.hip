@@ -287,7 +287,12 @@ __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
 #define KVECC_ATTN_BOUNDS __launch_bounds__(kBlock)
 #endif
 
-template <typename T, int CODEC, int VEC, int W, bool BUF>
+// GQA (G > 1): workgroup (split, y) serves the G query heads hg*G .. hg*G+G-1
+// of batch b = y / (H/G), which share one cache head: each K and V row is
+// loaded and decoded once and used G times (a dot product, an online softmax
+// state and an accumulator per head), where one workgroup per query head read
+// and decoded every cache row H/Hkv times.
+template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1>
 __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
@@ -309,9 +314,9 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   __shared__ float gml[2][TP];             // per-group running max / sum
   __shared__ h84_lut_t lut[CODEC == KVECC_CODEC_H84 ? 256 : 1];  // H(8,4): codeword byte -> data - 8
 
-  const int64_t bh = blockIdx.y;
-  const int64_t b = bh / a.heads, h = bh % a.heads;
-  const int64_t hk = h / (a.heads / a.kv_heads);
+  const int64_t hgroups = a.heads / G;
+  const int64_t b = blockIdx.y / hgroups, h0 = (blockIdx.y % hgroups) * G;  // query heads h0 .. h0+G-1
+  const int64_t hk = h0 / (a.heads / a.kv_heads);
   const int grp = threadIdx.x / W, c = threadIdx.x % W;
   const int64_t ctx = min<int64_t>(a.ctx_lens[b], a.max_blocks * a.bs);  // table bound
   const int64_t t0 = (int64_t)blockIdx.x * a.split;
@@ -319,7 +324,8 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
   const bool live = c < (a.g + VEC - 1) / VEC;  // lanes past the row idle
   const int cs = live ? c : 0;
-  float *ws = a.ws + (bh * a.nsplit + blockIdx.x) * (a.d + 2);
+  const int64_t ws_stride = a.nsplit * (a.d + 2);  // per query head
+  float *ws0 = a.ws + ((b * a.heads + h0) * a.nsplit + blockIdx.x) * (a.d + 2);
 
   {  // block-table slice -> LDS (one load per logical block), then one 32-bit
      // division per token; none in the streaming loop
@@ -365,16 +371,20 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
     h84_decode4(threadIdx.x, q, t, n1, n2);
     lut[threadIdx.x] = (h84_lut_t)((int)(q & 0xFu) - 8);
   }
-  float qv[E];
+  float qv[G][E];
   const float qscale = a.sm_scale * kAttnLogScale;
-  float qsum = 0.0f;  // sum of this lane's q (folds the decode's kOffset out of the K sums)
+  float qsum[G];  // sum of this lane's q (folds the decode's kOffset out of the K sums)
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int64_t di = (int64_t)c * E + e;
-    qv[e] = (live && di < a.d)
-                ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h) * a.d + di]) * qscale
-                : 0.0f;
-    qsum += qv[e];
+  for (int j = 0; j < G; ++j) {
+    qsum[j] = 0.0f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t di = (int64_t)c * E + e;
+      qv[j][e] = (live && di < a.d)
+                     ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h0 + j) * a.d + di]) * qscale
+                     : 0.0f;
+      qsum[j] += qv[j][e];
+    }
   }
   __syncthreads();
 
@@ -388,10 +398,17 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   const __amdgpu_buffer_rsrc_t vsrs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v_scales), 0, (int)a.scale_bytes, kRsrcWord3);
   // ---- one pass: U K and V rows in flight per lane, online softmax per group
-  float m = -INFINITY, l = 0.0f, acc[E];
-  float psum = 0.0f;  // sum of p * v_scale, for the kOffset fold of the V sums
+  // (and per query head j of the workgroup)
+  float m[G], l[G], acc[G][E];
+  float psum[G];  // sum of p * v_scale, for the kOffset fold of the V sums
 #pragma unroll
-  for (int e = 0; e < E; ++e) acc[e] = 0.0f;
+  for (int j = 0; j < G; ++j) {
+    m[j] = -INFINITY;
+    l[j] = 0.0f;
+    psum[j] = 0.0f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[j][e] = 0.0f;
+  }
   for (int i0 = grp; i0 < ntok; i0 += TP * U) {
     C kc[U], vc[U];
     float ks[U], vs[U];
@@ -413,73 +430,104 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
         vs[u] = a.v_scales[row];
       }
     }
-    float sc[U];
-    float mn = m;
+    float sc[G][U];
+    float mn[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) mn[j] = m[j];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      float part = 0.0f;
+      float part[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) part[j] = 0.0f;
       if (live) {
         float kv[E];
         kc[u].decode(lut, gtab, kv);
-        part = dot<E>(qv, kv);
-        if (C::kOffset != 0.0f) part -= C::kOffset * qsum;
-        part *= ks[u];  // sum q (n - 8) s = s * sum q (n - 8)
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          part[j] = dot<E>(qv[j], kv);
+          if (C::kOffset != 0.0f) part[j] -= C::kOffset * qsum[j];
+          part[j] *= ks[u];  // sum q (n - 8) s = s * sum q (n - 8)
+        }
       }
-      part = group_sum<W>(part);
-      sc[u] = ok[u] ? part : -INFINITY;
-      mn = fmaxf(mn, sc[u]);
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        part[j] = group_sum<W>(part[j]);
+        sc[j][u] = ok[u] ? part[j] : -INFINITY;
+        mn[j] = fmaxf(mn[j], sc[j][u]);
+      }
     }
-    if (mn == -INFINITY) continue;  // no valid row yet (uniform per group)
-    const float alpha = attn_exp(m - mn);  // m = -inf -> 0
-    l *= alpha;
-    psum *= alpha;
+    bool any = false;
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] *= alpha;
+    for (int j = 0; j < G; ++j) any |= mn[j] != -INFINITY;
+    if (!any) continue;  // no valid row yet (uniform per group)
+    float ps[G][U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float p = attn_exp(sc[u] - mn);  // invalid rows: exp(-inf) = 0
-      l += p;
-      if (live) {
+    for (int j = 0; j < G; ++j) {
+      if (G > 1 && mn[j] == -INFINITY) {  // this head has no finite score yet: no update
+#pragma unroll
+        for (int u = 0; u < U; ++u) ps[j][u] = 0.0f;
+        continue;
+      }
+      const float alpha = attn_exp(m[j] - mn[j]);  // m = -inf -> 0
+      l[j] *= alpha;
+      psum[j] *= alpha;
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[j][e] *= alpha;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float p = attn_exp(sc[j][u] - mn[j]);  // invalid rows: exp(-inf) = 0
+        l[j] += p;
+        ps[j][u] = p * vs[u];
+        psum[j] += ps[j][u];
+      }
+      m[j] = mn[j];
+    }
+    if (live) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
         float vv[E];
         vc[u].decode(lut, gtab, vv);
-        const float ps = p * vs[u];
-        psum += ps;
-        axpy<E>(acc, ps, vv);
+#pragma unroll
+        for (int j = 0; j < G; ++j) axpy<E>(acc[j], ps[j][u], vv);
       }
     }
-    m = mn;
   }
 
-  // ---- merge the TP groups ------------------------------------------------------
+  // ---- merge the TP groups (one query head at a time) ------------------------------
   if (kSpread) __syncthreads();  // the tables (aliased by red) fully read
-  if (live) {
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-      red[(grp * W + c) * E + e] = C::kOffset != 0.0f ? acc[e] - C::kOffset * psum : acc[e];
-  }
-  if (c == 0) {
-    gml[0][grp] = m;
-    gml[1][grp] = l;
-  }
-  __syncthreads();
   __shared__ float gw[TP];  // e^(m_g - M) per group
-  float M = -INFINITY;
-  for (int gi = 0; gi < TP; ++gi) M = fmaxf(M, gml[0][gi]);
-  if (threadIdx.x < TP) {
-    const float mg = gml[0][threadIdx.x];
-    gw[threadIdx.x] = mg == -INFINITY ? 0.0f : attn_exp(mg - M);
-  }
-  __syncthreads();
-  for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
-    float sum = 0.0f;
-    for (int gi = 0; gi < TP; ++gi) sum += red[gi * W * E + di] * gw[gi];
-    ws[2 + di] = sum;
-  }
-  if (threadIdx.x == 0) {
-    float L = 0.0f;
-    for (int gi = 0; gi < TP; ++gi) L += gml[1][gi] * gw[gi];
-    ws[0] = M;
-    ws[1] = L;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    if (j > 0) __syncthreads();  // the previous head's merge fully read red / gml / gw
+    if (live) {
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        red[(grp * W + c) * E + e] = C::kOffset != 0.0f ? acc[j][e] - C::kOffset * psum[j] : acc[j][e];
+    }
+    if (c == 0) {
+      gml[0][grp] = m[j];
+      gml[1][grp] = l[j];
+    }
+    __syncthreads();
+    float M = -INFINITY;
+    for (int gi = 0; gi < TP; ++gi) M = fmaxf(M, gml[0][gi]);
+    if (threadIdx.x < TP) {
+      const float mg = gml[0][threadIdx.x];
+      gw[threadIdx.x] = mg == -INFINITY ? 0.0f : attn_exp(mg - M);
+    }
+    __syncthreads();
+    float *ws = ws0 + j * ws_stride;
+    for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
+      float sum = 0.0f;
+      for (int gi = 0; gi < TP; ++gi) sum += red[gi * W * E + di] * gw[gi];
+      ws[2 + di] = sum;
+    }
+    if (threadIdx.x == 0) {
+      float L = 0.0f;
+      for (int gi = 0; gi < TP; ++gi) L += gml[1][gi] * gw[gi];
+      ws[0] = M;
+      ws[1] = L;
+    }
   }
 }
 
@@ -536,7 +584,7 @@ static int launch_split_w(const AttnArgs &a, dim3 grid, hipStream_t st) {
   switch (w) {
 #define KVECC_ATTN_CASE(WW)                                                                       \
   case WW:                                                                                        \
-    KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, WW, BUF>), grid, dim3(kBlock), 0, st, a); \
+    KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, WW, BUF, 1>), grid, dim3(kBlock), 0, st, a); \
     return KVECC_OK;
     KVECC_ATTN_CASE(1)
     KVECC_ATTN_CASE(2)
@@ -558,21 +606,65 @@ static int launch_split(const AttnArgs &a, dim3 grid, hipStream_t st) {
                        : launch_split_w<T, CODEC, VEC, false>(a, grid, st);
 }
 
+// words per lane of a token row: the VEC the codec's kernels use at head_dim d
+// (the H(8,4) GQA kernels take 2 words = 8 codewords per lane: with G query
+// rows and accumulators per lane, 4 words took 188 VGPRs at G = 4)
+constexpr int kH84GqaVec = 2;
+static int attn_vec(int codec, int64_t d, bool gqa = false) {
+  if (codec == KVECC_CODEC_H84)
+    return gqa && d % 8 == 0 ? kH84GqaVec : d % (4 * kH84Vec) == 0 ? kH84Vec : d % 16 == 0 ? 4 : 1;
+  return codec == KVECC_CODEC_GOLAY ? kGolayVec : kGolayPackedVec;
+}
+
+// query heads per workgroup: the GQA kernels cover buffer-addressed caches with
+// lane groups of 8-32 lanes per row (head_dim 64-256) and G in {2, 4} dividing
+// H / Hkv (G 8 would hold 8 query rows and accumulators per lane); else 1
+#ifndef KVECC_ATTN_GQA
+#define KVECC_ATTN_GQA 1
+#endif
+static int attn_heads_per_wg(int codec, int64_t d, int64_t g, int64_t heads, int64_t kv_heads, bool buf) {
+  const int64_t group = heads / kv_heads;
+  const int vec = attn_vec(codec, d, true);
+  const int w = pow2_at_least((g + vec - 1) / vec);
+  if (!KVECC_ATTN_GQA || !buf || w < 8 || w > 32 || (codec == KVECC_CODEC_H84 && d % 8 != 0)) return 1;
+  const int gmax = codec == KVECC_CODEC_GOLAY_PACKED ? 2 : 4;  // packed: 4 codewords per lane
+  return group % 4 == 0 && gmax >= 4 ? 4 : group % 2 == 0 ? 2 : 1;
+}
+
+template <typename T, int CODEC, int VEC, int G>
+static int launch_split_gqa(const AttnArgs &a, dim3 grid, hipStream_t st) {
+  switch (pow2_at_least((a.g + VEC - 1) / VEC)) {
+    case 8: KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, 8, true, G>), grid, dim3(kBlock), 0, st, a); break;
+    case 16: KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, 16, true, G>), grid, dim3(kBlock), 0, st, a); break;
+    default: KVECC_LAUNCH((paged_attn_split_kernel<T, CODEC, VEC, 32, true, G>), grid, dim3(kBlock), 0, st, a); break;
+  }
+  return KVECC_OK;
+}
+
+template <typename T, int CODEC, int VEC>
+static int launch_split_g(const AttnArgs &a, int64_t batch, int gq, hipStream_t st) {
+  dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads / gq));
+  if (gq == 1) return launch_split<T, CODEC, VEC>(a, grid, st);
+  constexpr int GV = CODEC == KVECC_CODEC_H84 ? kH84GqaVec : VEC;
+  if constexpr (CODEC != KVECC_CODEC_GOLAY_PACKED)
+    if (gq == 4) return launch_split_gqa<T, CODEC, GV, 4>(a, grid, st);
+  return launch_split_gqa<T, CODEC, GV, 2>(a, grid, st);
+}
+
 template <typename T, int CODEC>
-static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
-  dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads));
+static int launch_attn(const AttnArgs &a, int64_t batch, int gq, hipStream_t st) {
   int rc;
   if constexpr (CODEC == KVECC_CODEC_H84) {
     if (a.d % (4 * kH84Vec) == 0)
-      rc = launch_split<T, CODEC, kH84Vec>(a, grid, st);  // 16-byte loads, 16 codewords per lane
+      rc = launch_split_g<T, CODEC, kH84Vec>(a, batch, gq, st);  // 16-byte loads, 16 codewords per lane
     else if (a.d % 16 == 0)
-      rc = launch_split<T, CODEC, 4>(a, grid, st);
+      rc = launch_split_g<T, CODEC, 4>(a, batch, gq, st);
     else
-      rc = launch_split<T, CODEC, 1>(a, grid, st);
+      rc = launch_split_g<T, CODEC, 1>(a, batch, gq, st);
   } else if constexpr (CODEC == KVECC_CODEC_GOLAY) {
-    rc = launch_split<T, CODEC, kGolayVec>(a, grid, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
+    rc = launch_split_g<T, CODEC, kGolayVec>(a, batch, gq, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
   } else {
-    rc = launch_split<T, CODEC, kGolayPackedVec>(a, grid, st);  // 4 codewords per lane: 43 -> 11 of 16
+    rc = launch_split_g<T, CODEC, kGolayPackedVec>(a, batch, gq, st);  // 4 codewords per lane: 43 -> 11 of 16
   }
   if (rc != KVECC_OK) return rc;
   KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
@@ -580,11 +672,11 @@ static int launch_attn(const AttnArgs &a, int64_t batch, hipStream_t st) {
 }
 
 template <typename T>
-static int launch_codec(int codec, const AttnArgs &a, int64_t batch, hipStream_t st) {
+static int launch_codec(int codec, const AttnArgs &a, int64_t batch, int gq, hipStream_t st) {
   switch (codec) {
-    case KVECC_CODEC_H84: return launch_attn<T, KVECC_CODEC_H84>(a, batch, st);
-    case KVECC_CODEC_GOLAY: return launch_attn<T, KVECC_CODEC_GOLAY>(a, batch, st);
-    default: return launch_attn<T, KVECC_CODEC_GOLAY_PACKED>(a, batch, st);
+    case KVECC_CODEC_H84: return launch_attn<T, KVECC_CODEC_H84>(a, batch, gq, st);
+    case KVECC_CODEC_GOLAY: return launch_attn<T, KVECC_CODEC_GOLAY>(a, batch, gq, st);
+    default: return launch_attn<T, KVECC_CODEC_GOLAY_PACKED>(a, batch, gq, st);
   }
 }
 
@@ -614,8 +706,10 @@ extern "C" {
 KVECC_API int64_t kvecc_paged_attention_workspace(int64_t batch, int64_t heads, int64_t head_dim,
                                                   int64_t max_context_len) {
   if (batch <= 0 || heads <= 0 || head_dim <= 0 || max_context_len <= 0) return 0;
-  return batch * heads * cdiv(max_context_len, choose_split(batch * heads, max_context_len)) *
-         (head_dim + 2);
+  // the GQA kernels split finer (their grid has H/G workgroups per split):
+  // room for the finest, G = 4 (choose_split is monotone in its first argument)
+  const int64_t bh = std::max<int64_t>(1, batch * heads / 4);
+  return batch * heads * cdiv(max_context_len, choose_split(bh, max_context_len)) * (head_dim + 2);
 }
 
 KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *k_cache,
@@ -670,12 +764,9 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.layer = layer;
   a.bs = block_size;
   a.max_blocks = max_blocks;
-  a.split = choose_split(batch * heads, max_context_len);
-  a.nsplit = cdiv(max_context_len, a.split);
-  if (a.nsplit > kMaxSplits)
-    return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
   a.sm_scale = sm_scale;
   a.empty_value = codec == KVECC_CODEC_H84 ? -8.0f : 0.0f;
+  int gq = 1;
   {
     const int64_t rows_total = num_blocks * num_layers * kv_heads * block_size;
     const int64_t cb = rows_total * (codec == KVECC_CODEC_H84            ? head_dim
@@ -684,7 +775,12 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     const bool fits = cb <= 0xFFFFFFFFLL && rows_total * 4 <= 0xFFFFFFFFLL;
     a.cache_bytes = fits ? (uint32_t)cb : 0u;  // 0 selects the 64-bit-addressed kernels
     a.scale_bytes = fits ? (uint32_t)(rows_total * 4) : 0u;
+    gq = attn_heads_per_wg(codec, head_dim, a.g, heads, kv_heads, fits);
   }
+  a.split = choose_split(batch * heads / gq, max_context_len);
+  a.nsplit = cdiv(max_context_len, a.split);
+  if (a.nsplit > kMaxSplits)
+    return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
   a.par = a.cor = nullptr;
   a.atab = nullptr;
   if (codec != KVECC_CODEC_H84) {
@@ -696,9 +792,9 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   hipStream_t st = as_stream(stream);
   int rc;
   switch (q_dtype) {
-    case KVECC_F32: rc = launch_codec<float>(codec, a, batch, st); break;
-    case KVECC_F16: rc = launch_codec<__half>(codec, a, batch, st); break;
-    case KVECC_BF16: rc = launch_codec<__hip_bfloat16>(codec, a, batch, st); break;
+    case KVECC_F32: rc = launch_codec<float>(codec, a, batch, gq, st); break;
+    case KVECC_F16: rc = launch_codec<__half>(codec, a, batch, gq, st); break;
+    case KVECC_BF16: rc = launch_codec<__hip_bfloat16>(codec, a, batch, gq, st); break;
     default: return set_error(KVECC_EINVAL, "paged_attention: bad dtype %d", q_dtype);
   }
   if (rc != KVECC_OK) return rc;
