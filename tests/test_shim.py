@@ -382,3 +382,34 @@ def test_golay_packed_storage_hip_equals_cpu(gpu):
         for i in range(6):
             assert torch.equal(hip[i], cpu[i]), (d, i)
         assert hip[6] == cpu[6] and hip[6][0] > 0, d
+
+
+@pytest.mark.gpu
+def test_config4_full_size_hip_equals_cpu_backend(gpu):
+    """BASELINE config 4 at its size: random-init GPT-2 (12 layers, 12 heads,
+    768 hidden) over seq_len 1024 inside patch_model_with_ecc_attention,
+    Hamming(8,4) + interpolation, BER 1e-3 (ecc_shim.py:1396-1481, stats
+    :1627-1642).  fp32 model on both backends with one scale rule, so both
+    write the same cache bytes: get_ecc_stats must be equal and the logits
+    agree to fp32 matmul rounding (GPU vs host GEMMs)."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+    from kvecc.ecc_shim import ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention, reset_ecc_cache
+    torch.manual_seed(0)
+    cpu_model = GPT2LMHeadModel(GPT2Config(n_positions=1024)).eval()
+    gpu_model = GPT2LMHeadModel(GPT2Config(n_positions=1024)).eval()
+    gpu_model.load_state_dict(cpu_model.state_dict())
+    gpu_model = gpu_model.to(gpu)
+    ids = torch.randint(0, 50257, (1, 1024), generator=torch.Generator().manual_seed(0))
+    res = {}
+    for backend, model, dev in (("hip", gpu_model, gpu), ("cpu", cpu_model, torch.device("cpu"))):
+        cfg = ECCShimConfig(codec="hamming84", ber=1e-3, inject_errors=True, seed=42, block_size=16,
+                            use_interpolation=True, backend=backend, scale_rule="div7")
+        with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=64):
+            reset_ecc_cache(model)
+            out = model(ids.to(dev), labels=ids.to(dev))
+            res[backend] = (out.logits.float().cpu(), float(out.loss), get_ecc_stats(model))
+    (lh, loss_h, st_h), (lc, loss_c, st_c) = res["hip"], res["cpu"]
+    assert st_h == st_c, (st_h, st_c)
+    assert st_h["errors_corrected"] > 0 and st_h["errors_detected"] > 0
+    assert torch.allclose(lh, lc, rtol=1e-3, atol=1e-3), float((lh - lc).abs().max())
+    assert abs(loss_h - loss_c) < 1e-3 * max(1.0, abs(loss_c))
