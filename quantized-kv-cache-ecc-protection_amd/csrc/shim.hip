@@ -294,20 +294,28 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 #ifndef KVECC_SHIM_BYTES_LDS_PAD
 #define KVECC_SHIM_BYTES_LDS_PAD KVECC_SHIM_TILE_LDS_PAD
 #endif
-// DYN (CHUNK 0): a wave takes its first DYN_STATIC tiles w, w + nwaves, ...
-// statically and the rest from work counters (kDynCounters per launch, counter
-// c handing out tiles base + k kDynCounters + c in turn), one atomic per tile,
-// issued a tile ahead.  With equal static shares the waves of one launch
-// finished 119-166 us apart at [8,4096,32,128] (mean 143 us;
-// tools/exp/run_wave_times.py): memory latency is not even across the chip.
+// DYN (CHUNK 0): a wave takes the first DYN_STATIC_PCT % of its even share of
+// tiles statically (w, w + nwaves, ...) and the rest from work counters
+// (kDynCounters per launch, counter c handing out tiles base + k kDynCounters
+// + c in turn), one atomic per tile, issued a tile ahead.  With equal static
+// shares the waves of one launch finished 119-166 us apart at
+// [8,4096,32,128] (mean 143 us; tools/exp/run_wave_times.py): memory latency
+// is not even across the chip.  Tiles handed out dynamically go to whichever
+// CU asks, which costs locality (a static order with the waves scrambled over
+// the tiles of each round ran 8 % slower), so the dynamic part is the tail:
+// 25 % of the tiles measured 150.9 us against 169.9 static and 160-161 with
+// 50 or 75 % dynamic (Golay int32 -> fp16; profiles/r03/fused/).
 #ifndef KVECC_SHIM_TILE_DYN
-#define KVECC_SHIM_TILE_DYN 0
+#define KVECC_SHIM_TILE_DYN 1
+#endif
+#ifndef KVECC_SHIM_BYTES_DYN
+#define KVECC_SHIM_BYTES_DYN KVECC_SHIM_TILE_DYN
 #endif
 #ifndef KVECC_SHIM_DYN_PROBE
 #define KVECC_SHIM_DYN_PROBE 0
 #endif
-#ifndef KVECC_SHIM_TILE_DYN_STATIC
-#define KVECC_SHIM_TILE_DYN_STATIC 8
+#ifndef KVECC_SHIM_TILE_DYN_STATIC_PCT
+#define KVECC_SHIM_TILE_DYN_STATIC_PCT 75
 #endif
 constexpr int kTileBlock = KVECC_SHIM_TILE_BLOCK;  // 8 waves per workgroup
 constexpr int kTileTPI = KVECC_SHIM_TILE_TPI;      // tiles in flight per wave
@@ -344,7 +352,7 @@ struct ShimTileArgs {
 // counter shared by all waves instead serialised their exits: ~40 us.)
 template <bool DYN>
 struct TileSchedule {
-  uint32_t gw, nwaves, units, cidx, sidx, gk, last_k;
+  uint32_t gw, nwaves, units, cidx, sidx, gk, last_k, nstatic;
   uint32_t *ctr;
   // a bijection of [0, nwaves) for power-of-two nwaves (probe 3 only)
   __device__ __forceinline__ uint32_t perm(uint32_t w) const { return (w * 2654435761u) & (nwaves - 1); }
@@ -364,10 +372,12 @@ struct TileSchedule {
     nwaves = nwaves_;
     units = a.units;
     sidx = 1;
+    // static tiles per wave: DYN_STATIC_PCT % of the even share, at least 1
+    nstatic = max(1u, (uint32_t)(KVECC_SHIM_TILE_DYN_STATIC_PCT * ((units + nwaves - 1) / nwaves) / 100));
     if (DYN || KVECC_SHIM_DYN_PROBE) {
       cidx = gw % kDynCounters;
       ctr = a.dyn + kDynStride * cidx;
-      const uint32_t base = KVECC_SHIM_TILE_DYN_STATIC * nwaves;
+      const uint32_t base = nstatic * nwaves;
       const uint32_t kc = units > base + cidx ? (units - base - cidx + kDynCounters - 1) / kDynCounters : 0u;
       const uint32_t active = min(nwaves, units);  // waves with a first tile (gw < active)
       const uint32_t wc = (active - cidx + kDynCounters - 1) / kDynCounters;  // >= 1: this wave
@@ -387,7 +397,7 @@ struct TileSchedule {
       return r * nwaves + perm(gw);
     }
 #endif
-    constexpr uint32_t S = KVECC_SHIM_TILE_DYN_STATIC;
+    const uint32_t S = nstatic;
     if (sidx < S) {
       const uint32_t t = gw + sidx * nwaves;
       ++sidx;
@@ -401,6 +411,61 @@ struct TileSchedule {
     else if (k == last_k && lane == 0)  // the counter's last user
       __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return t;
+  }
+};
+
+// KVECC_SHIM_TILE_DYN == 2 (experiment): the schedule at workgroup granularity.
+// Group g is the kTileWaves consecutive tiles g kTileWaves + wave; the
+// workgroup takes its first DYN_STATIC_PCT % of groups statically (blockIdx,
+// blockIdx + nwg, ...) and the rest from the counters, wave 0 grabbing one
+// group ahead and handing it to the other waves through LDS at a workgroup
+// barrier per tile.  Counter c serves workgroups blockIdx = c (mod
+// kDynCounters); its last user resets it, as in TileSchedule.
+struct WgSchedule {
+  uint32_t ngroups, nwg, sidx, nstatic, cidx, gk, last_k, it, base;
+  uint32_t *ctr;
+  __device__ __forceinline__ uint32_t grab(uint32_t lane) {
+    uint32_t z;
+    asm("v_mov_b32 %0, 0" : "=v"(z));
+    uint32_t k = 0;
+    if (lane == 0) k = __hip_atomic_fetch_add(ctr + z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return k;
+  }
+  __device__ __forceinline__ void init(const ShimTileArgs &a, uint32_t wave, uint32_t lane) {
+    ngroups = (a.units + kTileWaves - 1) / kTileWaves;
+    nwg = gridDim.x;
+    sidx = 1;
+    it = 0;
+    nstatic = max(1u, (uint32_t)(KVECC_SHIM_TILE_DYN_STATIC_PCT * ((ngroups + nwg - 1) / nwg) / 100));
+    base = nstatic * nwg;
+    cidx = blockIdx.x % kDynCounters;
+    ctr = a.dyn + kDynStride * cidx;
+    const uint32_t kc = ngroups > base + cidx ? (ngroups - base - cidx + kDynCounters - 1) / kDynCounters : 0u;
+    const uint32_t active = min(nwg, ngroups);
+    const uint32_t wc = (active - cidx + kDynCounters - 1) / kDynCounters;
+    last_k = kc + wc - 1;
+    if (wave == 0) gk = grab(lane);
+  }
+  // the workgroup's next group (>= ngroups: none); every wave calls it
+  __device__ __forceinline__ uint32_t next(uint32_t *slot, uint32_t wave, uint32_t lane) {
+    if (sidx < nstatic) {
+      const uint32_t g = blockIdx.x + sidx * nwg;
+      ++sidx;
+      if (g < ngroups) return g;
+      sidx = nstatic;
+    }
+    ++it;
+    if (wave == 0) {
+      const uint32_t k = __builtin_amdgcn_readfirstlane(gk);
+      const uint32_t g = base + k * kDynCounters + cidx;
+      if (g < ngroups)
+        gk = grab(lane);
+      else if (k == last_k && lane == 0)
+        __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) slot[it & 1] = g;
+    }
+    __syncthreads();  // slot[it & 1] written; slot[(it + 1) & 1] is not rewritten before the next barrier
+    return __builtin_amdgcn_readfirstlane(slot[it & 1]);
   }
 };
 
@@ -615,14 +680,21 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   // kTileTPI tiles per iteration: u, u + ustep, ...; all their loads in flight
   constexpr uint32_t kChunk = KVECC_SHIM_TILE_CHUNK;
   static_assert(kChunk == 0 || kTileTPI == 1, "chunked tiles take one tile per iteration");
-  constexpr bool kDyn = KVECC_SHIM_TILE_DYN && kChunk == 0 && kTileTPI == 1;
+  constexpr bool kDyn = KVECC_SHIM_TILE_DYN == 1 && kChunk == 0 && kTileTPI == 1;
+  constexpr bool kWgDyn = KVECC_SHIM_TILE_DYN == 2 && kChunk == 0 && kTileTPI == 1;
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
   uint32_t u = kChunk ? gw * kChunk : gw;
   const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
   const uint32_t ustep = kChunk ? 1u : nwaves;
-  if (u >= uend) return;  // no workgroup barrier below: waves retire independently
+  // (no workgroup barrier below except WgSchedule's: waves retire independently)
+  if (!kWgDyn && u >= uend) return;
   TileSchedule<kDyn> sched;
-  sched.init(a, gw, nwaves, lane);
+  WgSchedule wsched;
+  __shared__ uint32_t wg_slot[2];
+  if (kWgDyn)
+    wsched.init(a, wave, lane);
+  else
+    sched.init(a, gw, nwaves, lane);
 #if KVECC_SHIM_DYN_PROBE == 3
   u = sched.perm(gw);
 #endif
@@ -701,9 +773,17 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 #if KVECC_SHIM_WAVE_TIMES
     ++n_tiles;
 #endif
-    u = kDyn ? sched.next(u, lane) : u + kTileTPI * ustep;
-    const bool more = u < uend;
-    if (more) fetch(u);
+    bool more;
+    if (kWgDyn) {
+      const uint32_t g = wsched.next(wg_slot, wave, lane);
+      more = g < wsched.ngroups;  // uniform over the workgroup
+      u = g * kTileWaves + wave;
+      if (more) fetch(u);  // valid[] = u < units: a wave past the last tile idles, keeps the barriers
+    } else {
+      u = kDyn ? sched.next(u, lane) : u + kTileTPI * ustep;
+      more = u < uend;
+      if (more) fetch(u);
+    }
     // ---- phase 2: dequantize VPL values per lane, one 16-byte store each -------
     // (stores of rows past the tile fall outside its output descriptor: dropped)
 #pragma unroll
@@ -816,11 +896,14 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
   }
   uint32_t n1 = 0, n2 = 0;
   constexpr uint32_t kChunk = KVECC_SHIM_BYTES_CHUNK;
+  constexpr bool kDyn = KVECC_SHIM_BYTES_DYN && kChunk == 0;
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
   uint32_t u = kChunk ? gw * kChunk : gw;
   const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
   const uint32_t ustep = kChunk ? 1u : nwaves;
   if (u >= uend) return;
+  TileSchedule<kDyn> sched;
+  sched.init(a, gw, nwaves, lane);
 
   ShimTile cur;
   u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
@@ -928,7 +1011,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     }
     wave_lds_sync();
     const ShimTile t = cur;
-    u += ustep;
+    u = kDyn ? sched.next(u, lane) : u + ustep;
     const bool more = u < uend;
     if (more) fetch(u);
     // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
@@ -1271,6 +1354,8 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
       a.tpb = (uint32_t)cdiv(block_size, a.tr);
       a.nlb = (uint32_t)cdiv(ctx, block_size);
       a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+      a.dyn = shim_dyn_slot();
+      if (!a.dyn) return KVECC_EHIP;
       switch (out_dtype) {
         case KVECC_F32: launch_bytes_tiles<float>(codec, interp, a, st); break;
         case KVECC_F16: launch_bytes_tiles<__half>(codec, interp, a, st); break;

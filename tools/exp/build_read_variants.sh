@@ -13,13 +13,12 @@ build() {  # name flags...
   local name=$1; shift
   $CC "$@" -o libread_$name.so $CSRC/shim.hip $CSRC/runtime.hip &
 }
-# dynamic tile schedule: off, and DYN_STATIC static tiles per wave before the
-# counters; 2 or 3 workgroups per CU (VGPRs allow 3 since the packed dequantization)
+# dynamic tile schedule: off; per wave (DYN 1, the product) at 65 %;
+# per workgroup (DYN 2) at 50 / 75 / 90 % static
 build nodyn -DKVECC_SHIM_TILE_DYN=0
-build nodyn_cu3 -DKVECC_SHIM_TILE_DYN=0 -DKVECC_SHIM_TILE_PER_CU=3
-for st in 8 16 24; do
-  build dyn$st -DKVECC_SHIM_TILE_DYN_STATIC=$st
+build pct65 -DKVECC_SHIM_TILE_DYN_STATIC_PCT=65
+for p in 50 75 90; do
+  build wg$p -DKVECC_SHIM_TILE_DYN=2 -DKVECC_SHIM_BYTES_DYN=1 -DKVECC_SHIM_TILE_DYN_STATIC_PCT=$p
 done
-build dyn16_cu3 -DKVECC_SHIM_TILE_DYN_STATIC=16 -DKVECC_SHIM_TILE_PER_CU=3
 wait
 ls -la libread_*.so

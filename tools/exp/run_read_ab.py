@@ -86,8 +86,10 @@ def main():
             per, inb = D, D
         bs = caches[0].shape[-1] // per
         cid = ops.SHIM_CODECS[codec]
-        outs = [(torch.empty(B, H, L, D, dtype=ODT, device=dev), torch.empty(B, H, L, D, dtype=ODT, device=dev))
-                for _ in handles]
+        # one output pair for every library: where the outputs sit in HBM
+        # relative to the caches moved a library's time by up to 6 %
+        shared = (torch.empty(B, H, L, D, dtype=ODT, device=dev), torch.empty(B, H, L, D, dtype=ODT, device=dev))
+        outs = [shared for _ in handles]
         stats = [ops.new_stats(dev) for _ in handles]
 
         def call(i, ev=None):
@@ -104,14 +106,17 @@ def main():
                 call(i)
         for s in stats:
             s.zero_()
+        ok, ref = [], None
         for i in range(len(handles)):
+            shared[0].fill_(float("nan"))
+            shared[1].fill_(float("nan"))
             call(i)
-        torch.cuda.synchronize()
-        ref = outs[0]
-        ok = []
-        for i in range(len(handles)):
-            ok.append(torch.equal(outs[i][0], ref[0]) and torch.equal(outs[i][1], ref[1])
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = (shared[0].clone(), shared[1].clone())
+            ok.append(torch.equal(shared[0], ref[0]) and torch.equal(shared[1], ref[1])
                       and ops.read_stats(stats[i]) == ops.read_stats(stats[0]))
+        del ref
         times = [[] for _ in handles]
         for r in range(ROUNDS):
             for i in range(len(handles)):
