@@ -180,6 +180,11 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_kernel(
 #ifndef KVECC_PACKED_DEC_STAGED
 #define KVECC_PACKED_DEC_STAGED 1
 #endif
+// workgroups per CU of the decode grid (a cap: smaller grids loop over tiles,
+// staging the 16 KiB of tables once per workgroup instead of once per tile)
+#ifndef KVECC_PACKED_DEC_PER_CU
+#define KVECC_PACKED_DEC_PER_CU 32
+#endif
 constexpr int kPkWaveBytes = kPkWaveCw * 3;  // 3072
 template <bool WITH_FLAGS, bool WITH_STATS>
 __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
@@ -419,7 +424,7 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
   if (KVECC_PACKED_DEC_STAGED && aligned(nibbles, 4) && aligned(codewords, 16)) {
     const int64_t ntiles = m / kPkTile;
     if (ntiles > 0) {
-      const dim3 grid(grid_for(ntiles, 1, 32)), block(kPkBlock);
+      const dim3 grid(grid_for(ntiles, 1, KVECC_PACKED_DEC_PER_CU)), block(kPkBlock);
       const uint32_t *c = reinterpret_cast<const uint32_t *>(codewords);
       uint32_t *n = reinterpret_cast<uint32_t *>(nibbles);
       if (uncorrectable && stats)

@@ -9,7 +9,8 @@
 plus the extended kernels (packed Golay, paged attention, shim write/read).
 Config 4 (GPT-2 forward) is tools/bench_shim.py.
 
-Kernel times are HIP events around `reps` back-to-back launches of one kernel
+Kernel times are HIP events around `reps` back-to-back launches of one kernel,
+after 100 untimed calls (a cold GPU reads 10-15 % high until its clocks ramp)
 (inputs resident in HBM, statistics on the device); "pipeline" times one
 encode -> inject -> decode chain.  Bytes/unit follow SURVEY 8(d).
 
@@ -33,7 +34,7 @@ import torch  # noqa: E402
 PEAK = 8000.0  # GB/s
 
 
-def timed(fn, reps, warmup=10):
+def timed(fn, reps, warmup=100):
     for _ in range(warmup):
         fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -164,8 +165,10 @@ def extended(reps):
                                      n, "values", 1.5)
     out["packed_h84_decode"] = entry(timed(lambda: ops.hamming84_decode_packed_into(
         hcw, hn2, ht, n, st), reps), n, "values", 1.75)
-    # paged decode attention, [8 seqs x 4096 ctx, 32 heads, D=128]
-    for codec in ("hamming84", "golay", "golay_packed"):
+    # paged decode attention, [8 seqs x 4096 ctx, 32 heads, D=128]; MHA and
+    # GQA with 8 cache heads (Llama-style 32/8: a workgroup serves 4 query heads)
+    for codec, hkv in (("hamming84", 32), ("golay", 32), ("golay_packed", 32),
+                       ("hamming84", 8), ("golay", 8), ("golay_packed", 8)):
         b, hq, d, ctx, bs = 8, 32, 128, 4096, 16
         per = d if codec == "hamming84" else (d + 2) // 3
         if codec == "golay_packed":  # bytes per token row (KVECC_GOLAY_PACKED_ROW)
@@ -173,10 +176,10 @@ def extended(reps):
         nb = ctx // bs
         blocks = b * nb
         from kvecc.memory_layout import kv_cache_pair  # K/V as SimpleBlockManager lays them out
-        kc, vc = kv_cache_pair((blocks, 1, hq, bs * per), torch.int32 if codec == "golay" else torch.uint8, dev)
+        kc, vc = kv_cache_pair((blocks, 1, hkv, bs * per), torch.int32 if codec == "golay" else torch.uint8, dev)
         kc.random_(0, 1 << 24 if codec == "golay" else 256)
         vc.copy_(kc.roll(1, 0))
-        ks = torch.rand(blocks, 1, hq, bs, device=dev)
+        ks = torch.rand(blocks, 1, hkv, bs, device=dev)
         vs = torch.rand_like(ks)
         table = torch.randperm(blocks, device=dev).to(torch.int32).view(b, nb)
         lens = torch.full((b,), ctx, dtype=torch.int32, device=dev)
@@ -184,11 +187,11 @@ def extended(reps):
         o = torch.empty_like(q)
         us = timed(lambda: ops.paged_attention_into(q, kc, vc, table, lens, ks, vs, o, 0, bs,
                                                     1 / math.sqrt(d), codec, ctx), reps)
-        byts = 2 * b * ctx * hq * (per * kc.element_size() + 4)
+        byts = 2 * b * ctx * hkv * (per * kc.element_size() + 4)
         e = entry(us, b * ctx, "tokens")
-        e.update({"bytes": byts, "GBps": byts / (us * 1e-6) / 1e9,
+        e.update({"heads": hq, "kv_heads": hkv, "bytes": byts, "GBps": byts / (us * 1e-6) / 1e9,
                   "hbm_frac": byts / (us * 1e-6) / 1e9 / PEAK})
-        out[f"paged_attention_{codec}"] = e
+        out[f"paged_attention_{codec}" + ("" if hkv == hq else f"_gqa{hq}x{hkv}")] = e
     return out
 
 
