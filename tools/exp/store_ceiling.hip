@@ -216,6 +216,43 @@ extern "C" __attribute__((visibility("default"))) int store_probe_dyn(const void
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// PERM: the fused-read mix with the reads gathered like the shim cache's:
+// unit u = (side, bh, lb) with lb fastest (256 logical blocks per (b, h), 32
+// heads, 8 sequences, 2 sides); its 2816 source bytes sit at physical block
+// perm[b * 256 + lb] of that head (random permutation of 2048 blocks), the
+// 32 heads of a block adjacent.  One unit per wave, full grid.
+__global__ __launch_bounds__(256) void probe_perm(const char *__restrict__ src, char *__restrict__ dst,
+                                                  uint32_t units, const int32_t *__restrict__ perm) {
+  const uint32_t lane = threadIdx.x % 64;
+  const uint32_t u = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  if (u >= units) return;
+  const uint32_t per_side = units / 2, side = u / per_side, r = u - side * per_side;
+  const uint32_t lb = r % 256, bh = r / 256, b = bh / 32, h = bh % 32;
+  const uint32_t blk = perm ? (uint32_t)perm[b * 256 + lb] : b * 256 + lb;
+  const size_t su = ((size_t)side * 2048 + blk) * 32 + h;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(src) + su * 2816, 0, 2816, 0x00020000);
+  u32x4 rr[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    rr[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * i + 16 * lane, 0, 2));
+  uint32_t acc = lane;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc ^= rr[i].x ^ rr[i].y ^ rr[i].z ^ rr[i].w;
+  const u32x4 v{acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+  u32x4 *o = reinterpret_cast<u32x4 *>(dst + (size_t)u * 4096) + lane;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) __builtin_nontemporal_store(v, o + 64 * i);
+}
+
+extern "C" __attribute__((visibility("default"))) int store_probe_perm(const void *src, void *dst, uint32_t units,
+                                                                       const void *perm, int lds, void *stream) {
+  hipLaunchKernelGGL(probe_perm, dim3((units + 3) / 4), dim3(256), lds, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const char *>(src), reinterpret_cast<char *>(dst), units,
+                     reinterpret_cast<const int32_t *>(perm));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 extern "C" __attribute__((visibility("default"))) void store_probe_mode(uint32_t per, uint32_t tab,
                                                                        const void *table) {
   g_per = per;
