@@ -483,6 +483,10 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
 // every tile, computed once; the next tile's loads are issued before the
 // current tile's stores.  Per-lane offsets are 32-bit inside a tile, tile
 // bases 64-bit and wave-uniform (descriptors in SGPRs).
+// dynamic tail schedule (kvecc_internal.h TileSchedule), as the fused reads
+#ifndef KVECC_GOLAY_ROWS_DYN
+#define KVECC_GOLAY_ROWS_DYN 0
+#endif
 constexpr int kRegBlock = 512;
 constexpr int kRegWaves = kRegBlock / kWave;
 constexpr int kRegGroups = 4;        // 4-codeword groups per lane per tile (max)
@@ -498,6 +502,7 @@ struct RegRowsArgs {
   uint32_t d, g, gpr, lr, tr;
   const void *tab;  // decode: spread tables (uint32[8192]); encode: parity (uint16[4096])
   uint64_t *stats;
+  uint32_t *dyn;    // work-counter slot (KVECC_GOLAY_ROWS_DYN; ntiles < 2^32)
 };
 
 struct RegItems {
@@ -542,6 +547,9 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
   int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
   if (t >= a.ntiles) return;  // no workgroup barrier below
   const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
+  constexpr bool kDyn = KVECC_GOLAY_ROWS_DYN;
+  TileSchedule<kDyn> sched;
+  if (kDyn) sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
   u32x4 w[kRegGroups];
   auto issue = [&](int64_t tt) {
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
@@ -580,7 +588,7 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
     }
     wave_lds_sync();
     const int64_t cur = t;
-    t += tstride;
+    t = kDyn ? (int64_t)sched.next((uint32_t)t, lane) : t + tstride;
     const bool more = t < a.ntiles;
     if (more) issue(t);
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
@@ -627,6 +635,9 @@ __global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRow
   int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
   if (t >= a.ntiles) return;
   const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
+  constexpr bool kDyn = KVECC_GOLAY_ROWS_DYN;
+  TileSchedule<kDyn> sched;
+  if (kDyn) sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
   u32x4 v[kRegChunks];
   auto issue = [&](int64_t tt) {
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
@@ -647,7 +658,7 @@ __global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRow
     }
     wave_lds_sync();
     const int64_t cur = t;
-    t += tstride;
+    t = kDyn ? (int64_t)sched.next((uint32_t)t, lane) : t + tstride;
     const bool more = t < a.ntiles;
     if (more) issue(t);
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
@@ -777,9 +788,11 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
   if (!par) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
   const RegGeom rg = reg_geom(d, g, true);
-  if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 16)) {
+  if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 16) &&
+      (!KVECC_GOLAY_ROWS_DYN || cdiv(rows, rg.tr) < (1LL << 31))) {
     RegRowsArgs a{nibbles, codewords, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
                   par, nullptr};
+    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot())) return KVECC_EHIP;
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
     KVECC_LAUNCH(golay_encode_rows_reg_kernel, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
     return check_launch("golay_encode_rows");
@@ -809,11 +822,13 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
   if (!par || !cor) return KVECC_EHIP;
   int64_t g = (d + 2) / 3;
   const RegGeom rg = reg_geom(d, g, false);
-  if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 4)) {
+  if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 4) &&
+      (!KVECC_GOLAY_ROWS_DYN || cdiv(rows, rg.tr) < (1LL << 31))) {
     const uint32_t *atab = golay_attn_table_dev();
     if (!atab) return KVECC_EHIP;
     RegRowsArgs a{codewords, nibbles, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
                   atab, stats};
+    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot())) return KVECC_EHIP;
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
     if (stats)
       KVECC_LAUNCH(golay_decode_rows_reg_kernel<true>, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);

@@ -31,7 +31,9 @@ for p in sys.argv[1:]:
         getattr(h, n).argtypes = _lib.SIGNATURES[n]
         getattr(h, n).restype = ctypes.c_int
     libs.append((os.path.basename(p), h))
-outs = [(torch.empty_like(ref_cw), torch.empty_like(x), ops.new_stats(dev)) for _ in libs]
+# one output pair for every library (where outputs sit in HBM moves times)
+shared = (torch.empty_like(ref_cw), torch.empty_like(x))
+outs = [(shared[0], shared[1], ops.new_stats(dev)) for _ in libs]
 
 
 def enc(i):
@@ -43,13 +45,18 @@ def dec(i):
                                               outs[i][2].data_ptr(), stream) == 0
 
 
-for i in range(len(libs)):
+ref = None
+for i, (name, _) in enumerate(libs):
+    shared[0].fill_(-1)
+    shared[1].fill_(0xEE)
     enc(i)
     dec(i)
-torch.cuda.synchronize()
-for i, (name, _) in enumerate(libs):
-    print(f"{name}: encode equal={torch.equal(outs[i][0], outs[0][0])} decode equal="
-          f"{torch.equal(outs[i][1], outs[0][1])} stats={ops.read_stats(outs[i][2])}", flush=True)
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = (shared[0].clone(), shared[1].clone())
+    print(f"{name}: encode equal={torch.equal(shared[0], ref[0])} decode equal="
+          f"{torch.equal(shared[1], ref[1])} stats={ops.read_stats(outs[i][2])}", flush=True)
+del ref
 times = {(i, k): [] for i in range(len(libs)) for k in ("enc", "dec")}
 for r in range(ROUNDS):
     for i in range(len(libs)):
