@@ -277,6 +277,9 @@ __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
   if (E % 2) acc[E - 1] = fmaf(p, v[E - 1], acc[E - 1]);
 }
 
+#ifndef KVECC_ATTN_GQA_PREFETCH
+#define KVECC_ATTN_GQA_PREFETCH 1
+#endif
 // minimum waves per SIMD the register allocation must allow (0: no bound)
 #ifndef KVECC_ATTN_MIN_WAVES
 #define KVECC_ATTN_MIN_WAVES 0
@@ -409,27 +412,47 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[j][e] = 0.0f;
   }
+  // GQA workgroups (G > 1) do G times the arithmetic per row and have a
+  // quarter of MHA's rows: they issue the next iteration's rows before using
+  // this one's (MHA measured no gain from that in round 1)
+  constexpr bool kPrefetch = G > 1 && CODEC == KVECC_CODEC_H84 && KVECC_ATTN_GQA_PREFETCH;
+  C pkc[U], pvc[U];
+  float pks[U], pvs[U];
+  bool pok[U];
+  auto load_rows = [&](int i0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // branch-free: invalid rows read row 0, masked
+      const int32_t r = rows[i0 + u * TP];
+      pok[u] = r >= 0;
+      const int64_t row = pok[u] ? r : 0;
+      if (BUF) {
+        pkc[u].load_buf(a, krs, (int32_t)row, cs);
+        pvc[u].load_buf(a, vrs, (int32_t)row, cs);
+        pks[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, (uint32_t)row * 4u, 0, 0));
+        pvs[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, (uint32_t)row * 4u, 0, 0));
+      } else {
+        pkc[u].load(a, a.k_cache, row, cs);
+        pvc[u].load(a, a.v_cache, row, cs);
+        pks[u] = a.k_scales[row];
+        pvs[u] = a.v_scales[row];
+      }
+    }
+  };
+  if (kPrefetch && grp < ntok) load_rows(grp);
   for (int i0 = grp; i0 < ntok; i0 += TP * U) {
+    if (!kPrefetch) load_rows(i0);
     C kc[U], vc[U];
     float ks[U], vs[U];
     bool ok[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {  // branch-free: invalid rows read row 0, masked
-      const int32_t r = rows[i0 + u * TP];
-      ok[u] = r >= 0;
-      const int64_t row = ok[u] ? r : 0;
-      if (BUF) {
-        kc[u].load_buf(a, krs, (int32_t)row, cs);
-        vc[u].load_buf(a, vrs, (int32_t)row, cs);
-        ks[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, (uint32_t)row * 4u, 0, 0));
-        vs[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, (uint32_t)row * 4u, 0, 0));
-      } else {
-        kc[u].load(a, a.k_cache, row, cs);
-        vc[u].load(a, a.v_cache, row, cs);
-        ks[u] = a.k_scales[row];
-        vs[u] = a.v_scales[row];
-      }
+    for (int u = 0; u < U; ++u) {
+      kc[u] = pkc[u];
+      vc[u] = pvc[u];
+      ks[u] = pks[u];
+      vs[u] = pvs[u];
+      ok[u] = pok[u];
     }
+    if (kPrefetch && i0 + TP * U < ntok) load_rows(i0 + TP * U);
     float sc[G][U];
     float mn[G];
 #pragma unroll

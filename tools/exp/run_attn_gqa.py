@@ -10,7 +10,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "quantiz
 import torch  # noqa: E402
 from kvecc import _lib  # noqa: E402
 VP, I64 = ctypes.c_void_p, ctypes.c_int64
-libs = {"prod": _lib.load(), "nogqa": ctypes.CDLL(os.path.join(HERE, "libattn_nogqa.so"))}
+libs = {"prod": _lib.load()}
+for name in os.environ.get("LIBS", "nogqa").split(","):
+    libs[name] = ctypes.CDLL(os.path.join(HERE, f"libattn_{name}.so"))
 for l in libs.values():
     l.kvecc_paged_attention.argtypes = [VP, ctypes.c_int, VP, VP, VP, VP, VP, VP, VP, I64, I64, I64, I64, I64,
                                         I64, I64, I64, I64, I64, ctypes.c_float, ctypes.c_int, VP, I64, VP]
@@ -63,10 +65,11 @@ for codec, (cid, per, dt) in codecs.items():
                 e1.record()
                 times[n].append((e0, e1))
         torch.cuda.synchronize()
-        diff = float((outs["prod"].float() - outs["nogqa"].float()).abs().max())
+        other = [n for n in libs if n != "prod"][0]
+        diff = float((outs["prod"].float() - outs[other].float()).abs().max())
         kv_bytes = 2 * blocks * hkv * BS * (per * kc.element_size() + 4)
         line = " ".join(f"{n} {statistics.median(a.elapsed_time(b) * 1e3 for a, b in t):6.1f} us"
                         for n, t in times.items())
         med = statistics.median(a.elapsed_time(b) * 1e3 for a, b in times["prod"])
         print(f"{codec:12s} H={H} Hkv={hkv:2d}: {line}  (prod {kv_bytes / med / 1e3:5.0f} GB/s of K+V cache)"
-              f"  max|prod-nogqa| {diff:.2e}", flush=True)
+              f"  max|prod-{other}| {diff:.2e}", flush=True)
