@@ -37,6 +37,9 @@ const uint16_t *golay_correct_table_dev();
 //   [4096, 8192) spread(data error of syndrome s) | ((count(s) & 3) | unc << 6) << 24
 //                (count 0-3 bits corrected; uncorrectable: spread part 0, byte 3 = 0x40)
 const uint32_t *golay_attn_table_dev();
+// packed decode tables, 24 KiB: uint16 [4096] parity(lo) << 2, then uint32
+// [4096] error data | (bits corrected & 3) << 24 | uncorrectable << 31
+const uint8_t *golay_pk_table_dev();
 // Work counters of the dynamically scheduled tile kernels (shim.hip): a ring of
 // kDynSlots slots per device, each kDynCounters counters kDynStride words apart,
 // zero between launches (each counter's last user resets it).  shim_dyn_slot() hands out the current device's slots round-robin,

@@ -243,6 +243,124 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
   if (WITH_STATS) flush_stats2<kPkBlock>(stats, bits, unc);
 }
 
+// Wave-tile decode (the default): a wave owns tiles of 1024 codewords (3072
+// codeword bytes in, 1536 nibble bytes + 128 flag bytes out), scheduled as the
+// fused reads are (TileSchedule: a static share, then per-launch counters), so
+// the grid is persistent -- 3 workgroups per CU, each staging its 24 KiB of
+// tables once -- and no wave waits on another.  The tile's bytes come in as
+// three 16-byte buffer loads per lane (each wave-instruction 1 KiB
+// contiguous), the next tile's already in flight, through a wave-private LDS
+// stage; each lane then decodes two groups of 8 codewords.  Per codeword: one
+// lookup of parity(lo) << 2 (a byte offset), one of the syndrome's entry
+// (error data | bits << 24 | uncorrectable << 31), data = (c ^ e) & 0xFFF in one
+// v_bitop3, the statistics as a 32-bit sum of entries (bits 24-30: corrected
+// bits of <= 8 codewords) and the flag bits shifted in with v_alignbit.
+#ifndef KVECC_PACKED_DEC_V2
+#define KVECC_PACKED_DEC_V2 1
+#endif
+#ifndef KVECC_PACKED_DEC_V2_PER_CU
+#define KVECC_PACKED_DEC_V2_PER_CU 3
+#endif
+#ifndef KVECC_PACKED_DEC_DYN
+#define KVECC_PACKED_DEC_DYN 1
+#endif
+constexpr int kPk2Block = 512;
+constexpr int kPk2Waves = kPk2Block / kWave;
+constexpr int kPk2TileCw = kWave * 16;         // codewords per wave tile
+constexpr int kPk2TileBytes = kPk2TileCw * 3;  // 3072
+
+struct PkDecArgs {
+  const uint8_t *cw;
+  uint32_t *nib;
+  uint8_t *flags;
+  uint32_t units;  // wave tiles
+  const uint8_t *tab;  // golay_pk_table_dev()
+  uint64_t *stats;
+  uint32_t *dyn;
+};
+
+template <bool WITH_FLAGS, bool WITH_STATS>
+__global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkDecArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t tab[24576];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kPk2Waves][kPk2TileBytes];
+  for (int i = threadIdx.x; i < 24576 / 16; i += kPk2Block)
+    reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
+  __syncthreads();
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  const uint32_t gw = blockIdx.x * kPk2Waves + wave, nwaves = gridDim.x * kPk2Waves;
+  if (gw >= a.units) return;  // no workgroup barrier below
+  uint8_t *stage = stage_all[wave];
+  constexpr bool kDyn = KVECC_PACKED_DEC_DYN;
+  TileSchedule<kDyn> sched;
+  if (kDyn) sched.init(a.units, a.dyn, gw, nwaves, lane);
+  // whole codeword buffer (< 2 GiB, checked on the host); nt loads
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t *>(a.cw), 0, (int)(a.units * (uint32_t)kPk2TileBytes), 0x00020000);
+  uint32_t t = gw;
+  u32x4 nxt[3];
+  auto issue = [&](uint32_t tt) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      nxt[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rs, tt * (uint32_t)kPk2TileBytes + 16u * (lane + kWave * k), 0, 2));
+  };
+  issue(t);
+  uint32_t bits = 0, unc = 0;
+  for (;;) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) reinterpret_cast<u32x4 *>(stage)[lane + kWave * k] = nxt[k];
+    wave_lds_sync();
+    const uint32_t cur = t;
+    t = kDyn ? sched.next(t, lane) : t + nwaves;
+    const bool more = t < a.units;
+    if (more) issue(t);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const u32x2 *p = reinterpret_cast<const u32x2 *>(stage + (g * kWave + lane) * 24);
+      const u32x2 x0 = p[0], x1 = p[1], x2 = p[2];
+      const uint32_t w[6] = {x0.x, x0.y, x1.x, x1.y, x2.x, x2.y};
+      uint32_t c[8];  // bits 24-31 are a neighbour's: every use below masks them
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        c[4 * h] = w[3 * h];
+        c[4 * h + 1] = __builtin_amdgcn_alignbyte(w[3 * h + 1], w[3 * h], 3);
+        c[4 * h + 2] = __builtin_amdgcn_alignbyte(w[3 * h + 2], w[3 * h + 1], 2);
+        c[4 * h + 3] = w[3 * h + 2] >> 8;
+      }
+      uint32_t d[8], esum = 0, fl = 0;
+#pragma unroll
+      for (int k = 7; k >= 0; --k) {  // descending: the flag of codeword k lands at bit k
+        const uint32_t pv = *reinterpret_cast<const uint16_t *>(tab + ((c[k] << 1) & 0x1FFEu));
+        const uint32_t off = __builtin_amdgcn_bitop3_b32(c[k] >> 10, pv, 0x3FFCu, 0x28);  // (S0 ^ S1) & S2
+        const uint32_t e = *reinterpret_cast<const uint32_t *>(tab + 8192 + off);
+        d[k] = __builtin_amdgcn_bitop3_b32(c[k], e, 0xFFFu, 0x28);
+        esum += e;
+        fl = __builtin_amdgcn_alignbit(fl, e, 31);  // fl << 1 | e >> 31
+      }
+      if (WITH_STATS) {
+        bits += (esum >> 24) & 0x7Fu;  // <= 8 * 3; bit 31 collects the flags, dropped
+        unc += __builtin_popcount(fl);
+      }
+      uint32_t n[3];
+      nib_pack8(d, n);
+      const uint32_t grp = cur * (kPk2TileCw / 8) + g * kWave + lane;  // group of 8 codewords
+      st_stream(reinterpret_cast<u32x3v *>(a.nib + (size_t)grp * 3), u32x3v{n[0], n[1], n[2]});
+      if (WITH_FLAGS) st_stream(a.flags + grp, (uint8_t)fl);
+    }
+    if (!more) break;
+    wave_lds_sync();
+  }
+  if (WITH_STATS) {
+    bits = wave_sum(bits);
+    unc = wave_sum(unc);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
+      if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+    }
+  }
+}
+
 // ---- scalar tails (< one tile), byte accesses -----------------------------------
 
 __device__ __forceinline__ uint32_t get_nib(const uint8_t *p, int64_t j) {
@@ -352,6 +470,89 @@ __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4
   if (WITH_STATS) flush_stats2<kHpBlock>(stats, n1, n2);
 }
 
+// Wave-tile decode (the default): a wave owns tiles of 64 lanes x kHp2Chunks
+// 16-value chunks (chunk k of a tile at lane + 64 k, so every wave-instruction
+// moves one contiguous 1 KiB / 512 B / 256 B span), all of a tile's loads
+// issued together and the next tile's before this one's stores, over a
+// persistent grid with the fused reads' dynamic tail (TileSchedule).
+#ifndef KVECC_H84_PACKED_V2
+#define KVECC_H84_PACKED_V2 1
+#endif
+#ifndef KVECC_H84_PACKED_CHUNKS
+#define KVECC_H84_PACKED_CHUNKS 4
+#endif
+#ifndef KVECC_H84_PACKED_PER_CU
+#define KVECC_H84_PACKED_PER_CU 8
+#endif
+constexpr int kHp2Chunks = KVECC_H84_PACKED_CHUNKS;
+constexpr int kHp2Block = 256;
+constexpr int kHp2Waves = kHp2Block / kWave;
+constexpr uint32_t kHp2TileChunks = kWave * kHp2Chunks;  // 16-value chunks per wave tile
+
+struct HpDecArgs {
+  const uint8_t *cw;
+  u32x2 *nib;
+  uint32_t *types;
+  uint32_t units;  // wave tiles
+  uint64_t *stats;
+  uint32_t *dyn;
+};
+
+template <bool WITH_TYPES, bool WITH_STATS>
+__global__ __launch_bounds__(kHp2Block) void h84_decode_packed_wave_kernel(HpDecArgs a) {
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  const uint32_t gw = blockIdx.x * kHp2Waves + wave, nwaves = gridDim.x * kHp2Waves;
+  if (gw >= a.units) return;
+  constexpr bool kDyn = KVECC_PACKED_DEC_DYN;
+  TileSchedule<kDyn> sched;
+  if (kDyn) sched.init(a.units, a.dyn, gw, nwaves, lane);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t *>(a.cw), 0, (int)(a.units * kHp2TileChunks * 16u), 0x00020000);
+  uint32_t t = gw;
+  u32x4 c[kHp2Chunks];
+  auto issue = [&](uint32_t tt) {
+#pragma unroll
+    for (int k = 0; k < kHp2Chunks; ++k)
+      c[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rs, 16u * (tt * kHp2TileChunks + lane + kWave * k), 0, 2));
+  };
+  issue(t);
+  uint32_t n1 = 0, n2 = 0;
+  for (;;) {
+    u32x2 nb[kHp2Chunks];
+    uint32_t tb[kHp2Chunks];
+#pragma unroll
+    for (int k = 0; k < kHp2Chunks; ++k) {
+      const uint32_t w[4] = {c[k].x, c[k].y, c[k].z, c[k].w};
+      uint32_t d[4], ty[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h84_decode4(w[j], d[j], ty[j], n1, n2);
+      nb[k] = u32x2{nib_pack4(d[0]) | nib_pack4(d[1]) << 16, nib_pack4(d[2]) | nib_pack4(d[3]) << 16};
+      tb[k] = type_pack4(ty[0]) | type_pack4(ty[1]) << 8 | type_pack4(ty[2]) << 16 | type_pack4(ty[3]) << 24;
+    }
+    const uint32_t cur = t;
+    t = kDyn ? sched.next(t, lane) : t + nwaves;
+    const bool more = t < a.units;
+    if (more) issue(t);
+#pragma unroll
+    for (int k = 0; k < kHp2Chunks; ++k) {
+      const size_t i = (size_t)cur * kHp2TileChunks + lane + kWave * k;
+      st_stream(a.nib + i, nb[k]);
+      if (WITH_TYPES) st_stream(a.types + i, tb[k]);
+    }
+    if (!more) break;
+  }
+  if (WITH_STATS) {
+    n1 = wave_sum(n1);
+    n2 = wave_sum(n2);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+      if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
+    }
+  }
+}
+
 // tails and unaligned buffers, byte accesses: encode one thread per value,
 // decode one thread per group of 4 values (2 nibble bytes + 1 type byte, never
 // shared because `begin` is a multiple of 16)
@@ -421,7 +622,25 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
   if (!par || !cor) return KVECC_EHIP;
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
-  if (KVECC_PACKED_DEC_STAGED && aligned(nibbles, 4) && aligned(codewords, 16)) {
+  const int64_t wave_tiles = m / kPk2TileCw;
+  if (KVECC_PACKED_DEC_V2 && aligned(nibbles, 4) && aligned(codewords, 16) && wave_tiles > 0 &&
+      wave_tiles * kPk2TileBytes < ((int64_t)1 << 31)) {
+    const uint8_t *tab = golay_pk_table_dev();
+    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot() : nullptr;
+    if (!tab || (KVECC_PACKED_DEC_DYN && !dyn)) return KVECC_EHIP;
+    const PkDecArgs a{codewords, reinterpret_cast<uint32_t *>(nibbles), uncorrectable, (uint32_t)wave_tiles,
+                      tab, stats, dyn};
+    const dim3 grid(grid_for(wave_tiles, kPk2Waves, KVECC_PACKED_DEC_V2_PER_CU)), block(kPk2Block);
+    if (uncorrectable && stats)
+      KVECC_LAUNCH((golay_decode_packed_wave_kernel<true, true>), grid, block, 0, st, a);
+    else if (uncorrectable)
+      KVECC_LAUNCH((golay_decode_packed_wave_kernel<true, false>), grid, block, 0, st, a);
+    else if (stats)
+      KVECC_LAUNCH((golay_decode_packed_wave_kernel<false, true>), grid, block, 0, st, a);
+    else
+      KVECC_LAUNCH((golay_decode_packed_wave_kernel<false, false>), grid, block, 0, st, a);
+    done = wave_tiles * kPk2TileCw;
+  } else if (KVECC_PACKED_DEC_STAGED && aligned(nibbles, 4) && aligned(codewords, 16)) {
     const int64_t ntiles = m / kPkTile;
     if (ntiles > 0) {
       const dim3 grid(grid_for(ntiles, 1, KVECC_PACKED_DEC_PER_CU)), block(kPkBlock);
@@ -497,13 +716,32 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
   if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "hamming84_decode_packed: null pointer");
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
-  if (aligned(nibbles, 8) && aligned(codewords, 16) && (!error_types || aligned(error_types, 4))) {
-    const int64_t n16 = n / 16;
+  const int64_t hp_tiles = n / (16 * (int64_t)kHp2TileChunks);
+  if (KVECC_H84_PACKED_V2 && aligned(nibbles, 8) && aligned(codewords, 16) &&
+      (!error_types || aligned(error_types, 4)) && hp_tiles > 0 && n < ((int64_t)1 << 31)) {
+    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot() : nullptr;
+    if (KVECC_PACKED_DEC_DYN && !dyn) return KVECC_EHIP;
+    const HpDecArgs a{codewords, reinterpret_cast<u32x2 *>(nibbles), reinterpret_cast<uint32_t *>(error_types),
+                      (uint32_t)hp_tiles, stats, dyn};
+    const dim3 grid(grid_for(hp_tiles, kHp2Waves, KVECC_H84_PACKED_PER_CU)), block(kHp2Block);
+    if (error_types && stats)
+      KVECC_LAUNCH((h84_decode_packed_wave_kernel<true, true>), grid, block, 0, st, a);
+    else if (error_types)
+      KVECC_LAUNCH((h84_decode_packed_wave_kernel<true, false>), grid, block, 0, st, a);
+    else if (stats)
+      KVECC_LAUNCH((h84_decode_packed_wave_kernel<false, true>), grid, block, 0, st, a);
+    else
+      KVECC_LAUNCH((h84_decode_packed_wave_kernel<false, false>), grid, block, 0, st, a);
+    done = hp_tiles * 16 * (int64_t)kHp2TileChunks;
+  }
+  if (done < n && aligned(nibbles, 8) && aligned(codewords, 16) && (!error_types || aligned(error_types, 4))) {
+    const int64_t n16 = (n - done) / 16;
     if (n16 > 0) {
       const dim3 grid(grid_for(n16, kHpBlock, 32)), block(kHpBlock);
-      const u32x4 *c = reinterpret_cast<const u32x4 *>(codewords);
-      u32x2 *o = reinterpret_cast<u32x2 *>(nibbles);
-      uint32_t *t = reinterpret_cast<uint32_t *>(error_types);
+      const int64_t i0 = done / 16;  // after the wave tiles
+      const u32x4 *c = reinterpret_cast<const u32x4 *>(codewords) + i0;
+      u32x2 *o = reinterpret_cast<u32x2 *>(nibbles) + i0;
+      uint32_t *t = error_types ? reinterpret_cast<uint32_t *>(error_types) + i0 : nullptr;
       if (error_types && stats)
         KVECC_LAUNCH((h84_decode_packed_kernel<true, true>), grid, block, 0, st, c, o, t, n16, stats);
       else if (error_types)
@@ -513,7 +751,7 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
       else
         KVECC_LAUNCH((h84_decode_packed_kernel<false, false>), grid, block, 0, st, c, o, t, n16, stats);
     }
-    done = n16 * 16;
+    done += n16 * 16;
   }
   if (done < n)
     KVECC_LAUNCH(h84_decode_packed_tail_kernel, dim3(grid_for(cdiv(n - done, 4), kBlock)),

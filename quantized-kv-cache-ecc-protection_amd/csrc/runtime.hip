@@ -7,6 +7,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <mutex>
 
@@ -37,6 +38,7 @@ static int g_cu[kMaxDev];
 static std::atomic<uint16_t *> g_parity[kMaxDev];
 static std::atomic<uint16_t *> g_correct[kMaxDev];
 static std::atomic<uint32_t *> g_attn[kMaxDev];
+static std::atomic<uint8_t *> g_pk[kMaxDev];
 static std::atomic<uint32_t *> g_dyn[kMaxDev];  // kDynSlots work-counter slots, zeroed
 static std::atomic<uint32_t> g_dyn_next[kMaxDev];
 
@@ -127,7 +129,10 @@ static int ensure_tables(int d) {
   struct Host {
     uint16_t par[4096], cor[4096];
     uint32_t attn[8192];
+    uint16_t pk0[4096];  // packed decode: parity(lo) << 2 (byte offset of the syndrome's entry)
+    uint32_t pk1[4096];  // packed decode: error data | (bits & 3) << 24 | uncorrectable << 31
   };
+  static_assert(offsetof(Host, pk1) == offsetof(Host, pk0) + 8192, "packed tables contiguous");
   static Host host;  // guarded by g_mu
   build_golay_parity_table(host.par);
   build_golay_correct_table(host.cor);
@@ -138,6 +143,8 @@ static int ensure_tables(int d) {
     // so a sum of byte 3 over up to 21 codewords keeps both fields apart
     const uint32_t n = host.cor[i] >> 12;  // 0-3 bits corrected, 4 = uncorrectable
     host.attn[4096 + i] = spread12(host.cor[i] & 0xFFFu) | ((n & 3u) | (n >> 2) << 6) << 24;
+    host.pk0[i] = (uint16_t)(host.par[i] << 2);
+    host.pk1[i] = (host.cor[i] & 0xFFFu) | (n & 3u) << 24 | (n >> 2) << 31;
   }
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
@@ -155,6 +162,7 @@ static int ensure_tables(int d) {
   g_dyn[d].store(dyn, std::memory_order_release);
   g_parity[d].store(buf->par, std::memory_order_release);
   g_correct[d].store(buf->cor, std::memory_order_release);
+  g_pk[d].store(reinterpret_cast<uint8_t *>(buf->pk0), std::memory_order_release);
   g_attn[d].store(buf->attn, std::memory_order_release);  // last: the "built" flag
   return KVECC_OK;
 }
@@ -170,6 +178,7 @@ static const P *table_dev(std::atomic<P *> *tabs) {
 const uint16_t *golay_parity_table_dev() { return table_dev(g_parity); }
 const uint16_t *golay_correct_table_dev() { return table_dev(g_correct); }
 const uint32_t *golay_attn_table_dev() { return table_dev(g_attn); }
+const uint8_t *golay_pk_table_dev() { return table_dev(g_pk); }
 
 uint32_t *shim_dyn_slot() {
   const int d = current_device();
