@@ -554,6 +554,276 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   }
 }
 
+// ---- GQA on the matrix cores (Hamming(8,4), fp16 queries) -----------------------
+//
+// With G query heads per cache head the VALU kernel above does G dot products
+// and G accumulator updates per decoded value, so its time stays near the MHA
+// kernel's while the cache bytes fall by G.  Here both products run on
+// v_mfma_f32_16x16x32_f16, and the VALU only decodes:
+//   S^T[16 tokens x 16 heads] = K[16 tokens x D] . Q^T[D x 16 heads]   (D/32 MFMAs per 16 tokens)
+//   O^T[16 d x 16 heads]     += V^T[16 d x 32 tokens] . P[32 tokens x 16 heads]
+// Columns are query heads (G <= 16 used, the rest zero).  Decoded values n - 8
+// (integers in [-8, 7]) and the fp16 queries are exact in f16, so the scores
+// are the fp32 sums of exact products, as in the VALU kernel; P (fp32) goes
+// in as two f16 halves, hi + lo, 22 bits.  The operand maps (A[row l&15][k =
+// 8(l>>4)+j], B[k][col l&15], C[row 4(l>>4)+r][col l&15]) are bent so that
+// every lane's loads stay contiguous and no value moves between lanes:
+//   * K: lane (token t = l&15, group g = l>>4) loads D/4 contiguous bytes of its
+//     token row, d = (D/4)g .. ; MFMA kk takes bytes 8kk..8kk+7 (the same k -> d
+//     map for the Q operand, which is loaded once);
+//   * a wave step is 32 tokens, two S^T tiles; lane (head n, g) then holds
+//     the scores of tokens 4g + r and 16 + 4g + r (r = 0..3) for head n -- which
+//     are exactly the 8 k-slots of the PV B operand when PV's k maps slot
+//     8g + j to token 16(j >> 2) + 4g + (j & 3): P needs no shuffle;
+//   * V: the same 8 tokens per lane, D/16 contiguous bytes each at d = (D/16) m
+//     (m = l&15); M-tile mt takes byte mt of each, so output row m of tile mt
+//     is d = (D/16)(4g + r) + mt.
+// Decode: LDS table byte -> data nibble (single errors corrected, doubles keep
+// their data, attention_ecc.py:56-149), pairs packed as f16 1024 + n by an OR
+// of 0x6400 and shifted by one v_pk_add_f16 of -1032.  The online softmax runs
+// per lane on its 8 scores (head maxima across the 4 lanes of a head with two
+// xor-shuffles), the workgroup's 4 waves merge through LDS, and the split goes
+// to the workspace of the combine kernel above.
+#ifndef KVECC_ATTN_MFMA
+#define KVECC_ATTN_MFMA 1
+#endif
+#ifndef KVECC_ATTN_MFMA_WG_PER_CU
+#define KVECC_ATTN_MFMA_WG_PER_CU 4
+#endif
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kMfmaStep = 32;  // tokens per wave step
+
+// two table values (data nibbles 0..15) -> f16 pair (n - 8), lo in bits 0..15
+__device__ __forceinline__ uint32_t nib_pair_f16(uint32_t lo, uint32_t hi) {
+  const f16x2 h = __builtin_bit_cast(f16x2, (lo | hi << 16) | 0x64006400u);  // 1024 + n
+  return __builtin_bit_cast(uint32_t, h + f16x2{(_Float16)-1032.0f, (_Float16)-1032.0f});
+}
+
+// NB contiguous bytes (2, 4, 8, 16 or 32) at byte offset off -> dwords w
+template <int NB>
+__device__ __forceinline__ void load_chunk(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t *w) {
+  if constexpr (NB == 2) {
+    w[0] = __builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0);
+  } else if constexpr (NB == 4) {
+    w[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+  } else if constexpr (NB == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+    w[0] = v[0];
+    w[1] = v[1];
+  } else {
+#pragma unroll
+    for (int k = 0; k < NB / 16; ++k) {
+      const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * k, 0, 0));
+      w[4 * k] = v.x;
+      w[4 * k + 1] = v.y;
+      w[4 * k + 2] = v.z;
+      w[4 * k + 3] = v.w;
+    }
+  }
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs a) {
+  constexpr int KK = D / 32;  // QK MFMAs per 16-token tile
+  constexpr int MT = D / 16;  // PV M-tiles; V bytes per lane per token
+  constexpr int KB = D / 4;   // K bytes per lane per token
+  constexpr int VW = MT >= 4 ? MT / 4 : 1;  // V dwords per token
+  constexpr int kWaves = kBlock / kWave;
+  __shared__ __attribute__((aligned(16))) int32_t rows[kMaxSplit + kMfmaStep];
+  __shared__ int32_t blks[kMaxSplit + 1];
+  __shared__ uint8_t lut[256];
+  __shared__ float red[kWaves][G][D];
+  __shared__ float gml[2][kWaves][G];
+
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int n = lane & 15, g = lane >> 4;
+  const int64_t hgroups = a.heads / G;
+  const int64_t b = blockIdx.y / hgroups, h0 = (blockIdx.y % hgroups) * G;
+  const int64_t hk = h0 / (a.heads / a.kv_heads);
+  const int64_t ctx = min<int64_t>(a.ctx_lens[b], a.max_blocks * a.bs);
+  const int64_t t0 = (int64_t)blockIdx.x * a.split;
+  const int64_t t1 = min<int64_t>(t0 + a.split, ctx);
+  const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
+  {  // block-table slice -> cache rows (-1: no block / past the split)
+    const uint32_t bs = (uint32_t)a.bs;
+    const uint32_t lb0 = (uint32_t)(t0 / a.bs);
+    const int nlb = ntok > 0 ? (int)((uint32_t)(t1 - 1) / bs - lb0 + 1) : 0;
+    const int32_t *tab = a.table + b * a.max_blocks + lb0;
+    for (int j = threadIdx.x; j < nlb; j += kBlock) blks[j] = tab[j];
+    __syncthreads();
+    const int32_t head_row0 = (int32_t)((a.layer * a.kv_heads + hk) * a.bs);
+    const int32_t blk_rows = (int32_t)(a.layers * a.kv_heads * a.bs);
+    const int npad = (ntok + kMfmaStep - 1) / kMfmaStep * kMfmaStep;
+    for (int i = threadIdx.x; i < npad; i += kBlock) {
+      int32_t row = -1;
+      if (i < ntok) {
+        const uint32_t pos = (uint32_t)(t0 + i);
+        const uint32_t lb = pos / bs;
+        const int32_t blk = blks[lb - lb0];
+        if (blk >= 0) row = blk * blk_rows + head_row0 + (int32_t)(pos - lb * bs);
+      }
+      rows[i] = row;
+    }
+  }
+  {
+    uint32_t dq, dt, n1 = 0, n2 = 0;
+    h84_decode4(threadIdx.x, dq, dt, n1, n2);  // kBlock == 256: one table entry per thread
+    lut[threadIdx.x] = (uint8_t)(dq & 0xFu);
+  }
+  // Q^T operand (B): column n = head h0 + n, k-slot 8g + j of MFMA kk = d (D/4)g + 8kk + j
+  f16x8 qop[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (n < G)
+      v = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const __half *>(a.q) +
+                                           (b * a.heads + h0 + n) * D + KB * g + 8 * kk);
+    qop[kk] = __builtin_bit_cast(f16x8, v);
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.k_cache), 0, (int)a.cache_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t vrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.v_cache), 0, (int)a.cache_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t ksrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.k_scales), 0, (int)a.scale_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t vsrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v_scales), 0, (int)a.scale_bytes, kRsrcWord3);
+  const float qscale = a.sm_scale * kAttnLogScale;
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float m = -INFINITY, l = 0.0f;
+
+  for (int i0 = wave * kMfmaStep; i0 < ntok; i0 += kWaves * kMfmaStep) {
+    // ---- loads: 2 K rows (tokens i0 + n, i0 + 16 + n), 8 V rows and scales
+    // (tokens i0 + 16(j >> 2) + 4g + (j & 3)); invalid rows read row 0, masked
+    int32_t rv[8];
+    {
+      const int4 r0 = *reinterpret_cast<const int4 *>(&rows[i0 + 4 * g]);
+      const int4 r1 = *reinterpret_cast<const int4 *>(&rows[i0 + 16 + 4 * g]);
+      rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+      rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+    }
+    uint32_t kw[2][KB / 4 > 0 ? KB / 4 : 1];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau) {
+      const int32_t r = rows[i0 + 16 * tau + n];
+      load_chunk<KB>(krs, (uint32_t)max(r, 0) * (uint32_t)D + (uint32_t)(KB * g), kw[tau]);
+    }
+    uint32_t vw[8][VW];
+    float ks[8], vs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t r = (uint32_t)max(rv[j], 0);
+      load_chunk<MT>(vrs, r * (uint32_t)D + (uint32_t)(MT * n), vw[j]);
+      ks[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, r * 4u, 0, 0));
+      vs[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, r * 4u, 0, 0));
+    }
+    // ---- S^T = K . Q^T, two 16-token tiles
+    f32x4 S[2];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau) {
+      S[tau] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        uint32_t p[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {  // bytes 8kk + 2h, 8kk + 2h + 1
+          const uint32_t w = kw[tau][2 * kk + h / 2];
+          const int sh = 16 * (h & 1);
+          p[h] = nib_pair_f16(lut[(w >> sh) & 0xFFu], lut[(w >> (sh + 8)) & 0xFFu]);
+        }
+        S[tau] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, u32x4{p[0], p[1], p[2], p[3]}),
+                                                        qop[kk], S[tau], 0, 0, 0);
+      }
+    }
+    // ---- online softmax over this lane's 8 tokens of head n
+    float s[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] = rv[j] >= 0 ? S[j >> 2][j & 3] * (qscale * ks[j]) : -INFINITY;
+      mx = fmaxf(mx, s[j]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    const float mn = fmaxf(m, mx);
+    const float mu = mn == -INFINITY ? 0.0f : mn;  // no valid token yet: nothing to scale
+    const float alpha = attn_exp(m - mu);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] *= alpha;
+    uint32_t phi[4], plo[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float p0 = attn_exp(s[2 * h] - mu), p1 = attn_exp(s[2 * h + 1] - mu);
+      l += p0 + p1;
+      const float w0 = p0 * vs[2 * h], w1 = p1 * vs[2 * h + 1];
+      const auto hi = __builtin_amdgcn_cvt_pkrtz(w0, w1);
+      const auto lo = __builtin_amdgcn_cvt_pkrtz(w0 - (float)hi[0], w1 - (float)hi[1]);
+      phi[h] = __builtin_bit_cast(uint32_t, hi);
+      plo[h] = __builtin_bit_cast(uint32_t, lo);
+    }
+    const f16x8 pb_hi = __builtin_bit_cast(f16x8, u32x4{phi[0], phi[1], phi[2], phi[3]});
+    const f16x8 pb_lo = __builtin_bit_cast(f16x8, u32x4{plo[0], plo[1], plo[2], plo[3]});
+    // ---- O^T += V^T . P: M-tile mt takes byte mt of each token's chunk
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      uint32_t p[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {  // tokens j = 2h, 2h + 1
+        const int sh = 8 * (mt & 3);
+        p[h] = nib_pair_f16(lut[(vw[2 * h][mt / 4] >> sh) & 0xFFu], lut[(vw[2 * h + 1][mt / 4] >> sh) & 0xFFu]);
+      }
+      const f16x8 va = __builtin_bit_cast(f16x8, u32x4{p[0], p[1], p[2], p[3]});
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb_hi, acc[mt], 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb_lo, acc[mt], 0, 0, 0);
+    }
+  }
+
+  // ---- merge: the 4 lanes of a head, then the workgroup's waves
+  l += __shfl_xor(l, 16, kWave);
+  l += __shfl_xor(l, 32, kWave);
+  if (n < G) {
+    if (g == 0) {
+      gml[0][wave][n] = m;
+      gml[1][wave][n] = l;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wave][n][MT * (4 * g + r) + mt] = acc[mt][r];
+  }
+  __syncthreads();
+  const int64_t ws_stride = a.nsplit * (a.d + 2);
+  float *ws0 = a.ws + ((b * a.heads + h0) * a.nsplit + blockIdx.x) * (a.d + 2);
+  for (int idx = threadIdx.x; idx < G * D; idx += kBlock) {
+    const int h = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) M = fmaxf(M, gml[0][w][h]);
+    float o = 0.0f, L = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const float mw = gml[0][w][h];
+      const float wt = mw == -INFINITY ? 0.0f : attn_exp(mw - M);
+      o += red[w][h][d] * wt;
+      L += gml[1][w][h] * wt;
+    }
+    float *ws = ws0 + h * ws_stride;
+    ws[2 + d] = o;
+    if (d == 0) {
+      ws[0] = M;
+      ws[1] = L;
+    }
+  }
+}
+
 // combine the splits of one (b, h): out = sum_s acc_s e^(m_s - M) / sum_s l_s e^(m_s - M)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) {
@@ -694,6 +964,39 @@ static int launch_attn(const AttnArgs &a, int64_t batch, int gq, hipStream_t st)
   return KVECC_OK;
 }
 
+template <int D>
+static int launch_mfma_d(const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
+  const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads / gm));
+  switch (gm) {
+    case 2: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 2>), grid, dim3(kBlock), 0, st, a); break;
+    case 4: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 4>), grid, dim3(kBlock), 0, st, a); break;
+    case 8: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 8>), grid, dim3(kBlock), 0, st, a); break;
+    default: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 16>), grid, dim3(kBlock), 0, st, a); break;
+  }
+  KVECC_LAUNCH(paged_attn_combine_kernel<__half>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
+  return KVECC_OK;
+}
+
+static int launch_mfma(const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
+  switch (a.d) {
+    case 32: return launch_mfma_d<32>(a, batch, gm, st);
+    case 64: return launch_mfma_d<64>(a, batch, gm, st);
+    default: return launch_mfma_d<128>(a, batch, gm, st);
+  }
+}
+
+// query heads per workgroup of the MFMA kernel (0: not applicable): Hamming(8,4)
+// caches under 4 GiB, fp16 queries (16-byte aligned), head_dim 32 / 64 / 128, a
+// group of >= 2 query heads per cache head
+static int attn_mfma_heads(int codec, int q_dtype, const void *query, int64_t d, int64_t heads,
+                           int64_t kv_heads, bool buf) {
+  const int64_t group = heads / kv_heads;
+  if (!KVECC_ATTN_MFMA || codec != KVECC_CODEC_H84 || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) ||
+      (d != 32 && d != 64 && d != 128) || group < 2)
+    return 0;
+  return group % 16 == 0 ? 16 : group % 8 == 0 ? 8 : group % 4 == 0 ? 4 : group % 2 == 0 ? 2 : 0;
+}
+
 template <typename T>
 static int launch_codec(int codec, const AttnArgs &a, int64_t batch, int gq, hipStream_t st) {
   switch (codec) {
@@ -709,12 +1012,12 @@ static int launch_codec(int codec, const AttnArgs &a, int64_t batch, int gq, hip
 #ifndef KVECC_ATTN_WG_PER_CU
 #define KVECC_ATTN_WG_PER_CU 4
 #endif
-static int64_t choose_split(int64_t bh, int64_t max_context_len) {
+static int64_t choose_split(int64_t bh, int64_t max_context_len, int per_cu = KVECC_ATTN_WG_PER_CU) {
   // longer splits amortise each workgroup's fixed work (table staging, the
   // group merge); measured best at 1024 for both codecs at [8,4096,32,128]
   const int64_t top = kMaxSplit;
   int64_t split = top;
-  const int64_t want = (int64_t)KVECC_ATTN_WG_PER_CU * cu_count();
+  const int64_t want = (int64_t)per_cu * cu_count();
   while (split > 32 && bh * cdiv(max_context_len, split) < want) split >>= 1;
   while (cdiv(max_context_len, split) > kMaxSplits && split < top) split <<= 1;
   return split;
@@ -789,7 +1092,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.max_blocks = max_blocks;
   a.sm_scale = sm_scale;
   a.empty_value = codec == KVECC_CODEC_H84 ? -8.0f : 0.0f;
-  int gq = 1;
+  int gq = 1, gm = 0;
   {
     const int64_t rows_total = num_blocks * num_layers * kv_heads * block_size;
     const int64_t cb = rows_total * (codec == KVECC_CODEC_H84            ? head_dim
@@ -799,8 +1102,13 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     a.cache_bytes = fits ? (uint32_t)cb : 0u;  // 0 selects the 64-bit-addressed kernels
     a.scale_bytes = fits ? (uint32_t)(rows_total * 4) : 0u;
     gq = attn_heads_per_wg(codec, head_dim, a.g, heads, kv_heads, fits);
+    gm = attn_mfma_heads(codec, q_dtype, query, head_dim, heads, kv_heads, fits);
   }
-  a.split = choose_split(batch * heads / gq, max_context_len);
+  if (gm)  // KVECC_ATTN_MFMA_WG_PER_CU workgroups per CU, never finer than the workspace allows
+    a.split = std::max(choose_split(batch * heads / gm, max_context_len, KVECC_ATTN_MFMA_WG_PER_CU),
+                       choose_split(std::max<int64_t>(1, batch * heads / 4), max_context_len));
+  else
+    a.split = choose_split(batch * heads / gq, max_context_len);
   a.nsplit = cdiv(max_context_len, a.split);
   if (a.nsplit > kMaxSplits)
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
@@ -813,6 +1121,11 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     if (!a.par || !a.cor || !a.atab) return KVECC_EHIP;
   }
   hipStream_t st = as_stream(stream);
+  if (gm) {
+    const int rc = launch_mfma(a, batch, gm, st);
+    if (rc != KVECC_OK) return rc;
+    return check_launch("paged_attention");
+  }
   int rc;
   switch (q_dtype) {
     case KVECC_F32: rc = launch_codec<float>(codec, a, batch, gq, st); break;

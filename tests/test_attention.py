@@ -86,7 +86,11 @@ CASES = [("hamming84", 2, 4, 4, 64, 300, 0.01), ("hamming84", 1, 12, 12, 64, 102
          ("hamming84", 3, 8, 2, 128, 700, 0.02), ("golay", 2, 4, 4, 128, 513, 0.02),
          ("golay", 1, 6, 3, 64, 77, 0.0), ("hamming84", 1, 2, 1, 32, 5, 0.05),
          # head_dim % 16 != 0: one-dword lane chunks (VEC 1) through the buffer-load kernel
-         ("hamming84", 2, 4, 2, 100, 333, 0.01), ("hamming84", 1, 3, 3, 20, 90, 0.02)]
+         ("hamming84", 2, 4, 2, 100, 333, 0.01), ("hamming84", 1, 3, 3, 20, 90, 0.02),
+         # GQA groups of 8 / 16 / 2 query heads at head_dim 64 / 128 / 32 (fp16
+         # queries: the matrix-core kernel; fp32: the VALU kernels)
+         ("hamming84", 2, 16, 2, 64, 257, 0.01), ("hamming84", 1, 32, 2, 128, 1000, 0.01),
+         ("hamming84", 2, 8, 4, 32, 100, 0.0)]
 
 
 @pytest.mark.parametrize("codec,batch,heads,kvh,d,ctx,ber", CASES)

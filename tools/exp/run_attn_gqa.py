@@ -11,7 +11,7 @@ import torch  # noqa: E402
 from kvecc import _lib  # noqa: E402
 VP, I64 = ctypes.c_void_p, ctypes.c_int64
 libs = {"prod": _lib.load()}
-for name in os.environ.get("LIBS", "nogqa").split(","):
+for name in os.environ.get("LIBS", "nomfma").split(","):
     libs[name] = ctypes.CDLL(os.path.join(HERE, f"libattn_{name}.so"))
 for l in libs.values():
     l.kvecc_paged_attention.argtypes = [VP, ctypes.c_int, VP, VP, VP, VP, VP, VP, VP, I64, I64, I64, I64, I64,
