@@ -127,6 +127,8 @@ struct AttnArgs {
   float empty_value;          // output when a (b, h) has no valid token
   const uint16_t *par, *cor;  // Golay tables
   const uint32_t *atab;       // Golay spread tables (KVECC_ATTN_GOLAY_SPREAD)
+  uint32_t *ctr;              // per-(batch, head group) split counters (attn_counter_slot), or
+                              // null: a separate combine launch
 };
 
 // Lane chunk c of a token row: VEC 32-bit words = 4*VEC H(8,4) codewords, or
@@ -277,6 +279,93 @@ __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
   if (E % 2) acc[E - 1] = fmaf(p, v[E - 1], acc[E - 1]);
 }
 
+// Workspace entries under the fused combine are read by a workgroup that may
+// sit on another XCD (another L2): they are written and read as agent-scope
+// relaxed atomics (global_store / global_load sc1, coherent at the memory side)
+// -- an agent-scope fence would write back and invalidate the whole L2
+// (buffer_wbl2 / buffer_inv sc1), which measured 4x the kernel's time.
+__device__ __forceinline__ void ws_put(float *p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool COHERENT>
+__device__ __forceinline__ float ws_get(const float *p) {
+  if (COHERENT) return __hip_atomic_load(const_cast<float *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
+// combine the splits of one (b, h): out = sum_s acc_s e^(m_s - M) / sum_s l_s e^(m_s - M)
+// (one workgroup; wt holds kMaxSplits floats, bred kBlock / kWave).  A one-pass
+// per-thread form (each thread folding every split online, one thread per
+// output value) measured slower: 29.5 vs 22.7 us per 32q/8kv call.
+template <typename T, bool COHERENT = false>
+__device__ void combine_bh(const AttnArgs &a, int64_t bh, float *wt, float *bred) {
+  const int64_t stride = a.d + 2;
+  const float *ws = a.ws + bh * a.nsplit * stride;
+  float mx = -INFINITY;
+  for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) mx = fmaxf(mx, ws_get<COHERENT>(ws + s * stride));
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0) bred[threadIdx.x / kWave] = mx;
+  __syncthreads();
+  mx = bred[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / kWave; ++w) mx = fmaxf(mx, bred[w]);
+  __syncthreads();
+  float L = 0.0f;
+  for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) {
+    const float ms = ws_get<COHERENT>(ws + s * stride);
+    const float w = ms == -INFINITY ? 0.0f : attn_exp(ms - mx);
+    wt[s] = w;
+    L += w * ws_get<COHERENT>(ws + s * stride + 1);
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) L += __shfl_xor(L, off, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) bred[threadIdx.x / kWave] = L;
+  __syncthreads();
+  L = 0.0f;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) L += bred[w];
+  T *out = reinterpret_cast<T *>(a.out) + bh * a.d;
+  for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int64_t s = 0; s < a.nsplit; ++s) acc += ws_get<COHERENT>(ws + s * stride + 2 + di) * wt[s];
+    out[di] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);  // no valid token: see the header
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) {
+  __shared__ float wt[kMaxSplits];
+  __shared__ float bred[kBlock / kWave];
+  combine_bh<T>(a, blockIdx.x, wt, bred);
+}
+
+// Fused combine: the workgroup that finishes the last split of its (batch, head
+// group) -- counted on a.ctr[blockIdx.y] -- combines the group's G query heads
+// and resets the counter, saving the combine launch.  The workspace stores are
+// sc1 (ws_put) and every thread waits for its own before the count; the last
+// workgroup reads the entries with sc1 loads.  wt: kMaxSplits floats of LDS the
+// caller no longer needs.
+template <typename T, int G>
+__device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
+  __shared__ float bred[kBlock / kWave];
+  __shared__ uint32_t last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's sc1 workspace stores performed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.ctr + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev + 1 == gridDim.x;
+    if (last) __hip_atomic_store(a.ctr + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  for (int j = 0; j < G; ++j) {
+    if (j) __syncthreads();
+    combine_bh<T, true>(a, bh0 + j, wt, bred);
+  }
+}
+
 #ifndef KVECC_ATTN_GQA_PREFETCH
 #define KVECC_ATTN_GQA_PREFETCH 1
 #endif
@@ -336,7 +425,10 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
     int32_t *blks = kSpread ? reinterpret_cast<int32_t *>(gtab) : blks_own;
     const uint32_t bs = (uint32_t)a.bs;
     const uint32_t lb0 = (uint32_t)(t0 / a.bs);
-    const int nlb = ntok > 0 ? (int)((uint32_t)(t1 - 1) / bs - lb0 + 1) : 0;
+    // the whole split's slice, bounded by the table rather than the context, so
+    // the load does not wait for context_lens (one dependent HBM trip fewer)
+    const int64_t tmax = min<int64_t>(t0 + a.split, a.max_blocks * a.bs);
+    const int nlb = tmax > t0 ? (int)((uint32_t)(tmax - 1) / bs - lb0 + 1) : 0;
     const int32_t *tab = a.table + b * a.max_blocks + lb0;
     for (int j = threadIdx.x; j < nlb; j += kBlock) blks[j] = tab[j];
     __syncthreads();
@@ -543,15 +635,16 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
     for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
       float sum = 0.0f;
       for (int gi = 0; gi < TP; ++gi) sum += red[gi * W * E + di] * gw[gi];
-      ws[2 + di] = sum;
+      ws_put(ws + 2 + di, sum);
     }
     if (threadIdx.x == 0) {
       float L = 0.0f;
       for (int gi = 0; gi < TP; ++gi) L += gml[1][gi] * gw[gi];
-      ws[0] = M;
-      ws[1] = L;
+      ws_put(ws, M);
+      ws_put(ws + 1, L);
     }
   }
+  if (a.ctr) combine_if_last<T, G>(a, b * a.heads + h0, reinterpret_cast<float *>(rows));
 }
 
 // ---- GQA on the matrix cores (Hamming(8,4), fp16 queries) -----------------------
@@ -587,6 +680,16 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
 #ifndef KVECC_ATTN_MFMA
 #define KVECC_ATTN_MFMA 1
 #endif
+// the last split of each (batch, head group) combines it (combine_if_last);
+// 0: a separate combine launch
+#ifndef KVECC_ATTN_FUSED_COMBINE
+#define KVECC_ATTN_FUSED_COMBINE 1
+#endif
+// 1: issue the next step's loads before this step's math (191 VGPRs at D = 128:
+// 2 waves per SIMD; 32q/8kv measured 29.8 us against 22.9 without)
+#ifndef KVECC_ATTN_MFMA_PREFETCH
+#define KVECC_ATTN_MFMA_PREFETCH 0
+#endif
 #ifndef KVECC_ATTN_MFMA_WG_PER_CU
 #define KVECC_ATTN_MFMA_WG_PER_CU 4
 #endif
@@ -595,8 +698,20 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMfmaStep = 32;  // tokens per wave step
 
-// two table values (data nibbles 0..15) -> f16 pair (n - 8), lo in bits 0..15
+// Decoded values as MFMA operands.  KVECC_ATTN_MFMA_SUBNORM (default): the
+// table's nibble n (0..15) goes into an f16 half as is -- the subnormal
+// n * 2^-24, exact -- so a pair costs one v_perm; the kernel scales the
+// products by 2^24 and folds the -8 out as -8 * sum(q) (scores) and
+// -8 * sum(p) (outputs).  0: f16 1024 + n by an OR of 0x6400, then one
+// v_pk_add_f16 of -1032 per pair: (n - 8) itself.
+#ifndef KVECC_ATTN_MFMA_SUBNORM
+#define KVECC_ATTN_MFMA_SUBNORM 1
+#endif
+constexpr float kMfmaValScale = KVECC_ATTN_MFMA_SUBNORM ? 16777216.0f : 1.0f;  // 2^24
+constexpr float kMfmaValOffset = KVECC_ATTN_MFMA_SUBNORM ? 8.0f : 0.0f;
+// two table values (data nibbles 0..15) -> f16 operand pair, lo in bits 0..15
 __device__ __forceinline__ uint32_t nib_pair_f16(uint32_t lo, uint32_t hi) {
+  if (KVECC_ATTN_MFMA_SUBNORM) return __builtin_amdgcn_perm(hi, lo, 0x0c040c00u);  // [0, hi, 0, lo]
   const f16x2 h = __builtin_bit_cast(f16x2, (lo | hi << 16) | 0x64006400u);  // 1024 + n
   return __builtin_bit_cast(uint32_t, h + f16x2{(_Float16)-1032.0f, (_Float16)-1032.0f});
 }
@@ -649,7 +764,10 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
   {  // block-table slice -> cache rows (-1: no block / past the split)
     const uint32_t bs = (uint32_t)a.bs;
     const uint32_t lb0 = (uint32_t)(t0 / a.bs);
-    const int nlb = ntok > 0 ? (int)((uint32_t)(t1 - 1) / bs - lb0 + 1) : 0;
+    // the whole split's slice, bounded by the table rather than the context, so
+    // the load does not wait for context_lens (one dependent HBM trip fewer)
+    const int64_t tmax = min<int64_t>(t0 + a.split, a.max_blocks * a.bs);
+    const int nlb = tmax > t0 ? (int)((uint32_t)(tmax - 1) / bs - lb0 + 1) : 0;
     const int32_t *tab = a.table + b * a.max_blocks + lb0;
     for (int j = threadIdx.x; j < nlb; j += kBlock) blks[j] = tab[j];
     __syncthreads();
@@ -682,6 +800,15 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
                                            (b * a.heads + h0 + n) * D + KB * g + 8 * kk);
     qop[kk] = __builtin_bit_cast(f16x8, v);
   }
+  float qsum = 0.0f;  // sum of head n's query over all d (the offset fold)
+  if (KVECC_ATTN_MFMA_SUBNORM) {
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qsum += (float)qop[kk][e];
+    qsum += __shfl_xor(qsum, 16, kWave);
+    qsum += __shfl_xor(qsum, 32, kWave);
+  }
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t krs =
@@ -697,32 +824,51 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   float m = -INFINITY, l = 0.0f;
+  float psum = 0.0f;  // sum of p * v_scale over this lane's tokens (the offset fold)
+  const float qoff = kMfmaValOffset * qsum;
 
-  for (int i0 = wave * kMfmaStep; i0 < ntok; i0 += kWaves * kMfmaStep) {
-    // ---- loads: 2 K rows (tokens i0 + n, i0 + 16 + n), 8 V rows and scales
-    // (tokens i0 + 16(j >> 2) + 4g + (j & 3)); invalid rows read row 0, masked
+  // one step's operands in registers: 2 K rows (tokens i0 + n, i0 + 16 + n),
+  // 8 V rows and scales (tokens i0 + 16(j >> 2) + 4g + (j & 3)); invalid rows
+  // read row 0 and are masked
+  struct Step {
     int32_t rv[8];
-    {
-      const int4 r0 = *reinterpret_cast<const int4 *>(&rows[i0 + 4 * g]);
-      const int4 r1 = *reinterpret_cast<const int4 *>(&rows[i0 + 16 + 4 * g]);
-      rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
-      rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
-    }
     uint32_t kw[2][KB / 4 > 0 ? KB / 4 : 1];
+    uint32_t vw[8][VW];
+    float ks[8], vs[8];
+  };
+  auto load_step = [&](int i0, Step &st) {
+    const int4 r0 = *reinterpret_cast<const int4 *>(&rows[i0 + 4 * g]);
+    const int4 r1 = *reinterpret_cast<const int4 *>(&rows[i0 + 16 + 4 * g]);
+    st.rv[0] = r0.x; st.rv[1] = r0.y; st.rv[2] = r0.z; st.rv[3] = r0.w;
+    st.rv[4] = r1.x; st.rv[5] = r1.y; st.rv[6] = r1.z; st.rv[7] = r1.w;
 #pragma unroll
     for (int tau = 0; tau < 2; ++tau) {
       const int32_t r = rows[i0 + 16 * tau + n];
-      load_chunk<KB>(krs, (uint32_t)max(r, 0) * (uint32_t)D + (uint32_t)(KB * g), kw[tau]);
+      load_chunk<KB>(krs, (uint32_t)max(r, 0) * (uint32_t)D + (uint32_t)(KB * g), st.kw[tau]);
     }
-    uint32_t vw[8][VW];
-    float ks[8], vs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const uint32_t r = (uint32_t)max(rv[j], 0);
-      load_chunk<MT>(vrs, r * (uint32_t)D + (uint32_t)(MT * n), vw[j]);
-      ks[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, r * 4u, 0, 0));
-      vs[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, r * 4u, 0, 0));
+      const uint32_t r = (uint32_t)max(st.rv[j], 0);
+      load_chunk<MT>(vrs, r * (uint32_t)D + (uint32_t)(MT * n), st.vw[j]);
+      st.ks[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, r * 4u, 0, 0));
+      st.vs[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, r * 4u, 0, 0));
     }
+  };
+  constexpr int kStride = kWaves * kMfmaStep;
+  Step nxt;
+  if (KVECC_ATTN_MFMA_PREFETCH && wave * kMfmaStep < ntok) load_step(wave * kMfmaStep, nxt);
+  for (int i0 = wave * kMfmaStep; i0 < ntok; i0 += kStride) {
+    Step cur;
+    if (KVECC_ATTN_MFMA_PREFETCH) {
+      cur = nxt;
+      if (i0 + kStride < ntok) load_step(i0 + kStride, nxt);  // next step's loads fly during this one
+    } else {
+      load_step(i0, cur);
+    }
+    const int32_t *rv = cur.rv;
+    const float *ks = cur.ks, *vs = cur.vs;
+    auto &kw = cur.kw;
+    auto &vw = cur.vw;
     // ---- S^T = K . Q^T, two 16-token tiles
     f32x4 S[2];
 #pragma unroll
@@ -746,7 +892,7 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      s[j] = rv[j] >= 0 ? S[j >> 2][j & 3] * (qscale * ks[j]) : -INFINITY;
+      s[j] = rv[j] >= 0 ? (S[j >> 2][j & 3] * kMfmaValScale - qoff) * (qscale * ks[j]) : -INFINITY;
       mx = fmaxf(mx, s[j]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
@@ -756,6 +902,7 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
     const float alpha = attn_exp(m - mu);
     m = mn;
     l *= alpha;
+    psum *= alpha;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] *= alpha;
     uint32_t phi[4], plo[4];
@@ -764,6 +911,7 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
       const float p0 = attn_exp(s[2 * h] - mu), p1 = attn_exp(s[2 * h + 1] - mu);
       l += p0 + p1;
       const float w0 = p0 * vs[2 * h], w1 = p1 * vs[2 * h + 1];
+      psum += w0 + w1;
       const auto hi = __builtin_amdgcn_cvt_pkrtz(w0, w1);
       const auto lo = __builtin_amdgcn_cvt_pkrtz(w0 - (float)hi[0], w1 - (float)hi[1]);
       phi[h] = __builtin_bit_cast(uint32_t, hi);
@@ -789,6 +937,9 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
   // ---- merge: the 4 lanes of a head, then the workgroup's waves
   l += __shfl_xor(l, 16, kWave);
   l += __shfl_xor(l, 32, kWave);
+  psum += __shfl_xor(psum, 16, kWave);
+  psum += __shfl_xor(psum, 32, kWave);
+  const float poff = kMfmaValOffset * psum;
   if (n < G) {
     if (g == 0) {
       gml[0][wave][n] = m;
@@ -797,7 +948,7 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[wave][n][MT * (4 * g + r) + mt] = acc[mt][r];
+      for (int r = 0; r < 4; ++r) red[wave][n][MT * (4 * g + r) + mt] = acc[mt][r] * kMfmaValScale - poff;
   }
   __syncthreads();
   const int64_t ws_stride = a.nsplit * (a.d + 2);
@@ -816,53 +967,18 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
       L += gml[1][w][h] * wt;
     }
     float *ws = ws0 + h * ws_stride;
-    ws[2 + d] = o;
+    ws_put(ws + 2 + d, o);
     if (d == 0) {
-      ws[0] = M;
-      ws[1] = L;
+      ws_put(ws, M);
+      ws_put(ws + 1, L);
     }
   }
+  if (a.ctr) combine_if_last<__half, G>(a, b * a.heads + h0, reinterpret_cast<float *>(rows));
 }
 
-// combine the splits of one (b, h): out = sum_s acc_s e^(m_s - M) / sum_s l_s e^(m_s - M)
 template <typename T>
-__global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) {
-  __shared__ float wt[kMaxSplits];
-  __shared__ float bred[kBlock / kWave];
-  const int64_t bh = blockIdx.x;
-  const int64_t stride = a.d + 2;
-  const float *ws = a.ws + bh * a.nsplit * stride;
-  float mx = -INFINITY;
-  for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) mx = fmaxf(mx, ws[s * stride]);
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
-  if ((threadIdx.x & (kWave - 1)) == 0) bred[threadIdx.x / kWave] = mx;
-  __syncthreads();
-  mx = bred[0];
-#pragma unroll
-  for (int w = 1; w < kBlock / kWave; ++w) mx = fmaxf(mx, bred[w]);
-  __syncthreads();
-  float L = 0.0f;
-  for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) {
-    const float ms = ws[s * stride];
-    const float w = ms == -INFINITY ? 0.0f : attn_exp(ms - mx);
-    wt[s] = w;
-    L += w * ws[s * stride + 1];
-  }
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) L += __shfl_xor(L, off, kWave);
-  if ((threadIdx.x & (kWave - 1)) == 0) bred[threadIdx.x / kWave] = L;
-  __syncthreads();
-  L = 0.0f;
-#pragma unroll
-  for (int w = 0; w < kBlock / kWave; ++w) L += bred[w];
-  T *out = reinterpret_cast<T *>(a.out) + bh * a.d;
-  for (int64_t di = threadIdx.x; di < a.d; di += kBlock) {
-    float acc = 0.0f;
-#pragma unroll 4
-    for (int64_t s = 0; s < a.nsplit; ++s) acc += ws[s * stride + 2 + di] * wt[s];
-    out[di] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);  // no valid token: see the header
-  }
+static void launch_combine(const AttnArgs &a, int64_t batch, hipStream_t st) {
+  KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
 }
 
 static int pow2_at_least(int64_t x) {
@@ -960,7 +1076,7 @@ static int launch_attn(const AttnArgs &a, int64_t batch, int gq, hipStream_t st)
     rc = launch_split_g<T, CODEC, kGolayPackedVec>(a, batch, gq, st);  // 4 codewords per lane: 43 -> 11 of 16
   }
   if (rc != KVECC_OK) return rc;
-  KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
+  if (!a.ctr) launch_combine<T>(a, batch, st);
   return KVECC_OK;
 }
 
@@ -973,7 +1089,7 @@ static int launch_mfma_d(const AttnArgs &a, int64_t batch, int gm, hipStream_t s
     case 8: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 8>), grid, dim3(kBlock), 0, st, a); break;
     default: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 16>), grid, dim3(kBlock), 0, st, a); break;
   }
-  KVECC_LAUNCH(paged_attn_combine_kernel<__half>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
+  if (!a.ctr) launch_combine<__half>(a, batch, st);
   return KVECC_OK;
 }
 
@@ -1114,6 +1230,13 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
   a.par = a.cor = nullptr;
   a.atab = nullptr;
+  a.ctr = nullptr;
+  // fused combine for one query head per workgroup only: with G heads the last
+  // workgroup's G serial combines became a tail (32q/8kv MFMA 23.6 -> 32.8 us)
+  if (KVECC_ATTN_FUSED_COMBINE && !gm && gq == 1 && batch * heads <= kAttnCtrPerSlot) {
+    a.ctr = attn_counter_slot();
+    if (!a.ctr) return KVECC_EHIP;
+  }
   if (codec != KVECC_CODEC_H84) {
     a.par = golay_parity_table_dev();
     a.cor = golay_correct_table_dev();

@@ -485,7 +485,7 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
 // bases 64-bit and wave-uniform (descriptors in SGPRs).
 // dynamic tail schedule (kvecc_internal.h TileSchedule), as the fused reads
 #ifndef KVECC_GOLAY_ROWS_DYN
-#define KVECC_GOLAY_ROWS_DYN 0
+#define KVECC_GOLAY_ROWS_DYN 1
 #endif
 constexpr int kRegBlock = 512;
 constexpr int kRegWaves = kRegBlock / kWave;

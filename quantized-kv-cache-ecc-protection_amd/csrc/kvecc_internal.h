@@ -52,6 +52,12 @@ constexpr int kDynStride = 64;  // uint32 words (256 B) between counters
 constexpr int kDynSlots = 64;
 constexpr int kDynSlotWords = kDynCounters * kDynStride;
 uint32_t *shim_dyn_slot();
+// Split counters of the paged-attention kernels (one per (batch, head group);
+// the split that finishes a group combines it and resets the counter): a ring
+// of kAttnCtrSlots slots of kAttnCtrPerSlot zeroed counters per device.
+constexpr int kAttnCtrSlots = 32;
+constexpr int kAttnCtrPerSlot = 4096;
+uint32_t *attn_counter_slot();
 // host-side table builders (product copy, independent of the test oracle)
 void build_golay_parity_table(uint16_t *out4096);
 void build_golay_correct_table(uint16_t *out4096);

@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
 #define KVECC_PACKED_DEC_V2 1
 #endif
 #ifndef KVECC_PACKED_DEC_V2_PER_CU
-#define KVECC_PACKED_DEC_V2_PER_CU 3
+#define KVECC_PACKED_DEC_V2_PER_CU 2
 #endif
 #ifndef KVECC_PACKED_DEC_DYN
 #define KVECC_PACKED_DEC_DYN 1
@@ -476,7 +476,7 @@ __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4
 // issued together and the next tile's before this one's stores, over a
 // persistent grid with the fused reads' dynamic tail (TileSchedule).
 #ifndef KVECC_H84_PACKED_V2
-#define KVECC_H84_PACKED_V2 1
+#define KVECC_H84_PACKED_V2 0
 #endif
 #ifndef KVECC_H84_PACKED_CHUNKS
 #define KVECC_H84_PACKED_CHUNKS 4

@@ -41,6 +41,8 @@ static std::atomic<uint32_t *> g_attn[kMaxDev];
 static std::atomic<uint8_t *> g_pk[kMaxDev];
 static std::atomic<uint32_t *> g_dyn[kMaxDev];  // kDynSlots work-counter slots, zeroed
 static std::atomic<uint32_t> g_dyn_next[kMaxDev];
+static std::atomic<uint32_t *> g_actr[kMaxDev];  // kAttnCtrSlots attention split counters, zeroed
+static std::atomic<uint32_t> g_actr_next[kMaxDev];
 
 int current_device() {
   int d = 0;
@@ -156,10 +158,15 @@ static int ensure_tables(int d) {
   if (e == hipSuccess) e = hipMemcpy(buf, &host, sizeof(Host), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&dyn, dyn_bytes);
   if (e == hipSuccess) e = hipMemset(dyn, 0, dyn_bytes);
+  uint32_t *actr = nullptr;
+  const size_t actr_bytes = sizeof(uint32_t) * kAttnCtrSlots * kAttnCtrPerSlot;
+  if (e == hipSuccess) e = hipMalloc(&actr, actr_bytes);
+  if (e == hipSuccess) e = hipMemset(actr, 0, actr_bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return set_error(KVECC_EHIP, "golay table upload: %s", hipGetErrorString(e));
   g_dyn[d].store(dyn, std::memory_order_release);
+  g_actr[d].store(actr, std::memory_order_release);
   g_parity[d].store(buf->par, std::memory_order_release);
   g_correct[d].store(buf->cor, std::memory_order_release);
   g_pk[d].store(reinterpret_cast<uint8_t *>(buf->pk0), std::memory_order_release);
@@ -185,6 +192,13 @@ uint32_t *shim_dyn_slot() {
   if (!table_dev(g_attn)) return nullptr;  // allocated with the tables
   const uint32_t k = g_dyn_next[d].fetch_add(1, std::memory_order_relaxed) % kDynSlots;
   return g_dyn[d].load(std::memory_order_acquire) + (size_t)k * kDynSlotWords;
+}
+
+uint32_t *attn_counter_slot() {
+  const int d = current_device();
+  if (!table_dev(g_attn)) return nullptr;  // allocated with the tables
+  const uint32_t k = g_actr_next[d].fetch_add(1, std::memory_order_relaxed) % kAttnCtrSlots;
+  return g_actr[d].load(std::memory_order_acquire) + (size_t)k * kAttnCtrPerSlot;
 }
 
 }  // namespace kvecc
