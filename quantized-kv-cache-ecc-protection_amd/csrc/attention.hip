@@ -294,9 +294,11 @@ __device__ __forceinline__ float ws_get(const float *p) {
 }
 
 // combine the splits of one (b, h): out = sum_s acc_s e^(m_s - M) / sum_s l_s e^(m_s - M)
-// (one workgroup; wt holds kMaxSplits floats, bred kBlock / kWave).  A one-pass
-// per-thread form (each thread folding every split online, one thread per
-// output value) measured slower: 29.5 vs 22.7 us per 32q/8kv call.
+// (one workgroup; wt holds kMaxSplits floats, bred kBlock / kWave).  Two
+// "one memory round trip" forms measured slower per 32q/8kv call: every thread
+// folding all splits online, one thread per output value (29.5 vs 22.7 us), and
+// one wave per (b, h) with the weights by v_readlane (31.2 vs 22.5 us) -- fewer,
+// longer-lived waves each walking the splits serially.
 template <typename T, bool COHERENT = false>
 __device__ void combine_bh(const AttnArgs &a, int64_t bh, float *wt, float *bred) {
   const int64_t stride = a.d + 2;

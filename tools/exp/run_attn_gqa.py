@@ -3,6 +3,7 @@ head across G query heads) against libattn_nogqa.so (KVECC_ATTN_GQA=0, one
 workgroup per query head), interleaved, on [B=8, ctx=4096, D=128] with 32
 query heads over 32 (MHA), 16 and 8 cache heads, every codec.  Times are
 per API call (split + combine kernels, hipEvent markers), median of ROUNDS.
+Env: LIBS (other builds, libattn_<name>.so), ROUNDS, CTX, CODECS, HKVS.
 usage: python tools/exp/run_attn_gqa.py"""
 import ctypes, math, os, statistics, sys
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -20,7 +21,10 @@ for l in libs.values():
     l.kvecc_paged_attention_workspace.restype = I64
 ROUNDS = int(os.environ.get("ROUNDS", "30"))
 dev = torch.device("cuda:0")
-B, H, CTX, BS, D = 8, 32, 4096, 16, 128
+B, H, BS, D = 8, 32, 16, 128
+CTX = int(os.environ.get("CTX", "4096"))
+CODECS = os.environ.get("CODECS", "hamming84,golay,golay_packed").split(",")
+HKVS = [int(x) for x in os.environ.get("HKVS", "32,16,8").split(",")]
 g = torch.Generator(device=dev).manual_seed(0)
 nb = CTX // BS
 blocks = B * nb
@@ -35,8 +39,10 @@ G3 = (D + 2) // 3
 RB = _lib.golay_packed_row_bytes(G3)
 codecs = {"hamming84": (1, D, torch.uint8), "golay": (2, G3, torch.int32), "golay_packed": (3, RB, torch.uint8)}
 for codec, (cid, per, dt) in codecs.items():
+    if codec not in CODECS:
+        continue
     cid = {"hamming84": _lib.CODEC_H84, "golay": _lib.CODEC_GOLAY, "golay_packed": _lib.CODEC_GOLAY_PACKED}[codec]
-    for hkv in (32, 16, 8):
+    for hkv in HKVS:
         shape = (blocks, 1, hkv, BS * per)
         if dt == torch.int32:
             kc = torch.randint(0, 1 << 24, shape, dtype=dt, device=dev, generator=g)
@@ -71,5 +77,5 @@ for codec, (cid, per, dt) in codecs.items():
         line = " ".join(f"{n} {statistics.median(a.elapsed_time(b) * 1e3 for a, b in t):6.1f} us"
                         for n, t in times.items())
         med = statistics.median(a.elapsed_time(b) * 1e3 for a, b in times["prod"])
-        print(f"{codec:12s} H={H} Hkv={hkv:2d}: {line}  (prod {kv_bytes / med / 1e3:5.0f} GB/s of K+V cache)"
+        print(f"{codec:12s} ctx={CTX} H={H} Hkv={hkv:2d}: {line}  (prod {kv_bytes / med / 1e3:5.0f} GB/s of K+V cache)"
               f"  max|prod-{other}| {diff:.2e}", flush=True)

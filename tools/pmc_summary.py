@@ -6,6 +6,7 @@ separate --pmc passes.  The median over the profiled launches of each kernel
 is reported next to the kernel's algorithmic bytes.
 
 usage: python tools/pmc_summary.py gpurun_out/r01c profiles/r01
+       python tools/pmc_summary.py --variants gpurun_out/<tag> profiles/<round>/fused_variants
 """
 
 from __future__ import annotations
@@ -22,6 +23,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 M = 8 * 4096 * 32 * 43  # codewords of the bench workload
 ALGO = {"golay_decode_kernel": 8 * M, "golay_encode_kernel": 7 * M,
         "golay_decode_packed_kernel": 4.625 * M, "golay_decode_packed_staged_kernel": 4.625 * M,
+        "golay_decode_packed_wave_kernel": 4.625 * M,
         "golay_encode_packed_kernel": 4.5 * M,
         # per-head rows: 128 nibble bytes + 43 codewords per row
         "golay_encode_rows_reg_kernel": 300 * (M // 43), "golay_decode_rows_reg_kernel": 300 * (M // 43),
@@ -49,7 +51,44 @@ def counters(path):
     return per
 
 
+# fused-read variants traced one per run (tools/gpu_read_variants.sh): the
+# variant's algorithmic bytes per launch (K+V token rows of [8,4096,32,128])
+VARIANTS = {"golay": ("shim_read_golay_tiles_kernel", 432), "golay_packed": ("shim_read_golay_tiles_kernel", 389),
+            "hamming84": ("shim_read_bytes_tiles_kernel", 388), "hamming84_interp": ("shim_read_bytes_tiles_kernel", 388)}
+
+
+def variants(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    out = {"source": src, "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), WRITE_SIZE x1",
+           "driver": "tools/exp/run_read_ab.py, one variant per rocprofv3 run", "variants": {}}
+    for var, (kern, per_row) in VARIANTS.items():
+        d = os.path.join(src, var)
+        if not os.path.isdir(d):
+            continue
+        fetch = counters(glob.glob(os.path.join(d, "pmc_fetch", "*counter_collection.csv"))[0])
+        write = counters(glob.glob(os.path.join(d, "pmc_write", "*counter_collection.csv"))[0])
+        stats_csv = glob.glob(os.path.join(d, "prof", "*kernel_stats.csv"))[0]
+        shutil.copy(stats_csv, os.path.join(dst, var + "_kernel_stats.csv"))
+        stats = {r["Name"]: r for r in csv.DictReader(open(stats_csv))}
+        name = next(k for k in stats if kern in k)
+        fk = next(k for k in fetch if kern in k)
+        wk = next(k for k in write if kern in k)
+        f = statistics.median(fetch[fk]) * 1024 * 2
+        w = statistics.median(write[wk]) * 1024
+        algo = per_row * 2 * (M // 43)
+        ns = float(stats[name]["AverageNs"])
+        out["variants"][var] = {"kernel": name, "avg_ns": ns, "calls": int(stats[name]["Calls"]),
+                                "algorithmic_bytes": algo, "fetch_bytes": f, "write_bytes": w,
+                                "hbm_bytes_per_launch": f + w, "traffic_over_algorithmic": (f + w) / algo,
+                                "achieved_tbs": algo / ns / 1e3, "frac_of_8tbs": algo / ns / 8e3}
+    with open(os.path.join(dst, "pmc_variants.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
 def main():
+    if sys.argv[1] == "--variants":
+        return variants(sys.argv[2], sys.argv[3])
     src, dst = sys.argv[1], sys.argv[2]
     os.makedirs(dst, exist_ok=True)
     fetch = counters(glob.glob(os.path.join(src, "pmc_fetch", "*counter_collection.csv"))[0])
