@@ -288,11 +288,21 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 #ifndef KVECC_SHIM_TILE_LDS_PAD
 #define KVECC_SHIM_TILE_LDS_PAD 0
 #endif
+// The byte-codec read without interpolation runs the full grid, one tile per
+// wave, 4 workgroups per CU (16 KiB of dynamic LDS on its 20 KiB): H(8,4) ->
+// fp16 at [8,4096,32,128] 137.6-138.6 us against 147.2 persistent with the
+// dynamic tail (8 workgroups per CU 138.6, 2: 174.2, 1: 261.4; 2 tiles per wave
+// 145.9).  The interpolating read keeps the persistent grid (172.1 full grid vs
+// 158.9: it prefetches the next tile's rows and halo behind the current one;
+// tools/exp/run_read_ab.py, profiles/r03/fused/read_ab11.log).
 #ifndef KVECC_SHIM_BYTES_CHUNK
-#define KVECC_SHIM_BYTES_CHUNK KVECC_SHIM_TILE_CHUNK
+#define KVECC_SHIM_BYTES_CHUNK 1
 #endif
 #ifndef KVECC_SHIM_BYTES_LDS_PAD
-#define KVECC_SHIM_BYTES_LDS_PAD KVECC_SHIM_TILE_LDS_PAD
+#define KVECC_SHIM_BYTES_LDS_PAD 16384
+#endif
+#ifndef KVECC_SHIM_BYTES_INTERP_CHUNK
+#define KVECC_SHIM_BYTES_INTERP_CHUNK KVECC_SHIM_TILE_CHUNK
 #endif
 // DYN (CHUNK 0): a wave takes the first DYN_STATIC_PCT % of its even share of
 // tiles statically (w, w + nwaves, ...) and the rest from work counters
@@ -794,7 +804,7 @@ constexpr int kByteTileItems = 4;  // 16-value chunks per lane per phase (max)
 #define KVECC_SHIM_INTERP_SKIP 1
 #endif
 
-template <typename TO, int CODEC, bool INTERP, bool STATS>
+template <typename TO, int CODEC, bool INTERP, bool STATS, int CHUNK>
 __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
   __shared__ float scale_all[kTileWaves][kWave];  // row scales, staged like the rows
@@ -820,7 +830,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
   uint32_t n1 = 0, n2 = 0;
-  constexpr uint32_t kChunk = KVECC_SHIM_BYTES_CHUNK;
+  constexpr uint32_t kChunk = CHUNK;
   constexpr bool kDyn = KVECC_SHIM_BYTES_DYN && kChunk == 0;
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
   uint32_t u = kChunk ? gw * kChunk : gw;
@@ -1066,26 +1076,28 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
 }
 
 template <typename TO, int CODEC, bool INTERP>
-static void launch_bytes_tiles_s(const ShimTileArgs &a, unsigned grid, hipStream_t st) {
+static void launch_bytes_tiles_s(const ShimTileArgs &a, hipStream_t st) {
+  constexpr int kChunk = INTERP ? KVECC_SHIM_BYTES_INTERP_CHUNK : KVECC_SHIM_BYTES_CHUNK;
+  const unsigned grid = tile_grid(a.units, kChunk);
+  const unsigned pad = kChunk ? KVECC_SHIM_BYTES_LDS_PAD : 0u;  // caps the workgroups per CU
   if (a.stats)
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true>), dim3(grid), dim3(kTileBlock),
-                 KVECC_SHIM_BYTES_LDS_PAD, st, a);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true, kChunk>), dim3(grid), dim3(kTileBlock), pad,
+                 st, a);
   else
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, false>), dim3(grid), dim3(kTileBlock),
-                 KVECC_SHIM_BYTES_LDS_PAD, st, a);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, false, kChunk>), dim3(grid), dim3(kTileBlock), pad,
+                 st, a);
 }
 
 template <typename TO>
 static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = tile_grid(a.units, KVECC_SHIM_BYTES_CHUNK);
   if (codec == KVECC_CODEC_H84 && interp)
-    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, true>(a, grid, st);
+    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, true>(a, st);
   else if (codec == KVECC_CODEC_H84)
-    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, false>(a, grid, st);
+    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, false>(a, st);
   else if (codec == KVECC_CODEC_H74)
-    launch_bytes_tiles_s<TO, KVECC_CODEC_H74, false>(a, grid, st);
+    launch_bytes_tiles_s<TO, KVECC_CODEC_H74, false>(a, st);
   else
-    launch_bytes_tiles_s<TO, KVECC_CODEC_NONE, false>(a, grid, st);
+    launch_bytes_tiles_s<TO, KVECC_CODEC_NONE, false>(a, st);
 }
 
 }  // namespace kvecc

@@ -13,12 +13,15 @@ build() {  # name flags...
   local name=$1; shift
   $CC "$@" -o libread_$name.so $CSRC/shim.hip $CSRC/runtime.hip &
 }
-# dynamic tile schedule: off; per wave (DYN 1, the product) at 65 %;
-# per workgroup (DYN 2) at 50 / 75 / 90 % static
-build nodyn -DKVECC_SHIM_TILE_DYN=0
-build pct65 -DKVECC_SHIM_TILE_DYN_STATIC_PCT=65
-for p in 50 75 90; do
-  build wg$p -DKVECC_SHIM_TILE_DYN=2 -DKVECC_SHIM_BYTES_DYN=1 -DKVECC_SHIM_TILE_DYN_STATIC_PCT=$p
-done
+# full grid (CHUNK P: wave w takes tiles [wP, wP + P), workgroups retire and are
+# replaced) for the byte-codec kernel at 8 / 4 / 2 / 1 workgroups per CU
+# (LDS 20 KiB + pad), and for the Golay kernel (its 32 KiB table per workgroup)
+build bc1 -DKVECC_SHIM_BYTES_CHUNK=1
+build bc1p4 -DKVECC_SHIM_BYTES_CHUNK=1 -DKVECC_SHIM_BYTES_LDS_PAD=16384
+build bc1p2 -DKVECC_SHIM_BYTES_CHUNK=1 -DKVECC_SHIM_BYTES_LDS_PAD=40960
+build bc1p1 -DKVECC_SHIM_BYTES_CHUNK=1 -DKVECC_SHIM_BYTES_LDS_PAD=65536
+build bc2p2 -DKVECC_SHIM_BYTES_CHUNK=2 -DKVECC_SHIM_BYTES_LDS_PAD=40960
+build tc4 -DKVECC_SHIM_TILE_CHUNK=4 -DKVECC_SHIM_BYTES_CHUNK=0
+build tc8 -DKVECC_SHIM_TILE_CHUNK=8 -DKVECC_SHIM_BYTES_CHUNK=0
 wait
 ls -la libread_*.so
