@@ -1233,8 +1233,11 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.par = a.cor = nullptr;
   a.atab = nullptr;
   a.ctr = nullptr;
-  // fused combine for one query head per workgroup only: with G heads the last
-  // workgroup's G serial combines became a tail (32q/8kv MFMA 23.6 -> 32.8 us)
+  // fused combine for one query head per workgroup only (MHA 59.7 -> 58.9 us).
+  // With G heads the tail after the last split -- the sc1 stores' acknowledgement,
+  // the counter's round trip and three rounds of sc1 loads, which bypass the L2
+  // -- cost more than the combine launch: 32q/8kv 22.6 -> 32.8 us with the G
+  // heads combined serially, 26.9 with one wave per head (profiles/r03/attn/).
   if (KVECC_ATTN_FUSED_COMBINE && !gm && gq == 1 && batch * heads <= kAttnCtrPerSlot) {
     a.ctr = attn_counter_slot();
     if (!a.ctr) return KVECC_EHIP;

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from kvecc import _lib  # noqa: E402
 VP, I64 = ctypes.c_void_p, ctypes.c_int64
 libs = {"prod": _lib.load()}
-for name in os.environ.get("LIBS", "nomfma").split(","):
+for name in [x for x in os.environ.get("LIBS", "nomfma").split(",") if x]:
     libs[name] = ctypes.CDLL(os.path.join(HERE, f"libattn_{name}.so"))
 for l in libs.values():
     l.kvecc_paged_attention.argtypes = [VP, ctypes.c_int, VP, VP, VP, VP, VP, VP, VP, I64, I64, I64, I64, I64,
@@ -71,7 +71,8 @@ for codec, (cid, per, dt) in codecs.items():
                 e1.record()
                 times[n].append((e0, e1))
         torch.cuda.synchronize()
-        other = [n for n in libs if n != "prod"][0]
+        others = [n for n in libs if n != "prod"]
+        other = others[0] if others else "prod"
         diff = float((outs["prod"].float() - outs[other].float()).abs().max())
         kv_bytes = 2 * blocks * hkv * BS * (per * kc.element_size() + 4)
         line = " ".join(f"{n} {statistics.median(a.elapsed_time(b) * 1e3 for a, b in t):6.1f} us"
