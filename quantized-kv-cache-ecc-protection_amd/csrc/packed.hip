@@ -266,8 +266,15 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
 #endif
 constexpr int kPk2Block = 512;
 constexpr int kPk2Waves = kPk2Block / kWave;
-constexpr int kPk2TileCw = kWave * 16;         // codewords per wave tile
-constexpr int kPk2TileBytes = kPk2TileCw * 3;  // 3072
+// groups of 8 codewords per lane per wave tile (2: 1024 codewords, 3 KiB);
+// 4 and 6 measured 41.0 and 52.4 us against 39.2 (profiles/r03/packed/pk_ab7.log)
+#ifndef KVECC_PACKED_DEC_GROUPS
+#define KVECC_PACKED_DEC_GROUPS 2
+#endif
+constexpr int kPk2Groups = KVECC_PACKED_DEC_GROUPS;
+constexpr int kPk2TileCw = kWave * 8 * kPk2Groups;  // codewords per wave tile
+constexpr int kPk2TileBytes = kPk2TileCw * 3;       // 3 KiB per 2 groups
+constexpr int kPk2Vec = kPk2TileBytes / 16 / kWave;  // 16-byte loads per lane
 
 struct PkDecArgs {
   const uint8_t *cw;
@@ -297,10 +304,10 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t *>(a.cw), 0, (int)(a.units * (uint32_t)kPk2TileBytes), 0x00020000);
   uint32_t t = gw;
-  u32x4 nxt[3];
+  u32x4 nxt[kPk2Vec];
   auto issue = [&](uint32_t tt) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k)
+    for (int k = 0; k < kPk2Vec; ++k)
       nxt[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                              rs, tt * (uint32_t)kPk2TileBytes + 16u * (lane + kWave * k), 0, 2));
   };
@@ -308,14 +315,14 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
   uint32_t bits = 0, unc = 0;
   for (;;) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) reinterpret_cast<u32x4 *>(stage)[lane + kWave * k] = nxt[k];
+    for (int k = 0; k < kPk2Vec; ++k) reinterpret_cast<u32x4 *>(stage)[lane + kWave * k] = nxt[k];
     wave_lds_sync();
     const uint32_t cur = t;
     t = kDyn ? sched.next(t, lane) : t + nwaves;
     const bool more = t < a.units;
     if (more) issue(t);
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < kPk2Groups; ++g) {
       const u32x2 *p = reinterpret_cast<const u32x2 *>(stage + (g * kWave + lane) * 24);
       const u32x2 x0 = p[0], x1 = p[1], x2 = p[2];
       const uint32_t w[6] = {x0.x, x0.y, x1.x, x1.y, x2.x, x2.y};
