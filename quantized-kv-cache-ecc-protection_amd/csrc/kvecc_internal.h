@@ -5,6 +5,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "codec_math.h"
@@ -136,6 +137,54 @@ __device__ __forceinline__ float dequant1(uint32_t n, float s) {
   float x = ((float)n - 8.0f) * s;
   asm volatile("" : "+v"(x));
   return x;
+}
+
+// ---- packed dequantization ----------------------------------------------------
+// (n - 8) * s exactly as the reference computes it (fp32 subtract, fp32 product,
+// then one RNE conversion), two values per instruction: per 8 values 8
+// v_cvt_f32_ubyte, 4 v_pk_add_f32, 4 v_pk_mul_f32, 4 v_cvt_pk_{f16,bf16}_f32
+// (dequant1 with scalar conversions took ~4.5 VALU ops per value, and its
+// volatile asm turned a `dead ? 0 : ...` per value into a branch per value).
+// A missing block's rows decode to n = 0 with scale 0 (their loads fall
+// outside the buffer descriptors); `dead` makes them n = 8, so they give
+// (8 - 8) * 0 = +0, where n = 0 would give -0.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// 4 nibble bytes -> 4 fp32 values, as two pairs
+__device__ __forceinline__ void dq4(uint32_t nb, float s, f32x2 &lo, f32x2 &hi) {
+  const f32x2 ss = {s, s}, m8 = {-8.0f, -8.0f};
+  const f32x2 a = {(float)(nb & 0xFFu), (float)(nb >> 8 & 0xFFu)};
+  const f32x2 b = {(float)(nb >> 16 & 0xFFu), (float)(nb >> 24)};
+  f32x2 x = a + m8, y = b + m8;
+  asm("" : "+v"(x), "+v"(y));  // (n - 8) exactly, then the product: no fma contraction
+  lo = x * ss;
+  hi = y * ss;
+  asm("" : "+v"(lo), "+v"(hi));  // rounded to fp32 here: no v_fma_mix with the conversion
+}
+
+template <typename TO>
+__device__ __forceinline__ uint32_t pack2(f32x2 v) {
+  if constexpr (std::is_same<TO, __half>::value)
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+  else
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
+// the 16 output bytes of VPL nibble bytes (fp16/bf16: nb[0..1], fp32: nb[0])
+template <typename TO>
+__device__ __forceinline__ u32x4 dq16(const uint32_t *nb, float s, bool dead) {
+  const uint32_t d8 = dead ? 0x08080808u : 0u;
+  f32x2 v[4];
+  dq4(nb[0] | d8, s, v[0], v[1]);
+  if constexpr (sizeof(TO) == 4) {
+    return u32x4{__float_as_uint(v[0].x), __float_as_uint(v[0].y), __float_as_uint(v[1].x),
+                 __float_as_uint(v[1].y)};
+  } else {
+    dq4(nb[1] | d8, s, v[2], v[3]);
+    return u32x4{pack2<TO>(v[0]), pack2<TO>(v[1]), pack2<TO>(v[2]), pack2<TO>(v[3])};
+  }
 }
 
 // element conversions of the fused kernels (fp32 / fp16 / bf16, RNE on the way out)
