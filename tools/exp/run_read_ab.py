@@ -6,7 +6,8 @@ bench's fused-read workloads; Golay at BER 1e-2, H84 at 1e-3).
 usage: python tools/exp/run_read_ab.py lib.so [lib.so ...]  (first = reference)
 
 Times are the kernels' own dispatch stamps (kvecc_time_next_launch), median
-over ROUNDS interleaved rounds; outputs and statistics are compared with the
+over ROUNDS interleaved rounds (BLOCK=n: n consecutive launches per library in
+turn, as bench.py times them); outputs and statistics are compared with the
 first library's.
 """
 import ctypes
@@ -118,11 +119,13 @@ def main():
                       and ops.read_stats(stats[i]) == ops.read_stats(stats[0]))
         del ref
         times = [[] for _ in handles]
-        for r in range(ROUNDS):
+        blk = int(os.environ.get("BLOCK", "1"))  # consecutive launches of one library before the next
+        for r in range(0, ROUNDS, blk):
             for i in range(len(handles)):
-                ev = ops.kernel_timer(dev)
-                call(i, ev)
-                times[i].append(ev)
+                for _ in range(blk):
+                    ev = ops.kernel_timer(dev)
+                    call(i, ev)
+                    times[i].append(ev)
         torch.cuda.synchronize()
         nbytes = 2 * B * L * H * (inb + 4 + ODT.itemsize * D)
         for i, (name, _, _) in enumerate(handles):
