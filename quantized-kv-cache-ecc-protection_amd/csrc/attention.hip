@@ -978,6 +978,262 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
   if (a.ctr) combine_if_last<__half, G>(a, b * a.heads + h0, reinterpret_cast<float *>(rows));
 }
 
+// ---- GQA on the matrix cores, Golay(24,12) int32 caches, head_dim 128 ---------
+//
+// The H(8,4) kernel's scheme with codeword-aligned operand maps (a row is 43
+// codewords = 129 nibbles, d = 3c + e):
+//   * QK: lane group g owns codewords 11g .. 11g+10 of its token's K row (44
+//     bytes: two 16-byte loads and a 12-byte one), i.e. d = 33g .. 33g+32, as
+//     k-slots 0..32 of 40 (5 MFMAs per 16 tokens; slots past 32, and d >= 128,
+//     carry q = 0);
+//   * PV: lane m owns codewords 3m .. 3m+2 (a 12-byte load per token), 9
+//     M-tiles, output row m of tile mt is d = 9m + mt (d >= 128 discarded).
+// Codewords decode through the spread tables (two LDS reads, one v_bitop3) to
+// nibbles one per byte; an operand pair is one v_perm of two decoded words
+// into f16 subnormals (n * 2^-24), with the 2^24 scale and the -8 folds of the
+// H(8,4) kernel.  Tokens, scales, the softmax and the merge are that kernel's.
+template <int G>
+__global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnArgs a) {
+  constexpr int D = 128, GC = 43;  // head_dim, codewords per row
+  constexpr int KC = 11, KK = 5;   // K codewords per lane group; QK MFMAs per 16 tokens
+  constexpr int VC = 3, MT = 9;    // V codewords per lane; PV M-tiles
+  constexpr uint32_t kRowBytes = GC * 4;
+  constexpr int kWaves = kBlock / kWave;
+  __shared__ __attribute__((aligned(16))) uint32_t gt[8192];  // spread tables (golay_attn_table_dev)
+  __shared__ __attribute__((aligned(16))) int32_t rows[kMaxSplit + kMfmaStep];
+  __shared__ int32_t blks[kMaxSplit + 1];
+  __shared__ float red[kWaves][G][D];
+  __shared__ float gml[2][kWaves][G];
+
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+  const int n = lane & 15, g = lane >> 4;
+  const int64_t hgroups = a.heads / G;
+  const int64_t b = blockIdx.y / hgroups, h0 = (blockIdx.y % hgroups) * G;
+  const int64_t hk = h0 / (a.heads / a.kv_heads);
+  const int64_t ctx = min<int64_t>(a.ctx_lens[b], a.max_blocks * a.bs);
+  const int64_t t0 = (int64_t)blockIdx.x * a.split;
+  const int64_t t1 = min<int64_t>(t0 + a.split, ctx);
+  const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
+  {  // block-table slice -> cache rows, as in the H(8,4) kernel
+    const uint32_t bs = (uint32_t)a.bs;
+    const uint32_t lb0 = (uint32_t)(t0 / a.bs);
+    const int64_t tmax = min<int64_t>(t0 + a.split, a.max_blocks * a.bs);
+    const int nlb = tmax > t0 ? (int)((uint32_t)(tmax - 1) / bs - lb0 + 1) : 0;
+    const int32_t *tab = a.table + b * a.max_blocks + lb0;
+    for (int j = threadIdx.x; j < nlb; j += kBlock) blks[j] = tab[j];
+    {
+      const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
+      for (int i = threadIdx.x; i < 2048; i += kBlock) reinterpret_cast<u32x4 *>(gt)[i] = src[i];
+    }
+    __syncthreads();
+    const int32_t head_row0 = (int32_t)((a.layer * a.kv_heads + hk) * a.bs);
+    const int32_t blk_rows = (int32_t)(a.layers * a.kv_heads * a.bs);
+    const int npad = (ntok + kMfmaStep - 1) / kMfmaStep * kMfmaStep;
+    for (int i = threadIdx.x; i < npad; i += kBlock) {
+      int32_t row = -1;
+      if (i < ntok) {
+        const uint32_t pos = (uint32_t)(t0 + i);
+        const uint32_t lb = pos / bs;
+        const int32_t blk = blks[lb - lb0];
+        if (blk >= 0) row = blk * blk_rows + head_row0 + (int32_t)(pos - lb * bs);
+      }
+      rows[i] = row;
+    }
+  }
+  // Q^T operand: k-slot v = 8kk + j of lane group g is d = 33g + v (v < 33, d < 128), else 0
+  f16x8 qop[KK];
+  float qsum = 0.0f;
+  {
+    const __half *qh = reinterpret_cast<const __half *>(a.q) + (b * a.heads + h0 + n) * D;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int v = 8 * kk + j, d = 33 * g + v;
+        _Float16 x = 0;
+        if (n < G && v < 3 * KC && d < D) x = __builtin_bit_cast(_Float16, qh[d]);
+        qop[kk][j] = x;
+        qsum += (float)x;
+      }
+    }
+    qsum += __shfl_xor(qsum, 16, kWave);
+    qsum += __shfl_xor(qsum, 32, kWave);
+  }
+  __syncthreads();
+
+  // codeword -> data nibbles one per byte (bytes 0..2), uncorrectable words keep their data
+  auto sp_of = [&](uint32_t c) -> uint32_t {
+    const uint32_t p = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gt) + ((c << 2) & 0x3FFCu));
+    const uint32_t off = ((c >> 10) ^ (p >> 18)) & 0x3FFCu;
+    const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gt + 4096) + off);
+    return __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
+  };
+  // f16 subnormal pair: byte e0 of lo (0x0c: zero), byte e1 of hi, in halves 0 and 1
+  auto pair = [](uint32_t hi, uint32_t lo, int e0, int e1) -> uint32_t {
+    const uint32_t s0 = e0 < 0 ? 0x0cu : (uint32_t)e0, s1 = e1 < 0 ? 0x0cu : (uint32_t)(4 + e1);
+    return __builtin_amdgcn_perm(hi, lo, 0x0c000c00u | s1 << 16 | s0);
+  };
+
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.k_cache), 0, (int)a.cache_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t vrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.v_cache), 0, (int)a.cache_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t ksrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.k_scales), 0, (int)a.scale_bytes, kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t vsrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.v_scales), 0, (int)a.scale_bytes, kRsrcWord3);
+  constexpr float kScale = 16777216.0f, kOff = 8.0f;  // subnormal operands: 2^24, and n - 8
+  const float qscale = a.sm_scale * kAttnLogScale;
+  const float qoff = kOff * qsum;
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float m = -INFINITY, l = 0.0f, psum = 0.0f;
+
+  for (int i0 = wave * kMfmaStep; i0 < ntok; i0 += kWaves * kMfmaStep) {
+    int32_t rv[8];
+    {
+      const int4 r0 = *reinterpret_cast<const int4 *>(&rows[i0 + 4 * g]);
+      const int4 r1 = *reinterpret_cast<const int4 *>(&rows[i0 + 16 + 4 * g]);
+      rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+      rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+    }
+    uint32_t kw[2][KC];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau) {
+      const uint32_t off = (uint32_t)max(rows[i0 + 16 * tau + n], 0) * kRowBytes + 44u * g;
+      const u32x4 x0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
+      const u32x4 x1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off + 16, 0, 0));
+      const auto x2 = __builtin_amdgcn_raw_buffer_load_b96(krs, off + 32, 0, 0);
+      kw[tau][0] = x0.x; kw[tau][1] = x0.y; kw[tau][2] = x0.z; kw[tau][3] = x0.w;
+      kw[tau][4] = x1.x; kw[tau][5] = x1.y; kw[tau][6] = x1.z; kw[tau][7] = x1.w;
+      kw[tau][8] = x2[0]; kw[tau][9] = x2[1]; kw[tau][10] = x2[2];
+    }
+    uint32_t vw[8][VC];
+    float ks[8], vs[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t r = (uint32_t)max(rv[j], 0);
+      const auto x = __builtin_amdgcn_raw_buffer_load_b96(vrs, r * kRowBytes + 12u * n, 0, 0);
+      vw[j][0] = x[0]; vw[j][1] = x[1]; vw[j][2] = x[2];
+      ks[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, r * 4u, 0, 0));
+      vs[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, r * 4u, 0, 0));
+    }
+    // ---- S^T = K . Q^T
+    f32x4 S[2];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau) {
+      uint32_t sp[KC];
+#pragma unroll
+      for (int c = 0; c < KC; ++c) sp[c] = sp_of(kw[tau][c]);
+      S[tau] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        uint32_t p[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int v0 = 8 * kk + 2 * h, v1 = v0 + 1;
+          const int c0 = v0 < 3 * KC ? v0 / 3 : 0, c1 = v1 < 3 * KC ? v1 / 3 : 0;
+          p[h] = pair(sp[c1], sp[c0], v0 < 3 * KC ? v0 % 3 : -1, v1 < 3 * KC ? v1 % 3 : -1);
+        }
+        S[tau] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, u32x4{p[0], p[1], p[2], p[3]}),
+                                                        qop[kk], S[tau], 0, 0, 0);
+      }
+    }
+    // ---- online softmax over this lane's 8 tokens of head n
+    float s[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] = rv[j] >= 0 ? (S[j >> 2][j & 3] * kScale - qoff) * (qscale * ks[j]) : -INFINITY;
+      mx = fmaxf(mx, s[j]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, kWave));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+    const float mn = fmaxf(m, mx);
+    const float mu = mn == -INFINITY ? 0.0f : mn;
+    const float alpha = attn_exp(m - mu);
+    m = mn;
+    l *= alpha;
+    psum *= alpha;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] *= alpha;
+    uint32_t phi[4], plo[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float p0 = attn_exp(s[2 * h] - mu), p1 = attn_exp(s[2 * h + 1] - mu);
+      l += p0 + p1;
+      const float w0 = p0 * vs[2 * h], w1 = p1 * vs[2 * h + 1];
+      psum += w0 + w1;
+      const auto hi = __builtin_amdgcn_cvt_pkrtz(w0, w1);
+      const auto lo = __builtin_amdgcn_cvt_pkrtz(w0 - (float)hi[0], w1 - (float)hi[1]);
+      phi[h] = __builtin_bit_cast(uint32_t, hi);
+      plo[h] = __builtin_bit_cast(uint32_t, lo);
+    }
+    const f16x8 pb_hi = __builtin_bit_cast(f16x8, u32x4{phi[0], phi[1], phi[2], phi[3]});
+    const f16x8 pb_lo = __builtin_bit_cast(f16x8, u32x4{plo[0], plo[1], plo[2], plo[3]});
+    // ---- O^T += V^T . P: tile mt takes nibble mt % 3 of codeword mt / 3
+    uint32_t sv[8][VC];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int c = 0; c < VC; ++c) sv[j][c] = sp_of(vw[j][c]);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      uint32_t p[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) p[h] = pair(sv[2 * h + 1][mt / 3], sv[2 * h][mt / 3], mt % 3, mt % 3);
+      const f16x8 va = __builtin_bit_cast(f16x8, u32x4{p[0], p[1], p[2], p[3]});
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb_hi, acc[mt], 0, 0, 0);
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb_lo, acc[mt], 0, 0, 0);
+    }
+  }
+
+  // ---- merge, as in the H(8,4) kernel
+  l += __shfl_xor(l, 16, kWave);
+  l += __shfl_xor(l, 32, kWave);
+  psum += __shfl_xor(psum, 16, kWave);
+  psum += __shfl_xor(psum, 32, kWave);
+  const float poff = kOff * psum;
+  if (n < G) {
+    if (g == 0) {
+      gml[0][wave][n] = m;
+      gml[1][wave][n] = l;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int d = MT * (4 * g + r) + mt;
+        if (d < D) red[wave][n][d] = acc[mt][r] * kScale - poff;
+      }
+  }
+  __syncthreads();
+  const int64_t ws_stride = a.nsplit * (a.d + 2);
+  float *ws0 = a.ws + ((b * a.heads + h0) * a.nsplit + blockIdx.x) * (a.d + 2);
+  for (int idx = threadIdx.x; idx < G * D; idx += kBlock) {
+    const int h = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) M = fmaxf(M, gml[0][w][h]);
+    float o = 0.0f, L = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      const float mw = gml[0][w][h];
+      const float wt = mw == -INFINITY ? 0.0f : attn_exp(mw - M);
+      o += red[w][h][d] * wt;
+      L += gml[1][w][h] * wt;
+    }
+    float *ws = ws0 + h * ws_stride;
+    ws_put(ws + 2 + d, o);
+    if (d == 0) {
+      ws_put(ws, M);
+      ws_put(ws + 1, L);
+    }
+  }
+  if (a.ctr) combine_if_last<__half, G>(a, b * a.heads + h0, reinterpret_cast<float *>(rows));
+}
+
 template <typename T>
 static void launch_combine(const AttnArgs &a, int64_t batch, hipStream_t st) {
   KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
@@ -1095,7 +1351,18 @@ static int launch_mfma_d(const AttnArgs &a, int64_t batch, int gm, hipStream_t s
   return KVECC_OK;
 }
 
-static int launch_mfma(const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
+static int launch_mfma(int codec, const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
+  if (codec == KVECC_CODEC_GOLAY) {  // head_dim 128 (attn_mfma_heads)
+    const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads / gm));
+    switch (gm) {
+      case 2: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<2>), grid, dim3(kBlock), 0, st, a); break;
+      case 4: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<4>), grid, dim3(kBlock), 0, st, a); break;
+      case 8: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<8>), grid, dim3(kBlock), 0, st, a); break;
+      default: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<16>), grid, dim3(kBlock), 0, st, a); break;
+    }
+    if (!a.ctr) launch_combine<__half>(a, batch, st);
+    return KVECC_OK;
+  }
   switch (a.d) {
     case 32: return launch_mfma_d<32>(a, batch, gm, st);
     case 64: return launch_mfma_d<64>(a, batch, gm, st);
@@ -1103,14 +1370,18 @@ static int launch_mfma(const AttnArgs &a, int64_t batch, int gm, hipStream_t st)
   }
 }
 
-// query heads per workgroup of the MFMA kernel (0: not applicable): Hamming(8,4)
-// caches under 4 GiB, fp16 queries (16-byte aligned), head_dim 32 / 64 / 128, a
-// group of >= 2 query heads per cache head
+// query heads per workgroup of the MFMA kernels (0: not applicable): caches under
+// 4 GiB, fp16 queries (16-byte aligned), a group of >= 2 query heads per cache
+// head; Hamming(8,4) at head_dim 32 / 64 / 128, Golay int32 at head_dim 128
+#ifndef KVECC_ATTN_MFMA_GOLAY
+#define KVECC_ATTN_MFMA_GOLAY 1
+#endif
 static int attn_mfma_heads(int codec, int q_dtype, const void *query, int64_t d, int64_t heads,
                            int64_t kv_heads, bool buf) {
   const int64_t group = heads / kv_heads;
-  if (!KVECC_ATTN_MFMA || codec != KVECC_CODEC_H84 || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) ||
-      (d != 32 && d != 64 && d != 128) || group < 2)
+  const bool h84 = codec == KVECC_CODEC_H84 && (d == 32 || d == 64 || d == 128);
+  const bool golay = KVECC_ATTN_MFMA_GOLAY && codec == KVECC_CODEC_GOLAY && d == 128;
+  if (!KVECC_ATTN_MFMA || !(h84 || golay) || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) || group < 2)
     return 0;
   return group % 16 == 0 ? 16 : group % 8 == 0 ? 8 : group % 4 == 0 ? 4 : group % 2 == 0 ? 2 : 0;
 }
@@ -1250,7 +1521,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   }
   hipStream_t st = as_stream(stream);
   if (gm) {
-    const int rc = launch_mfma(a, batch, gm, st);
+    const int rc = launch_mfma(codec, a, batch, gm, st);
     if (rc != KVECC_OK) return rc;
     return check_launch("paged_attention");
   }

@@ -188,6 +188,29 @@ def test_hip_packed_golay_vs_torch(gpu, batch, heads, kvh, d, ctx, ber, dtype):
     assert torch.allclose(got, ref, atol=tol[0], rtol=tol[1]), float((got - ref).abs().max())
 
 
+GOLAY_FP16_CASES = [(2, 8, 2, 128, 300, 0.02), (1, 32, 2, 128, 1000, 0.01), (3, 4, 2, 128, 77, 0.0),
+                    (2, 32, 16, 128, 513, 0.01), (1, 16, 4, 64, 200, 0.01), (2, 4, 4, 128, 129, 0.02)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,heads,kvh,d,ctx,ber", GOLAY_FP16_CASES)
+def test_hip_golay_fp16_native_vs_torch(gpu, batch, heads, kvh, d, ctx, ber):
+    """The native entry (paged_attention_into) with fp16 queries over int32
+    Golay caches, output fp16: GQA groups 4 / 16 / 2 / 2 at head_dim 128 take
+    the matrix-core kernel, head_dim 64 and MHA the VALU kernels."""
+    from kvecc import ops
+    kc, vc, table, lens, ks, vs = _cache("cpu", "golay", batch, heads, kvh, d, ctx, ber, seed=ctx + 3)
+    q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(2)).half()
+    ref = _torch_reference(q.float(), kc, vc, table, lens, ks, vs, 1, 16, "golay")
+    dev = lambda t: t.to(gpu)  # noqa: E731
+    out = torch.empty(batch, heads, d, dtype=torch.float16, device=gpu)
+    ops.paged_attention_into(dev(q), dev(kc), dev(vc), dev(table), dev(lens), dev(ks), dev(vs), out, 1, 16,
+                             1 / math.sqrt(d), "golay")
+    got = out.float().cpu()
+    # fp16 output: one fp16 ulp of the fp32 result
+    assert torch.allclose(got, ref, atol=1e-3, rtol=1e-3), float((got - ref).abs().max())
+
+
 # ---- reference-generated fixtures (tools/gen_golden.py gen_attention) ---------------
 # Outputs of the reference's own paged_attention_ecc: the Triton H84 kernel
 # (attention_ecc.py:264-427) under TRITON_INTERPRET=1 and the Golay
