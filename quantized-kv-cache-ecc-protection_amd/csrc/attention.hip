@@ -1376,6 +1376,11 @@ static int launch_mfma(int codec, const AttnArgs &a, int64_t batch, int gm, hipS
 #ifndef KVECC_ATTN_MFMA_GOLAY
 #define KVECC_ATTN_MFMA_GOLAY 1
 #endif
+// workgroups per CU of the Golay kernel's split choice (157 VGPRs, 49-73 KiB of
+// LDS): 2 measured 30.6 vs 34.2 us at 4 (32q/8kv; profiles/r03/attn/attn_gqa14.log)
+#ifndef KVECC_ATTN_MFMA_GOLAY_WG_PER_CU
+#define KVECC_ATTN_MFMA_GOLAY_WG_PER_CU 2
+#endif
 static int attn_mfma_heads(int codec, int q_dtype, const void *query, int64_t d, int64_t heads,
                            int64_t kv_heads, bool buf) {
   const int64_t group = heads / kv_heads;
@@ -1494,7 +1499,9 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     gm = attn_mfma_heads(codec, q_dtype, query, head_dim, heads, kv_heads, fits);
   }
   if (gm)  // KVECC_ATTN_MFMA_WG_PER_CU workgroups per CU, never finer than the workspace allows
-    a.split = std::max(choose_split(batch * heads / gm, max_context_len, KVECC_ATTN_MFMA_WG_PER_CU),
+    a.split = std::max(choose_split(batch * heads / gm, max_context_len,
+                                    codec == KVECC_CODEC_GOLAY ? KVECC_ATTN_MFMA_GOLAY_WG_PER_CU
+                                                               : KVECC_ATTN_MFMA_WG_PER_CU),
                        choose_split(std::max<int64_t>(1, batch * heads / 4), max_context_len));
   else
     a.split = choose_split(batch * heads / gq, max_context_len);
