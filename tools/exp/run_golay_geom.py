@@ -1,5 +1,6 @@
 """A/B: Golay encode/decode geometry variants (tools/exp/libgl_*.so) vs production, cold cache,
-interleaved.  Build: make -C tools/exp libgl_g1.so libgl_g1deep.so libgl_g2deep.so libgl_b256.so"""
+interleaved.  Build: make -C tools/exp libgl_g1.so libgl_g1deep.so libgl_g2deep.so libgl_b256.so
+Env: LIBS (libgl_<name>.so list), WARM=1 (no cache flush between launches), ROUNDS."""
 import ctypes, os, statistics, sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
@@ -8,7 +9,7 @@ import torch
 from kvecc import _lib, ops
 VP, I64 = ctypes.c_void_p, ctypes.c_int64
 libs = {"prod": _lib.load()}
-for n in ("g1", "g1deep", "g2deep", "b256"):
+for n in os.environ.get("LIBS", "g1,g1deep,g2deep,b256").split(","):
     p = os.path.join(HERE, f"libgl_{n}.so")
     if os.path.exists(p):
         libs[n] = ctypes.CDLL(p)
@@ -39,9 +40,11 @@ ok = {}
 for k, (fn, out, ref, _) in cases.items():
     out.zero_(); fn(); torch.cuda.synchronize(); ok[k] = torch.equal(out, ref)
 t = {k: [] for k in cases}
-for _ in range(9):
+WARM = os.environ.get("WARM") == "1"  # back-to-back as bench.py runs, instead of cold
+for _ in range(int(os.environ.get("ROUNDS", "9"))):
     for k, (fn, *_r) in cases.items():
-        junk.fill_(1)
+        if not WARM:
+            junk.fill_(1)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(); fn(); b.record(); torch.cuda.synchronize()
         t[k].append(a.elapsed_time(b) * 1e3)
