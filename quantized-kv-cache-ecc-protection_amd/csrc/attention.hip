@@ -992,12 +992,20 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
 // nibbles one per byte; an operand pair is one v_perm of two decoded words
 // into f16 subnormals (n * 2^-24), with the 2^24 scale and the -8 folds of the
 // H(8,4) kernel.  Tokens, scales, the softmax and the merge are that kernel's.
-template <int G>
+//
+// Packed caches (3-byte codewords, 132-byte rows) keep the maps where the loads
+// stay dword-aligned: K lane groups own 12 codewords (36 bytes at 36g, d = 36g
+// .. 36g+35, still 5 MFMAs), V lanes own codewords 3m .. 3m+2 (9 bytes at 9m:
+// one 12-byte load from the dword below, then v_alignbyte by m & 3).  Bytes past
+// the row's 129 belong to d >= 128 (q = 0, outputs discarded).
+template <int G, bool PACKED>
 __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnArgs a) {
-  constexpr int D = 128, GC = 43;  // head_dim, codewords per row
-  constexpr int KC = 11, KK = 5;   // K codewords per lane group; QK MFMAs per 16 tokens
-  constexpr int VC = 3, MT = 9;    // V codewords per lane; PV M-tiles
-  constexpr uint32_t kRowBytes = GC * 4;
+  constexpr int D = 128, GC = 43;          // head_dim, codewords per row
+  constexpr int KC = PACKED ? 12 : 11;     // K codewords per lane group
+  constexpr int KD = 3 * KC, KK = 5;       // its values; QK MFMAs per 16 tokens
+  constexpr int VC = 3, MT = 9;            // V codewords per lane; PV M-tiles
+  constexpr int KW = PACKED ? 9 : KC;      // K dwords per lane group
+  constexpr uint32_t kRowBytes = PACKED ? KVECC_GOLAY_PACKED_ROW(GC) : GC * 4;
   constexpr int kWaves = kBlock / kWave;
   __shared__ __attribute__((aligned(16))) uint32_t gt[8192];  // spread tables (golay_attn_table_dev)
   __shared__ __attribute__((aligned(16))) int32_t rows[kMaxSplit + kMfmaStep];
@@ -1040,7 +1048,7 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
       rows[i] = row;
     }
   }
-  // Q^T operand: k-slot v = 8kk + j of lane group g is d = 33g + v (v < 33, d < 128), else 0
+  // Q^T operand: k-slot v = 8kk + j of lane group g is d = KD g + v (v < KD, d < 128), else 0
   f16x8 qop[KK];
   float qsum = 0.0f;
   {
@@ -1049,9 +1057,9 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
     for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int v = 8 * kk + j, d = 33 * g + v;
+        const int v = 8 * kk + j, d = KD * g + v;
         _Float16 x = 0;
-        if (n < G && v < 3 * KC && d < D) x = __builtin_bit_cast(_Float16, qh[d]);
+        if (n < G && v < KD && d < D) x = __builtin_bit_cast(_Float16, qh[d]);
         qop[kk][j] = x;
         qsum += (float)x;
       }
@@ -1098,23 +1106,30 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
       rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
       rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
     }
-    uint32_t kw[2][KC];
+    uint32_t kw[2][KW];
 #pragma unroll
     for (int tau = 0; tau < 2; ++tau) {
-      const uint32_t off = (uint32_t)max(rows[i0 + 16 * tau + n], 0) * kRowBytes + 44u * g;
+      const uint32_t off = (uint32_t)max(rows[i0 + 16 * tau + n], 0) * kRowBytes + 4u * KW * g;
       const u32x4 x0 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0));
       const u32x4 x1 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(krs, off + 16, 0, 0));
-      const auto x2 = __builtin_amdgcn_raw_buffer_load_b96(krs, off + 32, 0, 0);
       kw[tau][0] = x0.x; kw[tau][1] = x0.y; kw[tau][2] = x0.z; kw[tau][3] = x0.w;
       kw[tau][4] = x1.x; kw[tau][5] = x1.y; kw[tau][6] = x1.z; kw[tau][7] = x1.w;
-      kw[tau][8] = x2[0]; kw[tau][9] = x2[1]; kw[tau][10] = x2[2];
+      if constexpr (PACKED) {
+        kw[tau][8] = __builtin_amdgcn_raw_buffer_load_b32(krs, off + 32, 0, 0);
+      } else {
+        const auto x2 = __builtin_amdgcn_raw_buffer_load_b96(krs, off + 32, 0, 0);
+        kw[tau][8] = x2[0]; kw[tau][9] = x2[1]; kw[tau][10] = x2[2];
+      }
     }
+    // V: this lane's codewords start 12n bytes (int32) or 9n bytes (packed) into the row
+    const uint32_t voff = PACKED ? (9u * n) & ~3u : 12u * n;
+    const uint32_t vsh = n & 3;  // packed: byte of the first codeword in the loaded dword
     uint32_t vw[8][VC];
     float ks[8], vs[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t r = (uint32_t)max(rv[j], 0);
-      const auto x = __builtin_amdgcn_raw_buffer_load_b96(vrs, r * kRowBytes + 12u * n, 0, 0);
+      const auto x = __builtin_amdgcn_raw_buffer_load_b96(vrs, r * kRowBytes + voff, 0, 0);
       vw[j][0] = x[0]; vw[j][1] = x[1]; vw[j][2] = x[2];
       ks[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ksrs, r * 4u, 0, 0));
       vs[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vsrs, r * 4u, 0, 0));
@@ -1123,9 +1138,23 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
     f32x4 S[2];
 #pragma unroll
     for (int tau = 0; tau < 2; ++tau) {
+      uint32_t cw[KC];
+      if constexpr (PACKED) {  // 4 little-endian 3-byte codewords per 3 dwords
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const uint32_t d0 = kw[tau][3 * t], d1 = kw[tau][3 * t + 1], d2 = kw[tau][3 * t + 2];
+          cw[4 * t] = d0;
+          cw[4 * t + 1] = __builtin_amdgcn_alignbyte(d1, d0, 3);
+          cw[4 * t + 2] = __builtin_amdgcn_alignbyte(d2, d1, 2);
+          cw[4 * t + 3] = d2 >> 8;
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < KC; ++c) cw[c] = kw[tau][c];
+      }
       uint32_t sp[KC];
 #pragma unroll
-      for (int c = 0; c < KC; ++c) sp[c] = sp_of(kw[tau][c]);
+      for (int c = 0; c < KC; ++c) sp[c] = sp_of(cw[c]);
       S[tau] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
@@ -1133,8 +1162,8 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const int v0 = 8 * kk + 2 * h, v1 = v0 + 1;
-          const int c0 = v0 < 3 * KC ? v0 / 3 : 0, c1 = v1 < 3 * KC ? v1 / 3 : 0;
-          p[h] = pair(sp[c1], sp[c0], v0 < 3 * KC ? v0 % 3 : -1, v1 < 3 * KC ? v1 % 3 : -1);
+          const int c0 = v0 < KD ? v0 / 3 : 0, c1 = v1 < KD ? v1 / 3 : 0;
+          p[h] = pair(sp[c1], sp[c0], v0 < KD ? v0 % 3 : -1, v1 < KD ? v1 % 3 : -1);
         }
         S[tau] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, u32x4{p[0], p[1], p[2], p[3]}),
                                                         qop[kk], S[tau], 0, 0, 0);
@@ -1175,9 +1204,16 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
     // ---- O^T += V^T . P: tile mt takes nibble mt % 3 of codeword mt / 3
     uint32_t sv[8][VC];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+    for (int j = 0; j < 8; ++j) {
+      if constexpr (PACKED) {  // codeword c at byte vsh + 3c of the 12 loaded (alignbyte uses shift & 3)
+        const uint32_t d0 = vw[j][0], d1 = vw[j][1], d2 = vw[j][2];
+        vw[j][0] = __builtin_amdgcn_alignbyte(d1, d0, vsh);
+        vw[j][1] = __builtin_amdgcn_alignbyte(vsh ? d2 : d1, vsh ? d1 : d0, vsh + 3);
+        vw[j][2] = __builtin_amdgcn_alignbyte(d2, vsh < 2 ? d1 : d2, vsh + 2);
+      }
 #pragma unroll
       for (int c = 0; c < VC; ++c) sv[j][c] = sp_of(vw[j][c]);
+    }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       uint32_t p[4];
@@ -1351,17 +1387,23 @@ static int launch_mfma_d(const AttnArgs &a, int64_t batch, int gm, hipStream_t s
   return KVECC_OK;
 }
 
+template <bool PACKED>
+static int launch_golay_mfma(const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
+  const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads / gm));
+  switch (gm) {
+    case 2: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<2, PACKED>), grid, dim3(kBlock), 0, st, a); break;
+    case 4: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<4, PACKED>), grid, dim3(kBlock), 0, st, a); break;
+    case 8: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<8, PACKED>), grid, dim3(kBlock), 0, st, a); break;
+    default: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<16, PACKED>), grid, dim3(kBlock), 0, st, a); break;
+  }
+  if (!a.ctr) launch_combine<__half>(a, batch, st);
+  return KVECC_OK;
+}
+
 static int launch_mfma(int codec, const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
-  if (codec == KVECC_CODEC_GOLAY) {  // head_dim 128 (attn_mfma_heads)
-    const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads / gm));
-    switch (gm) {
-      case 2: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<2>), grid, dim3(kBlock), 0, st, a); break;
-      case 4: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<4>), grid, dim3(kBlock), 0, st, a); break;
-      case 8: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<8>), grid, dim3(kBlock), 0, st, a); break;
-      default: KVECC_LAUNCH((paged_attn_golay_mfma_kernel<16>), grid, dim3(kBlock), 0, st, a); break;
-    }
-    if (!a.ctr) launch_combine<__half>(a, batch, st);
-    return KVECC_OK;
+  if (codec != KVECC_CODEC_H84) {  // Golay, head_dim 128 (attn_mfma_heads)
+    if (codec == KVECC_CODEC_GOLAY_PACKED) return launch_golay_mfma<true>(a, batch, gm, st);
+    return launch_golay_mfma<false>(a, batch, gm, st);
   }
   switch (a.d) {
     case 32: return launch_mfma_d<32>(a, batch, gm, st);
@@ -1372,7 +1414,7 @@ static int launch_mfma(int codec, const AttnArgs &a, int64_t batch, int gm, hipS
 
 // query heads per workgroup of the MFMA kernels (0: not applicable): caches under
 // 4 GiB, fp16 queries (16-byte aligned), a group of >= 2 query heads per cache
-// head; Hamming(8,4) at head_dim 32 / 64 / 128, Golay int32 at head_dim 128
+// head; Hamming(8,4) at head_dim 32 / 64 / 128, Golay (int32 or packed) at head_dim 128
 #ifndef KVECC_ATTN_MFMA_GOLAY
 #define KVECC_ATTN_MFMA_GOLAY 1
 #endif
@@ -1385,7 +1427,8 @@ static int attn_mfma_heads(int codec, int q_dtype, const void *query, int64_t d,
                            int64_t kv_heads, bool buf) {
   const int64_t group = heads / kv_heads;
   const bool h84 = codec == KVECC_CODEC_H84 && (d == 32 || d == 64 || d == 128);
-  const bool golay = KVECC_ATTN_MFMA_GOLAY && codec == KVECC_CODEC_GOLAY && d == 128;
+  const bool golay = KVECC_ATTN_MFMA_GOLAY && (codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED) &&
+                     d == 128;
   if (!KVECC_ATTN_MFMA || !(h84 || golay) || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) || group < 2)
     return 0;
   return group % 16 == 0 ? 16 : group % 8 == 0 ? 8 : group % 4 == 0 ? 4 : group % 2 == 0 ? 2 : 0;
@@ -1500,7 +1543,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   }
   if (gm)  // KVECC_ATTN_MFMA_WG_PER_CU workgroups per CU, never finer than the workspace allows
     a.split = std::max(choose_split(batch * heads / gm, max_context_len,
-                                    codec == KVECC_CODEC_GOLAY ? KVECC_ATTN_MFMA_GOLAY_WG_PER_CU
+                                    codec != KVECC_CODEC_H84 ? KVECC_ATTN_MFMA_GOLAY_WG_PER_CU
                                                                : KVECC_ATTN_MFMA_WG_PER_CU),
                        choose_split(std::max<int64_t>(1, batch * heads / 4), max_context_len));
   else

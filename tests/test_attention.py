@@ -193,19 +193,22 @@ GOLAY_FP16_CASES = [(2, 8, 2, 128, 300, 0.02), (1, 32, 2, 128, 1000, 0.01), (3, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["golay", "golay_packed"])
 @pytest.mark.parametrize("batch,heads,kvh,d,ctx,ber", GOLAY_FP16_CASES)
-def test_hip_golay_fp16_native_vs_torch(gpu, batch, heads, kvh, d, ctx, ber):
-    """The native entry (paged_attention_into) with fp16 queries over int32
-    Golay caches, output fp16: GQA groups 4 / 16 / 2 / 2 at head_dim 128 take
-    the matrix-core kernel, head_dim 64 and MHA the VALU kernels."""
+def test_hip_golay_fp16_native_vs_torch(gpu, batch, heads, kvh, d, ctx, ber, codec):
+    """The native entry (paged_attention_into) with fp16 queries over int32 and
+    packed Golay caches, output fp16: GQA groups 4 / 16 / 2 / 2 at head_dim 128
+    take the matrix-core kernel, head_dim 64 and MHA the VALU kernels."""
     from kvecc import ops
     kc, vc, table, lens, ks, vs = _cache("cpu", "golay", batch, heads, kvh, d, ctx, ber, seed=ctx + 3)
     q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(2)).half()
     ref = _torch_reference(q.float(), kc, vc, table, lens, ks, vs, 1, 16, "golay")
+    if codec == "golay_packed":
+        kc, vc = _pack_golay(kc, d), _pack_golay(vc, d)
     dev = lambda t: t.to(gpu)  # noqa: E731
     out = torch.empty(batch, heads, d, dtype=torch.float16, device=gpu)
     ops.paged_attention_into(dev(q), dev(kc), dev(vc), dev(table), dev(lens), dev(ks), dev(vs), out, 1, 16,
-                             1 / math.sqrt(d), "golay")
+                             1 / math.sqrt(d), codec)
     got = out.float().cpu()
     # fp16 output: one fp16 ulp of the fp32 result
     assert torch.allclose(got, ref, atol=1e-3, rtol=1e-3), float((got - ref).abs().max())
