@@ -299,10 +299,52 @@ __device__ __forceinline__ float ws_get(const float *p) {
 // folding all splits online, one thread per output value (29.5 vs 22.7 us), and
 // one wave per (b, h) with the weights by v_readlane (31.2 vs 22.5 us) -- fewer,
 // longer-lived waves each walking the splits serially.
+#ifndef KVECC_ATTN_COMBINE_PRELOAD
+#define KVECC_ATTN_COMBINE_PRELOAD 1
+#endif
 template <typename T, bool COHERENT = false>
 __device__ void combine_bh(const AttnArgs &a, int64_t bh, float *wt, float *bred) {
   const int64_t stride = a.d + 2;
   const float *ws = a.ws + bh * a.nsplit * stride;
+  if (KVECC_ATTN_COMBINE_PRELOAD && a.nsplit <= kBlock) {
+    // one memory round trip: thread s < nsplit loads its split's (m, l) while
+    // thread d < head_dim loads its first kPre accumulators; the two block
+    // reductions then run in LDS
+    constexpr int kPre = 16;
+    const int t = threadIdx.x, ns = (int)a.nsplit;
+    float ov[kPre];
+#pragma unroll
+    for (int s = 0; s < kPre; ++s) ov[s] = t < a.d && s < ns ? ws_get<COHERENT>(ws + s * stride + 2 + t) : 0.0f;
+    const float ms = t < ns ? ws_get<COHERENT>(ws + t * stride) : -INFINITY;
+    const float ls = t < ns ? ws_get<COHERENT>(ws + t * stride + 1) : 0.0f;
+    float mx = ms;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+    if ((t & (kWave - 1)) == 0) bred[t / kWave] = mx;
+    __syncthreads();
+    mx = bred[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / kWave; ++w) mx = fmaxf(mx, bred[w]);
+    __syncthreads();
+    const float w = ms == -INFINITY ? 0.0f : attn_exp(ms - mx);
+    if (t < ns) wt[t] = w;
+    float L = w * ls;
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) L += __shfl_xor(L, off, kWave);
+    if ((t & (kWave - 1)) == 0) bred[t / kWave] = L;
+    __syncthreads();
+    L = 0.0f;
+#pragma unroll
+    for (int v = 0; v < kBlock / kWave; ++v) L += bred[v];
+    if (t < a.d) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int s = 0; s < kPre; ++s) acc += ov[s] * (s < ns ? wt[s] : 0.0f);
+      for (int s = kPre; s < ns; ++s) acc += ws_get<COHERENT>(ws + s * stride + 2 + t) * wt[s];
+      reinterpret_cast<T *>(a.out)[bh * a.d + t] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);
+    }
+    return;
+  }
   float mx = -INFINITY;
   for (int64_t s = threadIdx.x; s < a.nsplit; s += kBlock) mx = fmaxf(mx, ws_get<COHERENT>(ws + s * stride));
 #pragma unroll
@@ -343,12 +385,60 @@ __global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) 
   combine_bh<T>(a, blockIdx.x, wt, bred);
 }
 
+// All G > 1 heads of a group at once for the fused combine: P = kBlock / G
+// threads per head, one memory round trip (thread s < nsplit of a head loads
+// split s's (m, l); every thread the first kPre accumulators of its up to kR
+// outputs alongside), the reductions over the head's splits from LDS.  Needs
+// nsplit <= P and head_dim <= kR * P (combine_group_fits); sh: 3 kBlock floats.
+constexpr int kGroupOuts = 4;
+template <int G>
+__host__ __device__ constexpr bool combine_group_fits(int64_t nsplit, int64_t d) {
+  return G > 1 && nsplit <= kBlock / G && d <= kGroupOuts * (kBlock / G);
+}
+template <typename T, int G>
+__device__ void combine_group(const AttnArgs &a, int64_t bh0, float *sh) {
+  constexpr int P = kBlock / G, kR = kGroupOuts, kPre = 16;
+  const int t = threadIdx.x, h = t / P, u = t % P, ns = (int)a.nsplit, d = (int)a.d;
+  const int64_t stride = a.d + 2;
+  const float *ws = a.ws + (bh0 + h) * a.nsplit * stride;
+  float ov[kR][kPre];
+#pragma unroll
+  for (int r = 0; r < kR; ++r)
+#pragma unroll
+    for (int s = 0; s < kPre; ++s)
+      ov[r][s] = u + r * P < d && s < ns ? ws_get<true>(ws + s * stride + 2 + u + r * P) : 0.0f;
+  const float ms = u < ns ? ws_get<true>(ws + u * stride) : -INFINITY;
+  const float ls = u < ns ? ws_get<true>(ws + u * stride + 1) : 0.0f;
+  float *shm = sh, *shw = sh + kBlock, *shl = sh + 2 * kBlock;
+  shm[t] = ms;
+  shl[t] = ls;
+  __syncthreads();
+  const float *hm = shm + h * P, *hw = shw + h * P, *hl = shl + h * P;
+  float M = -INFINITY;
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, hm[s]);
+  shw[t] = ms == -INFINITY ? 0.0f : attn_exp(ms - M);
+  __syncthreads();
+  float L = 0.0f;
+  for (int s = 0; s < ns; ++s) L += hw[s] * hl[s];
+  T *out = reinterpret_cast<T *>(a.out) + (bh0 + h) * a.d;
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int di = u + r * P;
+    if (di >= d) continue;
+    float acc = 0.0f;
+#pragma unroll
+    for (int s = 0; s < kPre; ++s) acc += ov[r][s] * (s < ns ? hw[s] : 0.0f);
+    for (int s = kPre; s < ns; ++s) acc += ws_get<true>(ws + s * stride + 2 + di) * hw[s];
+    out[di] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);
+  }
+}
+
 // Fused combine: the workgroup that finishes the last split of its (batch, head
 // group) -- counted on a.ctr[blockIdx.y] -- combines the group's G query heads
 // and resets the counter, saving the combine launch.  The workspace stores are
 // sc1 (ws_put) and every thread waits for its own before the count; the last
 // workgroup reads the entries with sc1 loads.  wt: kMaxSplits floats of LDS the
-// caller no longer needs.
+// caller no longer needs (3 kBlock for G > 1).
 template <typename T, int G>
 __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
   __shared__ float bred[kBlock / kWave];
@@ -362,6 +452,9 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
   }
   __syncthreads();
   if (!last) return;
+  if constexpr (G > 1) {
+    if (combine_group_fits<G>(a.nsplit, a.d)) return combine_group<T, G>(a, bh0, wt);
+  }
   for (int j = 0; j < G; ++j) {
     if (j) __syncthreads();
     combine_bh<T, true>(a, bh0 + j, wt, bred);
@@ -686,6 +779,12 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
 // 0: a separate combine launch
 #ifndef KVECC_ATTN_FUSED_COMBINE
 #define KVECC_ATTN_FUSED_COMBINE 1
+#endif
+// 1: also for G > 1 query heads per workgroup where combine_group fits (one
+// round trip for all G heads): 32q/8kv H(8,4) 26.7 us against 22.3 with the
+// combine launch, Golay 30.2 / 29.4 (profiles/r03/attn/attn_gqa19.log)
+#ifndef KVECC_ATTN_FUSED_COMBINE_GQA
+#define KVECC_ATTN_FUSED_COMBINE_GQA 0
 #endif
 // 1: issue the next step's loads before this step's math (191 VGPRs at D = 128:
 // 2 waves per SIMD; 32q/8kv measured 29.8 us against 22.9 without)
@@ -1556,10 +1655,18 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   a.ctr = nullptr;
   // fused combine for one query head per workgroup only (MHA 59.7 -> 58.9 us).
   // With G heads the tail after the last split -- the sc1 stores' acknowledgement,
-  // the counter's round trip and three rounds of sc1 loads, which bypass the L2
-  // -- cost more than the combine launch: 32q/8kv 22.6 -> 32.8 us with the G
-  // heads combined serially, 26.9 with one wave per head (profiles/r03/attn/).
-  if (KVECC_ATTN_FUSED_COMBINE && !gm && gq == 1 && batch * heads <= kAttnCtrPerSlot) {
+  // the counter's round trip and rounds of sc1 loads, which bypass the L2 -- cost
+  // more than the combine launch: 32q/8kv 22.6 -> 32.8 us with the G heads
+  // combined serially, 26.9 with one wave per head, 26.7 (against 22.3) with all
+  // G heads in one round trip (combine_group; profiles/r03/attn/).
+  const int gw = gm ? gm : gq;  // query heads per workgroup
+  const bool group_fits = gw == 2    ? combine_group_fits<2>(a.nsplit, head_dim)
+                          : gw == 4  ? combine_group_fits<4>(a.nsplit, head_dim)
+                          : gw == 8  ? combine_group_fits<8>(a.nsplit, head_dim)
+                          : gw == 16 ? combine_group_fits<16>(a.nsplit, head_dim)
+                                     : false;
+  if (KVECC_ATTN_FUSED_COMBINE && (gw == 1 || (KVECC_ATTN_FUSED_COMBINE_GQA && group_fits)) &&
+      batch * heads <= kAttnCtrPerSlot) {
     a.ctr = attn_counter_slot();
     if (!a.ctr) return KVECC_EHIP;
   }
