@@ -462,6 +462,14 @@ __global__ __launch_bounds__(kHpBlock) void h84_encode_packed_kernel(const u32x2
 #ifndef KVECC_H84_PACKED_PERM
 #define KVECC_H84_PACKED_PERM 1
 #endif
+// chunks per lane per grid-stride step (2: both loads issued first), and the
+// grid's workgroups per CU
+#ifndef KVECC_H84_PACKED_UNROLL
+#define KVECC_H84_PACKED_UNROLL 1
+#endif
+#ifndef KVECC_H84_PACKED_GRID_PER_CU
+#define KVECC_H84_PACKED_GRID_PER_CU 32
+#endif
 template <bool WITH_TYPES, bool WITH_STATS>
 __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4 *__restrict__ cw,
                                                                      u32x2 *__restrict__ nib,
@@ -469,9 +477,7 @@ __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4
                                                                      int64_t n16,
                                                                      uint64_t *__restrict__ stats) {
   uint32_t n1 = 0, n2 = 0;
-  for (int64_t i = (int64_t)blockIdx.x * kHpBlock + threadIdx.x; i < n16;
-       i += (int64_t)gridDim.x * kHpBlock) {
-    const u32x4 c = ld_stream(cw + i);
+  auto chunk = [&](const u32x4 c, int64_t i) {
     const uint32_t w[4] = {c.x, c.y, c.z, c.w};
     if (KVECC_H84_PACKED_PERM) {
       uint32_t y[4], z[4];
@@ -501,7 +507,7 @@ __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4
           n2 += __builtin_popcount(hi & ~tw & 0x55555555u);  // type 2: double, detected
         }
       }
-      continue;
+      return;
     }
     uint32_t d[4], t[4];
 #pragma unroll
@@ -511,7 +517,17 @@ __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4
     if (WITH_TYPES)
       st_stream(types + i, type_pack4(t[0]) | type_pack4(t[1]) << 8 | type_pack4(t[2]) << 16 |
                                type_pack4(t[3]) << 24);
+  };
+  const int64_t stride = (int64_t)gridDim.x * kHpBlock;
+  int64_t i = (int64_t)blockIdx.x * kHpBlock + threadIdx.x;
+  if constexpr (KVECC_H84_PACKED_UNROLL > 1) {  // two chunks' loads in flight per lane
+    for (; i + stride < n16; i += 2 * stride) {
+      const u32x4 c0 = ld_stream(cw + i), c1 = ld_stream(cw + i + stride);
+      chunk(c0, i);
+      chunk(c1, i + stride);
+    }
   }
+  for (; i < n16; i += stride) chunk(ld_stream(cw + i), i);
   if (WITH_STATS) flush_stats2<kHpBlock>(stats, n1, n2);
 }
 
@@ -782,7 +798,7 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
   if (done < n && aligned(nibbles, 8) && aligned(codewords, 16) && (!error_types || aligned(error_types, 4))) {
     const int64_t n16 = (n - done) / 16;
     if (n16 > 0) {
-      const dim3 grid(grid_for(n16, kHpBlock, 32)), block(kHpBlock);
+      const dim3 grid(grid_for(n16, kHpBlock, KVECC_H84_PACKED_GRID_PER_CU)), block(kHpBlock);
       const int64_t i0 = done / 16;  // after the wave tiles
       const u32x4 *c = reinterpret_cast<const u32x4 *>(codewords) + i0;
       u32x2 *o = reinterpret_cast<u32x2 *>(nibbles) + i0;
