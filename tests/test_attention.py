@@ -304,6 +304,35 @@ def test_hip_empty_context_values(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("codec", ["hamming84", "golay", "golay_packed"])
+def test_hip_mfma_gqa_holes_and_buffer_end(gpu, codec):
+    """The matrix-core GQA kernels (fp16 queries, head_dim 128, 4 query heads per
+    cache head) with an empty context, a -1 block inside a context, and the cache
+    buffer's last row in use (layer 2 of 3, last block, last cache head): the
+    packed Golay loads read past a row's 129 bytes, which the buffer descriptor's
+    range must absorb at the end of the allocation."""
+    from kvecc import ops
+    base = "hamming84" if codec == "hamming84" else "golay"
+    batch, heads, kvh, d, ctx, layer = 3, 16, 4, 128, 90, 2
+    kc, vc, table, lens, ks, vs = _cache("cpu", base, batch, heads, kvh, d, ctx, 1e-3, seed=11)
+    lens[0] = 96                     # sequence 0 ends on row 15 of its sixth block ...
+    table[0, 5] = kc.shape[0] - 1    # ... which is the buffer's last block
+    table[1, 2] = -1                 # tokens 32..47 of sequence 1 are skipped
+    lens[2] = 0
+    q = torch.randn(batch, heads, d, generator=torch.Generator().manual_seed(4)).half()
+    ref = _torch_reference(q.float(), kc, vc, table, lens, ks, vs, layer, 16, base)
+    if codec == "golay_packed":
+        kc, vc = _pack_golay(kc, d), _pack_golay(vc, d)
+    dev = lambda t: t.to(gpu)  # noqa: E731
+    out = torch.empty(batch, heads, d, dtype=torch.float16, device=gpu)
+    ops.paged_attention_into(dev(q), dev(kc), dev(vc), dev(table), dev(lens), dev(ks), dev(vs), out, layer, 16,
+                             1 / math.sqrt(d), codec)
+    got = out.float().cpu()
+    assert torch.equal(got[2], torch.full((heads, d), -8.0 if codec == "hamming84" else 0.0))
+    assert torch.allclose(got[:2], ref[:2], atol=1e-3, rtol=1e-3), float((got[:2] - ref[:2]).abs().max())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("codec", ["golay", "golay_packed"])
 def test_hip_golay_long_context_fold(gpu, codec):
     """The Golay kernel sums raw nibbles and folds the -8 out per split
