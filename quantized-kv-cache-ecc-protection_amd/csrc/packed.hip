@@ -275,6 +275,12 @@ constexpr int kPk2Groups = KVECC_PACKED_DEC_GROUPS;
 constexpr int kPk2TileCw = kWave * 8 * kPk2Groups;  // codewords per wave tile
 constexpr int kPk2TileBytes = kPk2TileCw * 3;       // 3 KiB per 2 groups
 constexpr int kPk2Vec = kPk2TileBytes / 16 / kWave;  // 16-byte loads per lane
+// uncorrectable flags (one byte per group of 8 codewords): staged in LDS and
+// stored as 16-byte stores by the first kPk2Groups * 4 lanes, instead of one
+// byte store per lane per group (needs a 16-byte aligned flag buffer)
+#ifndef KVECC_PACKED_DEC_FLAGS16
+#define KVECC_PACKED_DEC_FLAGS16 1
+#endif
 
 struct PkDecArgs {
   const uint8_t *cw;
@@ -284,12 +290,14 @@ struct PkDecArgs {
   const uint8_t *tab;  // golay_pk_table_dev()
   uint64_t *stats;
   uint32_t *dyn;
+  uint32_t flags16;  // flags staged and stored 16 bytes per lane
 };
 
 template <bool WITH_FLAGS, bool WITH_STATS>
 __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkDecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tab[24576];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kPk2Waves][kPk2TileBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t flag_all[kPk2Waves][kPk2Groups * kWave];
   for (int i = threadIdx.x; i < 24576 / 16; i += kPk2Block)
     reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
   __syncthreads();
@@ -352,7 +360,19 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
       nib_pack8(d, n);
       const uint32_t grp = cur * (kPk2TileCw / 8) + g * kWave + lane;  // group of 8 codewords
       st_stream(reinterpret_cast<u32x3v *>(a.nib + (size_t)grp * 3), u32x3v{n[0], n[1], n[2]});
-      if (WITH_FLAGS) st_stream(a.flags + grp, (uint8_t)fl);
+      if (WITH_FLAGS) {
+        if (a.flags16)
+          flag_all[wave][g * kWave + lane] = (uint8_t)fl;
+        else
+          st_stream(a.flags + grp, (uint8_t)fl);
+      }
+    }
+    if (WITH_FLAGS && a.flags16) {  // the tile's kPk2Groups * 64 flag bytes
+      wave_lds_sync();
+      constexpr uint32_t kFl = kPk2Groups * kWave / 16;
+      if (lane < kFl)
+        st_stream(reinterpret_cast<u32x4 *>(a.flags + (size_t)cur * (kPk2Groups * kWave)) + lane,
+                  reinterpret_cast<const u32x4 *>(flag_all[wave])[lane]);
     }
     if (!more) break;
     wave_lds_sync();
@@ -690,7 +710,8 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
     uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot() : nullptr;
     if (!tab || (KVECC_PACKED_DEC_DYN && !dyn)) return KVECC_EHIP;
     const PkDecArgs a{codewords, reinterpret_cast<uint32_t *>(nibbles), uncorrectable, (uint32_t)wave_tiles,
-                      tab, stats, dyn};
+                      tab, stats, dyn,
+                      (uint32_t)(KVECC_PACKED_DEC_FLAGS16 && uncorrectable && aligned(uncorrectable, 16))};
     const dim3 grid(grid_for(wave_tiles, kPk2Waves, KVECC_PACKED_DEC_V2_PER_CU)), block(kPk2Block);
     if (uncorrectable && stats)
       KVECC_LAUNCH((golay_decode_packed_wave_kernel<true, true>), grid, block, 0, st, a);

@@ -328,6 +328,13 @@ constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
 constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
 constexpr int kTileChunks = 5;                     // 8-value output chunks per lane per tile (max)
 constexpr int kTileAux = KVECC_SHIM_TILE_NT ? 2 : 0;  // buffer-load cache policy: nt
+// Golay read tables in LDS.  SPLITP: the parity half (data -> spread data |
+// parity << 20, linear over GF(2)) as two 64-entry tables, XORed, with the
+// 16 KiB correction half: 16.5 KiB instead of 32 KiB per workgroup.
+#ifndef KVECC_SHIM_GOLAY_SPLITP
+#define KVECC_SHIM_GOLAY_SPLITP 0
+#endif
+constexpr int kGolayTabWords = KVECC_SHIM_GOLAY_SPLITP ? 128 + 4096 : 8192;
 
 struct ShimTileArgs {
   const void *cache[2];
@@ -521,13 +528,18 @@ extern "C" __attribute__((visibility("default"))) int kvecc_exp_wave_times(void 
 
 template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kGolayTabWords];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileTPI][kTileStage];
   // row scales of the staged tiles: written in phase 1, read in phase 2 (a
   // scale kept in a register across the next tile's prefetch made the compiler
   // wait for that prefetch before phase 2)
   __shared__ float scale_all[kTileWaves][kTileTPI][kWave];
-  {
+  if (KVECC_SHIM_GOLAY_SPLITP) {  // parity half as two 64-entry tables (it is GF(2)-linear)
+    for (int i = threadIdx.x; i < 128; i += kTileBlock) tab[i] = a.atab[i < 64 ? i : (i - 64) << 6];
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab + 4096);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(tab + 128);
+    for (int i = threadIdx.x; i < 1024; i += kTileBlock) dst[i] = src[i];
+  } else {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(tab);
 #pragma unroll
@@ -631,9 +643,15 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
           const uint32_t p = cw, e = 0;
 #else
           const char *tb = reinterpret_cast<const char *>(tab);
-          const uint32_t p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
+          uint32_t p;
+          if (KVECC_SHIM_GOLAY_SPLITP)  // entries of data bits 0-5 and 6-11, XORed
+            p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0xFCu)) ^
+                *reinterpret_cast<const uint32_t *>(tb + 256 + ((cw >> 4) & 0xFCu));
+          else
+            p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
           // syndrome = parity bits ^ parity(data), as a byte offset: ((cw >> 12 ^ p >> 20) & 0xFFF) * 4
-          const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 16384 + (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
+          const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 4 * (kGolayTabWords - 4096) +
+                                                                 (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
 #endif
           sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
           if (STATS) cnt += e >> 24;

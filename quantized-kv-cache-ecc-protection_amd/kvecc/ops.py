@@ -898,8 +898,28 @@ def unpack_nibbles(packed: torch.Tensor, n: int) -> torch.Tensor:
     return torch.stack([p & 0xF, p >> 4], dim=1).reshape(-1)[:n].contiguous()
 
 
+def _check_packed_bufs(name, m, *bufs):
+    """Raw-pointer packed entry points: every buffer a contiguous uint8 tensor on
+    the first one's GPU, holding at least the bytes the kernel touches for m
+    units (the kernels take only pointers, so a short buffer would be overrun)."""
+    dev = bufs[0][0].device
+    _check_gpu(bufs[0][0])
+    if m < 0:
+        raise ValueError(f"{name}: negative count {m}")
+    for t, need, what in bufs:
+        if t is None:
+            continue
+        if t.dtype != torch.uint8 or not t.is_contiguous() or t.device != dev:
+            raise ValueError(f"{name}: {what} must be a contiguous uint8 tensor on {dev}")
+        if t.numel() < need:
+            raise ValueError(f"{name}: {what} holds {t.numel()} bytes, needs {need}")
+
+
 def golay_encode_packed_into(nibbles, codewords, m):
     """Asynchronous packed encode into caller buffers (device pointers, stream)."""
+    m = int(m)
+    _check_packed_bufs("golay_encode_packed_into", m, (nibbles, (3 * m + 1) // 2, "nibbles"),
+                       (codewords, 3 * m, "codewords"))
     _lib.call("kvecc_golay_encode_packed", _ptr(nibbles), _ptr(codewords), int(m),
               _stream(nibbles.device))
     return codewords
@@ -908,6 +928,8 @@ def golay_encode_packed_into(nibbles, codewords, m):
 def golay_decode_packed_into(codewords, nibbles, uncorrectable=None, m=None, stats=None):
     """Asynchronous packed decode into caller buffers; statistics stay on the device."""
     m = codewords.numel() // 3 if m is None else int(m)
+    _check_packed_bufs("golay_decode_packed_into", m, (codewords, 3 * m, "codewords"),
+                       (nibbles, (3 * m + 1) // 2, "nibbles"), (uncorrectable, (m + 7) // 8, "uncorrectable"))
     _lib.call("kvecc_golay_decode_packed", _ptr(codewords), _ptr(nibbles), _ptr(uncorrectable), m,
               _ptr(stats), _stream(codewords.device))
     return nibbles
@@ -961,6 +983,9 @@ def pack_error_types(types: torch.Tensor) -> torch.Tensor:
 
 
 def hamming84_encode_packed_into(nibbles, codewords, n):
+    n = int(n)
+    _check_packed_bufs("hamming84_encode_packed_into", n, (nibbles, (n + 1) // 2, "nibbles"),
+                       (codewords, n, "codewords"))
     _lib.call("kvecc_hamming84_encode_packed", _ptr(nibbles), _ptr(codewords), int(n),
               _stream(nibbles.device))
     return codewords
@@ -968,6 +993,8 @@ def hamming84_encode_packed_into(nibbles, codewords, n):
 
 def hamming84_decode_packed_into(codewords, nibbles, error_types=None, n=None, stats=None):
     n = codewords.numel() if n is None else int(n)
+    _check_packed_bufs("hamming84_decode_packed_into", n, (codewords, n, "codewords"),
+                       (nibbles, (n + 1) // 2, "nibbles"), (error_types, (n + 3) // 4, "error_types"))
     _lib.call("kvecc_hamming84_decode_packed", _ptr(codewords), _ptr(nibbles), _ptr(error_types), n,
               _ptr(stats), _stream(codewords.device))
     return nibbles

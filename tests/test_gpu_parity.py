@@ -475,6 +475,30 @@ def test_golay_packed_vs_cpu_backend(gpu, m, offset):
     assert torch.equal(out.cpu(), out_ref) and torch.equal(fl.cpu(), fl_ref)
 
 
+@pytest.mark.parametrize("foff", [0, 1, 4, 16])
+def test_golay_packed_decode_flag_buffer_offsets(gpu, foff):
+    """Caller flag buffers at any byte offset: 16-byte aligned ones take the
+    wave kernel's LDS-staged 16-byte flag stores, the others its byte stores;
+    both equal the host backend, and bytes around the flags stay untouched."""
+    from kvecc import cpu_ops, ops
+    m = 8192 * 6 + 13  # whole wave tiles plus a tail
+    g = torch.Generator().manual_seed(77 + foff)
+    nib = torch.randint(0, 256, ((3 * m + 1) // 2,), generator=g, dtype=torch.uint8)
+    noisy = cpu_ops.inject_bit_errors_triton(cpu_ops.golay_encode_packed(nib, m), 0.05, 8, seed=3)
+    out_ref, fl_ref, st_ref = cpu_ops.golay_decode_packed(noisy, m, return_uncorrectable=True)
+    nf = (m + 7) // 8
+    fbuf = torch.full((nf + foff + 32,), 0xA5, dtype=torch.uint8, device=gpu)
+    nib_out = torch.empty((3 * m + 1) // 2, dtype=torch.uint8, device=gpu)
+    st = ops.new_stats(gpu)
+    ops.golay_decode_packed_into(noisy.to(gpu), nib_out, fbuf[foff:foff + nf], m, st)
+    f = fbuf.cpu()
+    assert fl_ref.sum() > 0 and torch.equal(f[foff:foff + nf], fl_ref)
+    assert bool((f[:foff] == 0xA5).all()) and bool((f[foff + nf:] == 0xA5).all())
+    assert torch.equal(nib_out.cpu(), out_ref) and tuple(ops.read_stats(st)) == tuple(st_ref)
+    with pytest.raises(ValueError):  # a flag buffer one byte short is refused, not overrun
+        ops.golay_decode_packed_into(noisy.to(gpu), nib_out, fbuf[:nf - 1], m, st)
+
+
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 16 * 1000 + 9, 134_217_728])
 @pytest.mark.parametrize("offset", [0, 1])
 def test_hamming84_packed_vs_cpu_backend(gpu, n, offset):
