@@ -277,9 +277,11 @@ constexpr int kPk2TileBytes = kPk2TileCw * 3;       // 3 KiB per 2 groups
 constexpr int kPk2Vec = kPk2TileBytes / 16 / kWave;  // 16-byte loads per lane
 // uncorrectable flags (one byte per group of 8 codewords): staged in LDS and
 // stored as 16-byte stores by the first kPk2Groups * 4 lanes, instead of one
-// byte store per lane per group (needs a 16-byte aligned flag buffer)
+// byte store per lane per group (needs a 16-byte aligned flag buffer).
+// Measured no faster (38.4 vs 38.1 us at the bench's M, BER 1e-2;
+// profiles/r03/packed/pk_flags16_ab.log): the byte stores are not the limit.
 #ifndef KVECC_PACKED_DEC_FLAGS16
-#define KVECC_PACKED_DEC_FLAGS16 1
+#define KVECC_PACKED_DEC_FLAGS16 0
 #endif
 
 struct PkDecArgs {

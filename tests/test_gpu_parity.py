@@ -477,9 +477,9 @@ def test_golay_packed_vs_cpu_backend(gpu, m, offset):
 
 @pytest.mark.parametrize("foff", [0, 1, 4, 16])
 def test_golay_packed_decode_flag_buffer_offsets(gpu, foff):
-    """Caller flag buffers at any byte offset: 16-byte aligned ones take the
-    wave kernel's LDS-staged 16-byte flag stores, the others its byte stores;
-    both equal the host backend, and bytes around the flags stay untouched."""
+    """Caller flag buffers at any byte offset (a KVECC_PACKED_DEC_FLAGS16 build
+    stages 16-byte aligned ones through LDS) equal the host backend, and the
+    bytes around the flags stay untouched."""
     from kvecc import cpu_ops, ops
     m = 8192 * 6 + 13  # whole wave tiles plus a tail
     g = torch.Generator().manual_seed(77 + foff)
