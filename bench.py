@@ -58,6 +58,11 @@ def parse():
                     help="time budget of the CPU baseline sample (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--side-warmup", type=int, default=100,
+                    help="warm-up calls before each optional section (packed, rows, fused reads); the "
+                         "clocks ramp after the idle set-up of each section: the fused H(8,4) read "
+                         "timed 151-154 us after 5 calls and 139-141 after 100 "
+                         "(profiles/r03/fused/fused_warm.log)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-inject", action="store_true")
     ap.add_argument("--no-packed", action="store_true")
@@ -181,7 +186,7 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
             "write_share": 2 * D / bytes_per_row,
             "ceiling_note": "write-heavy mix: non-temporal write-only streams peak at 4.8-5.3 TB/s and "
                             "read-only at 6.1-6.9 TB/s on MI355X (profiles/r02/hbm_ceiling.log)",
-            "timing": f"HIP events carried by the dispatch, mean of {steps} launches"}
+            "timing": f"HIP events carried by the dispatch, mean of {steps} launches after {warmup} warm-up calls"}
 
 
 def fused_h84_bench(dev, steps, warmup):
@@ -230,7 +235,7 @@ def fused_h84_bench(dev, steps, warmup):
     res.update({"workload": "shim_read_batch hamming84 -> fp16, [B=8,L=4096,Hkv=32,D=128] K+V, block_size 16, "
                             "BER 1e-3; plain and with double-error interpolation",
                 "kernel": "shim_read_bytes_tiles_kernel", "bytes_per_token_row": D + 4 + 2 * D,
-                "timing": f"HIP events carried by the dispatch, mean of {steps} launches"})
+                "timing": f"HIP events carried by the dispatch, mean of {steps} launches after {warmup} warm-up calls"})
     return res
 
 
@@ -265,7 +270,7 @@ def rows_bench(dev, x, noisy_rows, steps, warmup):
             "hbm_gbs": {"encode": nbytes / (enc * 1e-3) / 1e9, "decode": nbytes / (dec * 1e-3) / 1e9},
             "frac": {"encode": nbytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "decode": nbytes / (dec * 1e-3) / 1e9 / HBM_PEAK_GBS},
-            "timing": f"HIP events carried by the dispatch, mean of {steps} launches"}
+            "timing": f"HIP events carried by the dispatch, mean of {steps} launches after {warmup} warm-up calls"}
 
 
 def cpu_quota():
@@ -535,6 +540,8 @@ def main():
     # ---- native packed layout (3-byte codewords, nibbles two per byte) -------
     # Same codewords, its own bytes/unit (4.5 B encode, 4.625 B decode); never
     # mixed into `value`, which is the reference layout.
+    side_warmup = max(args.warmup, args.side_warmup)  # optional sections only; the step keeps W
+
     def packed_section():
         nib = ops.pack_nibbles(trip.view(-1))
         cw3 = ops.golay_encode_packed(nib, m)
@@ -544,7 +551,7 @@ def main():
         flags = torch.empty((m + 7) // 8, dtype=torch.uint8, device=dev)  # uncorrectable bits
         pst = ops.new_stats(dev)
         pe = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-        for _ in range(args.warmup):
+        for _ in range(side_warmup):
             ops.golay_encode_packed(nib, m)
             ops.golay_decode_packed(noisy3, m, stats=pst)
         torch.cuda.synchronize()
@@ -570,19 +577,19 @@ def main():
         xr = torch.randint(0, 16, (B, L, H, D), generator=torch.Generator().manual_seed(rank),
                            dtype=torch.uint8).to(dev)
         noisy_rows = noisy.view(B * L * H, gsz)  # the same BER-1e-2 codewords, one row per head
-        return rows_bench(dev, xr, noisy_rows, max(args.steps, 10), args.warmup)
+        return rows_bench(dev, xr, noisy_rows, max(args.steps, 10), side_warmup)
 
     rows = None if args.no_rows else optional("golay_rows", rows_section)
 
     fused = None
     if not args.no_fused:
-        fused = optional("fused_golay_decode", lambda: fused_decode_bench(dev, max(args.steps, 10), args.warmup))
+        fused = optional("fused_golay_decode", lambda: fused_decode_bench(dev, max(args.steps, 10), side_warmup))
         if fused is not None:
             fused["packed"] = optional("fused_golay_decode.packed",
-                                       lambda: fused_decode_bench(dev, max(args.steps, 10), args.warmup,
+                                       lambda: fused_decode_bench(dev, max(args.steps, 10), side_warmup,
                                                                   packed=True))
             fused["hamming84"] = optional("fused_golay_decode.hamming84",
-                                          lambda: fused_h84_bench(dev, max(args.steps, 10), args.warmup))
+                                          lambda: fused_h84_bench(dev, max(args.steps, 10), side_warmup))
 
     if rank != 0:
         if dist is not None:
