@@ -317,13 +317,13 @@ struct TileSchedule {
     return k;  // lane 0's; next() broadcasts it when the tile is needed
   }
   __device__ __forceinline__ void init(uint32_t units_, uint32_t *dyn, uint32_t gw_, uint32_t nwaves_,
-                                       uint32_t lane) {
+                                       uint32_t lane, uint32_t pct = KVECC_SHIM_TILE_DYN_STATIC_PCT) {
     gw = gw_;
     nwaves = nwaves_;
     units = units_;
     sidx = 1;
     // static tiles per wave: DYN_STATIC_PCT % of the even share, at least 1
-    nstatic = max(1u, (uint32_t)(KVECC_SHIM_TILE_DYN_STATIC_PCT * ((units + nwaves - 1) / nwaves) / 100));
+    nstatic = max(1u, (uint32_t)(pct * ((units + nwaves - 1) / nwaves) / 100));
     if (DYN || KVECC_SHIM_DYN_PROBE) {
       cidx = gw % kDynCounters;
       ctr = dyn + kDynStride * cidx;

@@ -321,6 +321,13 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 #ifndef KVECC_SHIM_BYTES_DYN
 #define KVECC_SHIM_BYTES_DYN KVECC_SHIM_TILE_DYN
 #endif
+// the fused reads' static share (the other TileSchedule users keep
+// KVECC_SHIM_TILE_DYN_STATIC_PCT = 75): 65 % ran Golay 161.0 / packed 147.0 /
+// H(8,4)+interp 156.2 us against 161.6 / 148.0 / 159.8 at 75 and 166-168 /
+// 153-155 / 164-166 at 85-90 (profiles/r03/fused/static_pct_ab1.log)
+#ifndef KVECC_SHIM_READ_STATIC_PCT
+#define KVECC_SHIM_READ_STATIC_PCT 65
+#endif
 constexpr int kTileBlock = KVECC_SHIM_TILE_BLOCK;  // 8 waves per workgroup
 constexpr int kTileTPI = KVECC_SHIM_TILE_TPI;      // tiles in flight per wave
 constexpr int kTileWaves = kTileBlock / kWave;
@@ -595,7 +602,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   if (kWgDyn)
     wsched.init(a, wave, lane);
   else
-    sched.init(a.units, a.dyn, gw, nwaves, lane);
+    sched.init(a.units, a.dyn, gw, nwaves, lane, KVECC_SHIM_READ_STATIC_PCT);
 #if KVECC_SHIM_DYN_PROBE == 3
   u = sched.perm(gw);
 #endif
@@ -810,7 +817,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
   const uint32_t ustep = kChunk ? 1u : nwaves;
   if (u >= uend) return;
   TileSchedule<kDyn> sched;
-  sched.init(a.units, a.dyn, gw, nwaves, lane);
+  sched.init(a.units, a.dyn, gw, nwaves, lane, KVECC_SHIM_READ_STATIC_PCT);
 
   ShimTile cur;
   u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
