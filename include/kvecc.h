@@ -82,6 +82,21 @@ KVECC_API int kvecc_time_next_launch(void *start_event, void *stop_event);
 /* Upload the Golay tables to `device` (done lazily otherwise; call before graph
  * capture).  Replaces golay_triton.py:304-330 (_build_syndrome_table cache). */
 KVECC_API int kvecc_init_device(int device);
+/* Work / split counters of the dynamically scheduled kernels (the fused shim
+ * reads, the per-head Golay rows, the packed decodes, the paged-attention fused
+ * combine).  No reference counterpart: the reference launches one program per
+ * row and schedules nothing.  Each kernel needs its counters zero and to itself
+ * while it runs, and leaves them zero.  The library gives eager launches one
+ * counter slot per stream (per thread for hipStreamPerThread), and launches
+ * captured into a graph a slot of their own per (capture, stream), so launches
+ * that can overlap never share counters.  The first launch on a new stream
+ * takes a slot from a pool that grows outside captures only;
+ * kvecc_reserve_counter_slots(device, n) makes n slots available for the
+ * captures to come (kvecc_init_device keeps a reserve of 32). */
+KVECC_API int kvecc_reserve_counter_slots(int device, int n);
+/* Diagnostic (synchronises the device): slots handed out, and how many counter
+ * words of all slots are non-zero -- 0 whenever no launch is in flight. */
+KVECC_API int kvecc_counter_slots_check(int device, int64_t *slots_in_use, int64_t *nonzero_words);
 /* Host copies of the code tables the kernels use (for verification):
  *   syndrome table as the reference builds it, config.py:403-457 -> int32[4096]
  *   H row masks, config.py:354-379 -> uint32[12]                              */

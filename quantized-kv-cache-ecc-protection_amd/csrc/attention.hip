@@ -439,6 +439,19 @@ __device__ void combine_group(const AttnArgs &a, int64_t bh0, float *sh) {
 // sc1 (ws_put) and every thread waits for its own before the count; the last
 // workgroup reads the entries with sc1 loads.  wt: kMaxSplits floats of LDS the
 // caller no longer needs (3 kBlock for G > 1).
+//
+// Why no release/acquire: on gfx942/gfx950 an sc1 store (ws_put) is performed
+// at the memory side (it bypasses the non-coherent per-XCD L2 state for this
+// line) once the issuing wave's vmcnt reaches 0, and an sc1 load misses every
+// CU/L2 copy, so "store sc1; s_waitcnt vmcnt(0); barrier; atomic add" on the
+// writers and "atomic returns the last count; load sc1" on the reader order the
+// workspace without the whole-L2 writeback an agent-scope release costs
+// (buffer_wbl2: 4x the kernel).  That is a property of these
+// targets' cache hierarchy, not of the HIP memory model: any other target must
+// not compile this path (the launcher then uses the separate combine kernel).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "combine_if_last relies on gfx942/gfx950 sc1 + vmcnt ordering; use launch_combine on other targets"
+#endif
 template <typename T, int G>
 __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
   __shared__ float bred[kBlock / kWave];
@@ -1667,7 +1680,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
                                      : false;
   if (KVECC_ATTN_FUSED_COMBINE && (gw == 1 || (KVECC_ATTN_FUSED_COMBINE_GQA && group_fits)) &&
       batch * heads <= kAttnCtrPerSlot) {
-    a.ctr = attn_counter_slot();
+    a.ctr = attn_counter_slot(stream);
     if (!a.ctr) return KVECC_EHIP;
   }
   if (codec != KVECC_CODEC_H84) {

@@ -792,7 +792,7 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
       (!KVECC_GOLAY_ROWS_DYN || cdiv(rows, rg.tr) < (1LL << 31))) {
     RegRowsArgs a{nibbles, codewords, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
                   par, nullptr};
-    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot())) return KVECC_EHIP;
+    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
     KVECC_LAUNCH(golay_encode_rows_reg_kernel, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
     return check_launch("golay_encode_rows");
@@ -828,7 +828,7 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
     if (!atab) return KVECC_EHIP;
     RegRowsArgs a{codewords, nibbles, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
                   atab, stats};
-    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot())) return KVECC_EHIP;
+    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
     const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
     if (stats)
       KVECC_LAUNCH(golay_decode_rows_reg_kernel<true>, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);

@@ -41,24 +41,27 @@ const uint32_t *golay_attn_table_dev();
 // packed decode tables, 24 KiB: uint16 [4096] parity(lo) << 2, then uint32
 // [4096] error data | (bits corrected & 3) << 24 | uncorrectable << 31
 const uint8_t *golay_pk_table_dev();
-// Work counters of the dynamically scheduled tile kernels (shim.hip): a ring of
-// kDynSlots slots per device, each kDynCounters counters kDynStride words apart,
-// zero between launches (each counter's last user resets it).  shim_dyn_slot() hands out the current device's slots round-robin,
-// so up to kDynSlots launches may be in flight at once.
-#ifndef KVECC_SHIM_DYN_COUNTERS
-#define KVECC_SHIM_DYN_COUNTERS 128
-#endif
-constexpr int kDynCounters = KVECC_SHIM_DYN_COUNTERS;
+// Counter slots of the dynamically scheduled kernels (runtime.hip
+// counter_slot): zero at launch, owned by one launch until it exits, left zero
+// (each counter's last user resets it).  Eager launches get one slot per
+// stream, captured launches one per (capture, stream), so two launches that
+// can overlap never share a slot.  A slot holds
+//   [0, kDynSlotWords): the work counters of the tile kernels (shim.hip,
+//     golay.hip, packed.hip; TileSchedule), kDynCounters counters kDynStride
+//     words apart;
+//   [kDynSlotWords, +kAttnCtrPerSlot): the split counters of the paged-attention
+//     fused combine, one per (batch, head group).
+constexpr int kDynCounters = 128;
 constexpr int kDynStride = 64;  // uint32 words (256 B) between counters
-constexpr int kDynSlots = 64;
 constexpr int kDynSlotWords = kDynCounters * kDynStride;
-uint32_t *shim_dyn_slot();
-// Split counters of the paged-attention kernels (one per (batch, head group);
-// the split that finishes a group combines it and resets the counter): a ring
-// of kAttnCtrSlots slots of kAttnCtrPerSlot zeroed counters per device.
-constexpr int kAttnCtrSlots = 32;
 constexpr int kAttnCtrPerSlot = 4096;
-uint32_t *attn_counter_slot();
+constexpr int kSlotWords = kDynSlotWords + kAttnCtrPerSlot;
+uint32_t *counter_slot(void *stream);  // nullptr on error (kvecc_last_error set)
+inline uint32_t *shim_dyn_slot(void *stream) { return counter_slot(stream); }
+inline uint32_t *attn_counter_slot(void *stream) {
+  uint32_t *s = counter_slot(stream);
+  return s ? s + kDynSlotWords : nullptr;
+}
 // host-side table builders (product copy, independent of the test oracle)
 void build_golay_parity_table(uint16_t *out4096);
 void build_golay_correct_table(uint16_t *out4096);

@@ -709,7 +709,7 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
   if (KVECC_PACKED_DEC_V2 && aligned(nibbles, 4) && aligned(codewords, 16) && wave_tiles > 0 &&
       wave_tiles * kPk2TileBytes < ((int64_t)1 << 31)) {
     const uint8_t *tab = golay_pk_table_dev();
-    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot() : nullptr;
+    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot(stream) : nullptr;
     if (!tab || (KVECC_PACKED_DEC_DYN && !dyn)) return KVECC_EHIP;
     const PkDecArgs a{codewords, reinterpret_cast<uint32_t *>(nibbles), uncorrectable, (uint32_t)wave_tiles,
                       tab, stats, dyn,
@@ -803,7 +803,7 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
   const int64_t hp_tiles = n / (16 * (int64_t)kHp2TileChunks);
   if (KVECC_H84_PACKED_V2 && aligned(nibbles, 8) && aligned(codewords, 16) &&
       (!error_types || aligned(error_types, 4)) && hp_tiles > 0 && n < ((int64_t)1 << 31)) {
-    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot() : nullptr;
+    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot(stream) : nullptr;
     if (KVECC_PACKED_DEC_DYN && !dyn) return KVECC_EHIP;
     const HpDecArgs a{codewords, reinterpret_cast<u32x2 *>(nibbles), reinterpret_cast<uint32_t *>(error_types),
                       (uint32_t)hp_tiles, stats, dyn};

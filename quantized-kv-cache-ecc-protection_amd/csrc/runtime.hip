@@ -9,7 +9,12 @@
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
 
 #include "kvecc_internal.h"
 
@@ -39,10 +44,6 @@ static std::atomic<uint16_t *> g_parity[kMaxDev];
 static std::atomic<uint16_t *> g_correct[kMaxDev];
 static std::atomic<uint32_t *> g_attn[kMaxDev];
 static std::atomic<uint8_t *> g_pk[kMaxDev];
-static std::atomic<uint32_t *> g_dyn[kMaxDev];  // kDynSlots work-counter slots, zeroed
-static std::atomic<uint32_t> g_dyn_next[kMaxDev];
-static std::atomic<uint32_t *> g_actr[kMaxDev];  // kAttnCtrSlots attention split counters, zeroed
-static std::atomic<uint32_t> g_actr_next[kMaxDev];
 
 int current_device() {
   int d = 0;
@@ -152,21 +153,11 @@ static int ensure_tables(int d) {
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
   if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
   Host *buf = nullptr;
-  uint32_t *dyn = nullptr;
-  const size_t dyn_bytes = sizeof(uint32_t) * kDynSlots * kDynSlotWords;
   hipError_t e = hipMalloc(&buf, sizeof(Host));
   if (e == hipSuccess) e = hipMemcpy(buf, &host, sizeof(Host), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&dyn, dyn_bytes);
-  if (e == hipSuccess) e = hipMemset(dyn, 0, dyn_bytes);
-  uint32_t *actr = nullptr;
-  const size_t actr_bytes = sizeof(uint32_t) * kAttnCtrSlots * kAttnCtrPerSlot;
-  if (e == hipSuccess) e = hipMalloc(&actr, actr_bytes);
-  if (e == hipSuccess) e = hipMemset(actr, 0, actr_bytes);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return set_error(KVECC_EHIP, "golay table upload: %s", hipGetErrorString(e));
-  g_dyn[d].store(dyn, std::memory_order_release);
-  g_actr[d].store(actr, std::memory_order_release);
   g_parity[d].store(buf->par, std::memory_order_release);
   g_correct[d].store(buf->cor, std::memory_order_release);
   g_pk[d].store(reinterpret_cast<uint8_t *>(buf->pk0), std::memory_order_release);
@@ -187,18 +178,94 @@ const uint16_t *golay_correct_table_dev() { return table_dev(g_correct); }
 const uint32_t *golay_attn_table_dev() { return table_dev(g_attn); }
 const uint8_t *golay_pk_table_dev() { return table_dev(g_pk); }
 
-uint32_t *shim_dyn_slot() {
-  const int d = current_device();
-  if (!table_dev(g_attn)) return nullptr;  // allocated with the tables
-  const uint32_t k = g_dyn_next[d].fetch_add(1, std::memory_order_relaxed) % kDynSlots;
-  return g_dyn[d].load(std::memory_order_acquire) + (size_t)k * kDynSlotWords;
+// ---- counter slots of the dynamically scheduled kernels -------------------------
+// A kernel that takes work from counters (TileSchedule) or counts finished
+// splits (the paged-attention fused combine) needs its counters zero at launch
+// and to itself until it exits; it leaves them zero (each counter's last user
+// resets it).  Both hold by stream order if a slot is never shared between
+// launches that can overlap:
+//   - eager launches: one slot per stream (per thread for hipStreamPerThread),
+//     so consecutive users of a slot are ordered by their stream;
+//   - launches captured into a graph: a slot of their own per (capture, stream),
+//     never handed out again, so replays never share with eager work or with
+//     other graphs (replaying ONE graph concurrently with itself would race on
+//     its outputs anyway).
+// Slots come zeroed from a pool that grows outside captures only (a reserve of
+// kSlotReserve free slots is kept for them).
+struct SlotPool {
+  std::mutex mu;
+  std::vector<uint32_t *> free;                        // zeroed, never handed out
+  std::unordered_map<uint64_t, uint32_t *> eager;      // stream key -> slot
+  std::map<std::pair<uint64_t, unsigned long long>, uint32_t *> captured;  // (stream, capture id) -> slot
+  std::vector<uint32_t *> chunks;
+};
+static SlotPool g_pool[kMaxDev];
+constexpr int kSlotChunk = 64;    // slots per allocation (3 MiB)
+constexpr int kSlotReserve = 32;  // free slots kept for graph captures
+
+static int grow_pool(int d, SlotPool &p) {  // p.mu held; not during a capture
+  uint32_t *mem = nullptr;
+  const size_t bytes = sizeof(uint32_t) * (size_t)kSlotChunk * kSlotWords;
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
+  if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
+  hipError_t e = hipMalloc(&mem, bytes);
+  if (e == hipSuccess) e = hipMemset(mem, 0, bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(KVECC_EHIP, "counter slots: %s", hipGetErrorString(e));
+  p.chunks.push_back(mem);
+  for (int i = kSlotChunk - 1; i >= 0; --i) p.free.push_back(mem + (size_t)i * kSlotWords);
+  return KVECC_OK;
 }
 
-uint32_t *attn_counter_slot() {
+static int ensure_pool(int d) {
+  if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
+  SlotPool &p = g_pool[d];
+  std::lock_guard<std::mutex> lk(p.mu);
+  return p.chunks.empty() ? grow_pool(d, p) : KVECC_OK;
+}
+
+uint32_t *counter_slot(void *stream) {
   const int d = current_device();
-  if (!table_dev(g_attn)) return nullptr;  // allocated with the tables
-  const uint32_t k = g_actr_next[d].fetch_add(1, std::memory_order_relaxed) % kAttnCtrSlots;
-  return g_actr[d].load(std::memory_order_acquire) + (size_t)k * kAttnCtrPerSlot;
+  if (d < 0 || d >= kMaxDev) {
+    set_error(KVECC_EINVAL, "device %d out of range", d);
+    return nullptr;
+  }
+  hipStream_t st = as_stream(stream);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long cid = 0;
+  if (hipStreamGetCaptureInfo(st, &cs, &cid) != hipSuccess) cs = hipStreamCaptureStatusNone;
+  uint64_t key = reinterpret_cast<uint64_t>(stream);
+  if (st == hipStreamPerThread)  // one handle, a different stream in every thread
+    key = (uint64_t)std::hash<std::thread::id>{}(std::this_thread::get_id()) | (1ull << 63);
+  SlotPool &p = g_pool[d];
+  std::lock_guard<std::mutex> lk(p.mu);
+  const bool capturing = cs == hipStreamCaptureStatusActive;
+  if (!capturing) {
+    auto it = p.eager.find(key);
+    if (it != p.eager.end()) return it->second;
+  } else {
+    auto it = p.captured.find({key, cid});
+    if (it != p.captured.end()) return it->second;
+  }
+  if (!capturing && p.free.size() <= (size_t)kSlotReserve && grow_pool(d, p) != KVECC_OK) return nullptr;
+  if (p.free.empty()) {
+    set_error(KVECC_EHIP,
+              "no free counter slot during graph capture (call kvecc_reserve_counter_slots before capturing)");
+    return nullptr;
+  }
+  uint32_t *s = p.free.back();
+  p.free.pop_back();
+  if (!capturing) {
+    p.eager.emplace(key, s);
+  } else {
+    // a stream is in one capture at a time: its earlier captures' entries are done
+    for (auto it = p.captured.begin(); it != p.captured.end();)
+      it = it->first.first == key ? p.captured.erase(it) : std::next(it);
+    p.captured.emplace(std::make_pair(key, cid), s);
+  }
+  return s;
 }
 
 }  // namespace kvecc
@@ -227,7 +294,47 @@ KVECC_API int kvecc_init_device(int device) {
   int n = kvecc_device_count();
   if (n <= 0) return set_error(KVECC_ENODEV, "no HIP device visible");
   if (device < 0 || device >= n) return set_error(KVECC_EINVAL, "device %d not in [0,%d)", device, n);
-  return ensure_tables(device);
+  const int rc = ensure_tables(device);
+  return rc != KVECC_OK ? rc : ensure_pool(device);
+}
+
+KVECC_API int kvecc_reserve_counter_slots(int device, int n) {
+  int nd = kvecc_device_count();
+  if (nd <= 0) return set_error(KVECC_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= nd || device >= kMaxDev || n < 0)
+    return set_error(KVECC_EINVAL, "reserve_counter_slots: bad device %d or count %d", device, n);
+  SlotPool &p = g_pool[device];
+  std::lock_guard<std::mutex> lk(p.mu);
+  while (p.free.size() < (size_t)n + kSlotReserve) {
+    const int rc = grow_pool(device, p);
+    if (rc != KVECC_OK) return rc;
+  }
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_counter_slots_check(int device, int64_t *slots_in_use, int64_t *nonzero_words) {
+  int nd = kvecc_device_count();
+  if (nd <= 0) return set_error(KVECC_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= nd || device >= kMaxDev || !slots_in_use || !nonzero_words)
+    return set_error(KVECC_EINVAL, "counter_slots_check: bad argument");
+  SlotPool &p = g_pool[device];
+  std::lock_guard<std::mutex> lk(p.mu);
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
+    return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", device);
+  hipError_t e = hipDeviceSynchronize();
+  std::vector<uint32_t> h((size_t)kSlotChunk * kSlotWords);
+  int64_t nz = 0;
+  for (uint32_t *c : p.chunks) {
+    if (e == hipSuccess) e = hipMemcpy(h.data(), c, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) break;
+    for (uint32_t v : h) nz += v != 0;
+  }
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) return set_error(KVECC_EHIP, "counter_slots_check: %s", hipGetErrorString(e));
+  *slots_in_use = (int64_t)(p.chunks.size() * kSlotChunk - p.free.size());
+  *nonzero_words = nz;
+  return KVECC_OK;
 }
 
 KVECC_API int kvecc_golay_syndrome_table_host(int32_t *out) {

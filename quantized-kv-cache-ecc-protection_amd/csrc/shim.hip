@@ -577,10 +577,14 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   if (kItemsInRegs) {  // r2: row, j2: the item's LDS byte offset in the tile
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
+      // rows past the tile (r >= tr: a lane's last items) store outside the
+      // output descriptor (dropped); their LDS reads use row tr - 1, so every
+      // LDS index stays inside the wave's tile
       const uint32_t v = lane + kWave * i;
-      it.r2[i] = v / dv;
-      it.j2[i] = it.r2[i] * a.lr + V * (v - it.r2[i] * dv);
-      it.o2[i] = (it.r2[i] * a.d + V * (v - it.r2[i] * dv)) * (uint32_t)sizeof(TO);
+      const uint32_t r = v / dv, j = v - r * dv;
+      it.r2[i] = min(r, a.tr - 1);
+      it.j2[i] = it.r2[i] * a.lr + V * j;
+      it.o2[i] = (r * a.d + V * j) * (uint32_t)sizeof(TO);
     }
   }
   uint32_t bits = 0, unc = 0;
@@ -709,20 +713,20 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         if (i * kWave >= (int)chunks) break;  // uniform
-        uint32_t r, l;
+        uint32_t r, l, o = 0;
         if (kItemsInRegs) {
           r = it.r2[i];
           l = it.j2[i];
         } else {
           const uint32_t v = lane + kWave * i;
-          r = __umulhi(v, inv_dv);
-          l = r * a.lr + V * (v - r * dv);
+          const uint32_t rv = __umulhi(v, inv_dv), j = v - rv * dv;
+          r = min(rv, a.tr - 1);  // as it.r2: LDS reads stay inside the tile
+          l = r * a.lr + V * j;
+          o = (rv * a.d + V * j) * (uint32_t)sizeof(TO);
         }
         const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + l);
         const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
-        // output byte offset: (r d + V j) sizeof(TO), with V j = l - r lr
-        const uint32_t o = kItemsInRegs ? it.o2[i] : (r * a.d + l - r * a.lr) * (uint32_t)sizeof(TO);
-        tile_store(os, o, dq16<TO>(nb, scale_all[wave][k][r], dead));
+        tile_store(os, kItemsInRegs ? it.o2[i] : o, dq16<TO>(nb, scale_all[wave][k][r], dead));
       }
     }
     if (!more) break;
@@ -939,7 +943,9 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
 #pragma unroll
       for (int i = 0; i < NI2; ++i) {
         if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
-        const uint32_t r = i2r[i], c = i2c[i];
+        // a lane's items past the tile store outside its output descriptor
+        // (dropped); their LDS reads use row tr - 1 (indices stay in the tile)
+        const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
         const uint8_t *row = stage + off0 + r * a.d + V * c;
         uint32_t q[2] = {0u, 0u};
 #pragma unroll
@@ -953,7 +959,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
             q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
           }
         }
-        tile_store(os, (r * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+        tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
       }
     };
     if (INTERP && !KVECC_SHIM_INTERP_NOVALU && tile_dbl)
@@ -1234,7 +1240,7 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
     a.nlb = (uint32_t)cdiv(ctx, block_size);
     a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
     a.rowb = (uint32_t)(codec == KVECC_CODEC_GOLAY_PACKED ? KVECC_GOLAY_PACKED_ROW(g) : 4 * g);
-    a.dyn = shim_dyn_slot();
+    a.dyn = shim_dyn_slot(stream);
     if (!a.dyn) return KVECC_EHIP;
     const bool pk = codec == KVECC_CODEC_GOLAY_PACKED;
     switch (out_dtype) {
@@ -1270,7 +1276,7 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
       a.tpb = (uint32_t)cdiv(block_size, a.tr);
       a.nlb = (uint32_t)cdiv(ctx, block_size);
       a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
-      a.dyn = shim_dyn_slot();
+      a.dyn = shim_dyn_slot(stream);
       if (!a.dyn) return KVECC_EHIP;
       switch (out_dtype) {
         case KVECC_F32: launch_bytes_tiles<float>(codec, interp, a, st); break;

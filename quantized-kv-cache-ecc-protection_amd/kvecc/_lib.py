@@ -27,6 +27,8 @@ SIGNATURES = {
     "kvecc_device_count": [],
     "kvecc_time_next_launch": [_vp, _vp],
     "kvecc_init_device": [_int],
+    "kvecc_reserve_counter_slots": [_int, _int],
+    "kvecc_counter_slots_check": [_int, _vp, _vp],
     "kvecc_golay_syndrome_table_host": [_vp],
     "kvecc_golay_h_row_masks_host": [_vp],
     "kvecc_ber_threshold": [_f32],

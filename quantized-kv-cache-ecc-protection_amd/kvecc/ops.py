@@ -34,6 +34,22 @@ def _ptr(t):
     return _VP(t.data_ptr()) if t is not None else _VP(0)
 
 
+def _sptr(stats, device):
+    """Pointer to a statistics buffer (or NULL), validated: the kernels add at
+    slot (workgroup % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE of a contiguous
+    int64 buffer on the launch device, so anything shorter, of another dtype,
+    strided or elsewhere would be written past or misread."""
+    if stats is None:
+        return _VP(0)
+    if (not isinstance(stats, torch.Tensor) or stats.dtype != torch.int64 or not stats.is_contiguous()
+            or stats.numel() < STATS_SLOTS * STATS_STRIDE or stats.device != torch.device(device)):
+        raise ValueError(f"stats must be a contiguous int64 tensor of >= {STATS_SLOTS * STATS_STRIDE} "
+                         f"elements on {device} (ops.new_stats), got "
+                         f"{getattr(stats, 'dtype', type(stats))} {tuple(getattr(stats, 'shape', ()))} "
+                         f"on {getattr(stats, 'device', None)}")
+    return _VP(stats.data_ptr())
+
+
 def _stream(device):
     return _VP(torch.cuda.current_stream(device).cuda_stream)
 
@@ -51,6 +67,22 @@ def _ensure_device(device):
         _lib.call("kvecc_init_device", idx)
         _ready.add(idx)
     return idx
+
+
+def reserve_counter_slots(n, device=None):
+    """Make n counter slots available for launches captured into HIP graphs
+    (kvecc_reserve_counter_slots; each captured stream takes one slot per capture)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    _lib.call("kvecc_reserve_counter_slots", _ensure_device(dev), int(n))
+
+
+def counter_slots_check(device=None):
+    """(slots handed out, non-zero counter words) of a device (kvecc_counter_slots_check;
+    synchronises it).  Non-zero words with no launch in flight would be a scheduling bug."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    used, nz = ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.call("kvecc_counter_slots_check", _ensure_device(dev), ctypes.byref(used), ctypes.byref(nz))
+    return used.value, nz.value
 
 
 STATS_SLOTS = 32    # KVECC_STATS_SLOTS
@@ -113,13 +145,13 @@ def hamming84_encode_into(flat_in, out):
 
 def hamming74_decode_into(flat_cw, data, flag=None, stats=None):
     _lib.call("kvecc_hamming74_decode", _ptr(flat_cw), _ptr(data), _ptr(flag), flat_cw.numel(),
-              _ptr(stats), _stream(flat_cw.device))
+              _sptr(stats, flat_cw.device), _stream(flat_cw.device))
     return data
 
 
 def hamming84_decode_into(flat_cw, data, error_type=None, stats=None):
     _lib.call("kvecc_hamming84_decode", _ptr(flat_cw), _ptr(data), _ptr(error_type),
-              flat_cw.numel(), _ptr(stats), _stream(flat_cw.device))
+              flat_cw.numel(), _sptr(stats, flat_cw.device), _stream(flat_cw.device))
     return data
 
 
@@ -194,7 +226,7 @@ def golay_encode_into(flat_triplets, codewords, m):
 def golay_decode_into(flat_cw, triplets, counts=None, stats=None):
     _ensure_device(flat_cw.device)
     _lib.call("kvecc_golay_decode", _ptr(flat_cw), _ptr(triplets), _ptr(counts), flat_cw.numel(),
-              _ptr(stats), _stream(flat_cw.device))
+              _sptr(stats, flat_cw.device), _stream(flat_cw.device))
     return triplets
 
 
@@ -257,7 +289,7 @@ def golay_decode_rows(codewords: torch.Tensor, d: int, stats=None) -> torch.Tens
     rows = flat.numel() // g if g else 0
     out = torch.empty(*codewords.shape[:-1], d, dtype=torch.uint8, device=codewords.device)
     _ensure_device(codewords.device)
-    _lib.call("kvecc_golay_decode_rows", _ptr(flat), _ptr(out), rows, d, _ptr(stats),
+    _lib.call("kvecc_golay_decode_rows", _ptr(flat), _ptr(out), rows, d, _sptr(stats, codewords.device),
               _stream(codewords.device))
     return out
 
@@ -288,7 +320,7 @@ def golay_decode_rows_into(codewords: torch.Tensor, out: torch.Tensor, stats=Non
         raise ValueError("golay_decode_rows_into: contiguous int32 [..., ceil(D/3)] -> uint8 [..., D]")
     rows = codewords.numel() // g if g else 0
     _ensure_device(codewords.device)
-    _lib.call("kvecc_golay_decode_rows", _ptr(codewords), _ptr(out), rows, d, _ptr(stats), _stream(codewords.device))
+    _lib.call("kvecc_golay_decode_rows", _ptr(codewords), _ptr(out), rows, d, _sptr(stats, codewords.device), _stream(codewords.device))
 
 
 
@@ -308,7 +340,7 @@ def inject_into(flat_in, out, ber, n_bits, seed=0, counts=None, stats=None, glob
     else:
         raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
     _lib.call(name, _ptr(flat_in), _ptr(out), _ptr(counts), n, int(n_bits), int(seed), float(ber),
-              gn, int(offset0), _ptr(stats), _stream(flat_in.device))
+              gn, int(offset0), _sptr(stats, flat_in.device), _stream(flat_in.device))
     return out
 
 
@@ -321,7 +353,7 @@ def inject_rows_into(flat_in, out, rows, row_len, ber, n_bits, seed_base, stats=
     else:
         raise ValueError(f"Unsupported dtype: {flat_in.dtype}. Use uint8 or int32.")
     _lib.call(name, _ptr(flat_in), _ptr(out), int(rows), int(row_len), int(n_bits), int(seed_base),
-              float(ber), _ptr(stats), _stream(flat_in.device))
+              float(ber), _sptr(stats, flat_in.device), _stream(flat_in.device))
     return out
 
 
@@ -377,7 +409,7 @@ def inject_bit_errors_triton_vectorized(data, ber, n_bits, seed=0, return_stats=
     out = torch.empty_like(flat)
     stats = new_stats(data.device) if return_stats else None
     _lib.call(name, _ptr(flat), _ptr(out), _VP(0), flat.numel(), int(n_bits), int(seed), float(ber),
-              _ptr(stats), _stream(data.device))
+              _sptr(stats, data.device), _stream(data.device))
     out = out.view(data.shape)
     if return_stats:
         flips, affected = read_stats(stats)
@@ -417,7 +449,7 @@ def count_ne_into(a, b, stats):
     if a.dtype != torch.uint8 or b.dtype != torch.uint8 or a.numel() != b.numel() or a.device != b.device:
         raise ValueError("count_ne_into: two uint8 tensors of one size on one device")
     a, b = a.contiguous(), b.contiguous()
-    _lib.call("kvecc_count_ne_u8", _ptr(a), _ptr(b), a.numel(), _ptr(stats), _stream(a.device))
+    _lib.call("kvecc_count_ne_u8", _ptr(a), _ptr(b), a.numel(), _sptr(stats, a.device), _stream(a.device))
     return stats
 
 
@@ -562,7 +594,7 @@ def quantize_rows(input_tensor, scale_rule=None):
 def decode_dequant_h84_into(cw2d, scales, out, zero_doubles=True, stats=None):
     rows, d = cw2d.shape
     _lib.call("kvecc_decode_dequant_h84_rows", _ptr(cw2d), _ptr(scales), _ptr(out), _DT[out.dtype],
-              rows, d, int(bool(zero_doubles)), _ptr(stats), _stream(cw2d.device))
+              rows, d, int(bool(zero_doubles)), _sptr(stats, cw2d.device), _stream(cw2d.device))
     return out
 
 
@@ -643,7 +675,7 @@ def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=
               _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table), int(ctx),
               manager.num_kv_heads, manager.head_dim, manager.num_layers, manager.block_size,
               int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
-              _DT[out_dtype], _ptr(stats), _stream(dev))
+              _DT[out_dtype], _sptr(stats, dev), _stream(dev))
     return k_out, v_out
 
 
@@ -722,7 +754,7 @@ def shim_read_batch(k_cache, v_cache, k_scales, v_scales, block_table, ctx, head
     _lib.call("kvecc_shim_read_batch", _ptr(k_cache), _ptr(v_cache), _ptr(k_scales), _ptr(v_scales),
               _ptr(block_table), block_table.shape[1], batch, int(ctx), hkv, head_dim, nl, bs,
               int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
-              _DT[out_dtype], _ptr(stats), _stream(k_cache.device))
+              _DT[out_dtype], _sptr(stats, k_cache.device), _stream(k_cache.device))
     return k_out, v_out
 
 
@@ -931,7 +963,7 @@ def golay_decode_packed_into(codewords, nibbles, uncorrectable=None, m=None, sta
     _check_packed_bufs("golay_decode_packed_into", m, (codewords, 3 * m, "codewords"),
                        (nibbles, (3 * m + 1) // 2, "nibbles"), (uncorrectable, (m + 7) // 8, "uncorrectable"))
     _lib.call("kvecc_golay_decode_packed", _ptr(codewords), _ptr(nibbles), _ptr(uncorrectable), m,
-              _ptr(stats), _stream(codewords.device))
+              _sptr(stats, codewords.device), _stream(codewords.device))
     return nibbles
 
 
@@ -962,7 +994,7 @@ def golay_decode_packed(codewords: torch.Tensor, m: int, return_uncorrectable: b
     flags = torch.empty((m + 7) // 8, dtype=torch.uint8, device=dev) if return_uncorrectable else None
     st = new_stats(dev) if stats is None else stats
     _ensure_device(dev)
-    _lib.call("kvecc_golay_decode_packed", _ptr(cw), _ptr(nib), _ptr(flags), int(m), _ptr(st),
+    _lib.call("kvecc_golay_decode_packed", _ptr(cw), _ptr(nib), _ptr(flags), int(m), _sptr(st, dev),
               _stream(dev))
     if stats is not None:
         return (nib, flags) if return_uncorrectable else nib
@@ -996,7 +1028,7 @@ def hamming84_decode_packed_into(codewords, nibbles, error_types=None, n=None, s
     _check_packed_bufs("hamming84_decode_packed_into", n, (codewords, n, "codewords"),
                        (nibbles, (n + 1) // 2, "nibbles"), (error_types, (n + 3) // 4, "error_types"))
     _lib.call("kvecc_hamming84_decode_packed", _ptr(codewords), _ptr(nibbles), _ptr(error_types), n,
-              _ptr(stats), _stream(codewords.device))
+              _sptr(stats, codewords.device), _stream(codewords.device))
     return nibbles
 
 

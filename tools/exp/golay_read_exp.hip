@@ -1,0 +1,313 @@
+// golay_read_exp.hip -- experimental variants of the fused Golay read
+// (csrc/shim.hip shim_read_golay_tiles_kernel), NOT shipped.  Built with the
+// product sources (this file #includes shim.hip for its tile helpers) into
+// tools/exp/libgread.so; tools/exp/run_golay_read_exp.py times every variant
+// against the product kernel in one process and compares the outputs.
+//
+// Variant axes (template parameters, so one library holds all of them and a
+// rocprofv3 run tells them apart by kernel name):
+//   SCHED  0: the product's persistent grid + dynamic tail; 1: a full grid,
+//          wave w takes tiles [w CHUNK, w CHUNK + CHUNK) and workgroups retire
+//   STAGE  0: tables staged first (VGPR copy), then the first tile's loads (the
+//          product); 1: the first tile's loads first, then the VGPR copy;
+//          2: the first tile's loads first, then the tables by LDS-DMA
+//          (global_load_lds_dwordx4: no VGPRs, no wait before the barrier)
+//   GATHER 0: the real table lookups; 1: lookups at lane-private, conflict-free
+//          addresses (same instruction count, WRONG values: attributes the LDS
+//          bank conflicts); 2: no lookups (WRONG values: the memory ceiling)
+//   SPLITP the parity half as two 64-entry tables (16.5 KiB of tables)
+//   PAD    extra bytes per staged row in the phase-2 tile
+//   BLOCK  threads per workgroup
+#include "../../quantized-kv-cache-ecc-protection_amd/csrc/shim.hip"
+
+namespace kvecc {
+namespace exp {
+
+template <int SCHED, int CHUNK, int STAGE, int GATHER, int SPLITP, int PAD, int BLOCK, bool PACKED, int PCT = 65>
+__global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a) {
+  using TO = __half;
+  constexpr int kW = BLOCK / kWave;
+  // GATHER 3: only the split parity tables in LDS; the correction entry comes
+  // from the global table (16 KiB, cache-resident; ~79 % of lanes read entry 0)
+  constexpr int kTab = GATHER == 3 ? 128 : SPLITP ? 128 + 4096 : 8192;
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTab];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kW][kTileStage];
+  __shared__ float scale_all[kW][kWave];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  const uint32_t nwaves = gridDim.x * kW;
+  const uint32_t lr = a.lr + PAD;
+  const uint32_t groups = a.tr * a.gpr;
+  constexpr int V = kVpl<TO>, NC = kTileChunks * 8 / V;
+  const uint32_t dv = a.d / V;
+  const uint32_t chunks = a.tr * dv;
+  TileItems it;
+#pragma unroll
+  for (int i = 0; i < kTileGroups; ++i) {
+    const uint32_t f = lane + kWave * i;
+    it.r1[i] = f / a.gpr;
+    it.q1[i] = f - it.r1[i] * a.gpr;
+  }
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const uint32_t v = lane + kWave * i;
+    it.r2[i] = v / dv;
+    it.j2[i] = it.r2[i] * lr + V * (v - it.r2[i] * dv);
+    it.o2[i] = (it.r2[i] * a.d + V * (v - it.r2[i] * dv)) * (uint32_t)sizeof(TO);
+  }
+  uint32_t bits = 0, unc = 0;
+  const uint32_t gw = blockIdx.x * kW + wave;
+  uint32_t u = SCHED ? gw * CHUNK : gw;
+  const uint32_t uend = SCHED ? min(a.units, u + CHUNK) : a.units;
+  TileSchedule<SCHED == 0> sched;
+  ShimTile cur;
+  u32x4 w[kTileGroups];
+  float scale;
+  const bool active = u < uend;
+  auto stage_tables = [&]() {
+    if (STAGE == 2) {
+      // LDS-DMA: each wave-instruction writes 1 KiB (lane l at base + 16 l)
+      const char *src = reinterpret_cast<const char *>(a.atab);
+      if (SPLITP) {
+        // parity pieces are gathers (entries i and i << 6): plain copy below
+      } else {
+        for (int c = wave; c < 32; c += kW)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 1024 * c + 16 * lane),
+                                           reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                               reinterpret_cast<uintptr_t>(tab) + 1024 * c),
+                                           16, 0, 0);
+        return;
+      }
+    }
+    if (GATHER == 3) {
+      for (int i = threadIdx.x; i < 128; i += BLOCK) tab[i] = a.atab[i < 64 ? i : (i - 64) << 6];
+    } else if (SPLITP) {
+      for (int i = threadIdx.x; i < 128; i += BLOCK) tab[i] = a.atab[i < 64 ? i : (i - 64) << 6];
+      const u32x4 *s4 = reinterpret_cast<const u32x4 *>(a.atab + 4096);
+      u32x4 *d4 = reinterpret_cast<u32x4 *>(tab + 128);
+      for (int i = threadIdx.x; i < 1024; i += BLOCK) d4[i] = s4[i];
+    } else {
+      const u32x4 *s4 = reinterpret_cast<const u32x4 *>(a.atab);
+      u32x4 *d4 = reinterpret_cast<u32x4 *>(tab);
+#pragma unroll
+      for (int i = threadIdx.x; i < 2048; i += BLOCK) d4[i] = s4[i];
+    }
+  };
+  if (STAGE == 0) {
+    stage_tables();
+    __syncthreads();
+    if (!active) return;
+    if (SCHED == 0) sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
+    cur = shim_tile(a, u);
+    tile_issue<PACKED>(a, cur, lane, it, w, scale);
+  } else {
+    // the first tile's loads go out before the tables (a full grid has no
+    // inactive waves; a persistent one may: they still help stage)
+    if (active) {
+      if (SCHED == 0) sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
+      cur = shim_tile(a, u);
+      tile_issue<PACKED>(a, cur, lane, it, w, scale);
+    }
+    stage_tables();
+    if (STAGE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!active) return;
+  }
+  uint8_t *stage = stage_all[wave];
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.atab + 4096), 0, 16384, 0x00020000);
+  for (;;) {
+    scale_all[wave][lane] = scale;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kTileGroups; ++i) {
+      if (i * kWave >= (int)groups) break;
+      const uint32_t q = it.q1[i];
+      uint32_t sp[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t cw = tile_cw<PACKED>(w[i], c);
+        if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
+        const char *tb = reinterpret_cast<const char *>(tab);
+        uint32_t p, e;
+        if (GATHER == 2) {
+          p = cw;
+          e = 0;
+        } else if (GATHER == 3) {
+          p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0xFCu)) ^
+              *reinterpret_cast<const uint32_t *>(tb + 256 + ((cw >> 4) & 0xFCu));
+          e = __builtin_amdgcn_raw_buffer_load_b32(crs, ((cw >> 10) ^ (p >> 18)) & 0x3FFCu, 0, 0);
+        } else if (GATHER == 1) {  // bank = lane % 32: conflict-free, data-dependent row
+          p = *reinterpret_cast<const uint32_t *>(tb + 4 * ((lane & 31u) + 32u * (cw & 127u)));
+          e = *reinterpret_cast<const uint32_t *>(tb + 4 * (kTab - 4096) +
+                                                   4 * ((lane & 31u) + 32u * (((cw >> 12) ^ p) & 127u)));
+        } else {
+          if (SPLITP)
+            p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0xFCu)) ^
+                *reinterpret_cast<const uint32_t *>(tb + 256 + ((cw >> 4) & 0xFCu));
+          else
+            p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
+          e = *reinterpret_cast<const uint32_t *>(tb + 4 * (kTab - 4096) + (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
+        }
+        sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
+        cnt += e >> 24;
+      }
+      if (it.r1[i] < a.tr) {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(stage + it.r1[i] * lr + 12 * q);
+        dst[0] = sp[0] | sp[1] << 24;
+        dst[1] = sp[1] >> 8 | sp[2] << 16;
+        dst[2] = sp[2] >> 16 | sp[3] << 8;
+      }
+    }
+    bits += cnt & 63u;
+    unc += cnt >> 6;
+    wave_lds_sync();
+    const ShimTile t = cur;
+    u = SCHED == 0 ? sched.next(u, lane) : u + 1;
+    const bool more = u < uend;
+    if (more) {
+      cur = shim_tile(a, u);
+      tile_issue<PACKED>(a, cur, lane, it, w, scale);
+    }
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      if (i * kWave >= (int)chunks) break;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + it.j2[i]);
+      const uint32_t nb[2] = {src[0], src[1]};
+      tile_store(os, it.o2[i], dq16<TO>(nb, scale_all[wave][min(it.r2[i], a.tr - 1)], dead));
+    }
+    if (!more) break;
+    wave_lds_sync();
+  }
+  bits = wave_sum(bits);
+  unc = wave_sum(unc);
+  if (lane == 0) {
+    uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
+    if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+  }
+}
+
+struct Variant {
+  const char *name;
+  void (*kern)(ShimTileArgs);
+  int sched, chunk, block;
+};
+
+#define GV(NAME, S, C, ST, G, SP, PD, B, PK) \
+  {NAME, golay_read_exp_kernel<S, C, ST, G, SP, PD, B, PK>, S, C, B}
+#define GVP(NAME, B, PK, PCT) {NAME, golay_read_exp_kernel<0, 1, 0, 0, 0, 0, B, PK, PCT>, 0, 1, B}
+
+static const Variant kVariants[] = {
+    // persistent (product schedule)
+    GV("pers", 0, 1, 0, 0, 0, 0, 512, false),
+    GV("pers_cfree", 0, 1, 0, 1, 0, 0, 512, false),
+    GV("pers_nogather", 0, 1, 0, 2, 0, 0, 512, false),
+    GV("pers_pad8", 0, 1, 0, 0, 0, 8, 512, false),
+    GV("pers_fetch1st", 0, 1, 1, 0, 0, 0, 512, false),
+    GV("pers_glds", 0, 1, 2, 0, 0, 0, 512, false),
+    // full grid
+    GV("full1_s0", 1, 1, 0, 0, 0, 0, 512, false),
+    GV("full1_s1", 1, 1, 1, 0, 0, 0, 512, false),
+    GV("full1_glds", 1, 1, 2, 0, 0, 0, 512, false),
+    GV("full2_glds", 1, 2, 2, 0, 0, 0, 512, false),
+    GV("full4_glds", 1, 4, 2, 0, 0, 0, 512, false),
+    GV("full1_glds_b1024", 1, 1, 2, 0, 0, 0, 1024, false),
+    GV("full2_glds_b1024", 1, 2, 2, 0, 0, 0, 1024, false),
+    GV("full1_splitp_s1", 1, 1, 1, 0, 1, 0, 512, false),
+    GV("full2_splitp_s1", 1, 2, 1, 0, 1, 0, 512, false),
+    GV("full1_glds_nogather", 1, 1, 2, 2, 0, 0, 512, false),
+    GV("full1_glds_cfree", 1, 1, 2, 1, 0, 0, 512, false),
+    // packed
+    GV("pk_pers", 0, 1, 0, 0, 0, 0, 512, true),
+    GV("pk_full1_glds", 1, 1, 2, 0, 0, 0, 512, true),
+    GV("pk_full2_glds", 1, 2, 2, 0, 0, 0, 512, true),
+    // persistent grids of other workgroup sizes / static shares (waves per CU =
+    // block / 64 * per_cu)
+    GVP("pers_b256", 256, false, 65),
+    GVP("pers_b384", 384, false, 65),
+    GVP("pers_b768", 768, false, 65),
+    GVP("pers_b1024", 1024, false, 65),
+    GVP("pers_b256_p50", 256, false, 50),
+    GVP("pers_b256_p75", 256, false, 75),
+    GVP("pers_b512_p50", 512, false, 50),
+    GVP("pers_b512_p75", 512, false, 75),
+    GVP("pk_pers_b256", 256, true, 65),
+    GVP("pk_pers_b384", 384, true, 65),
+    GVP("pk_pers_b768", 768, true, 65),
+    // global correction table, split parity in LDS (0.5 KiB staged per workgroup)
+    GV("full1_gc", 1, 1, 0, 3, 1, 0, 512, false),
+    GV("full2_gc", 1, 2, 0, 3, 1, 0, 512, false),
+    GV("full1_gc_b256", 1, 1, 0, 3, 1, 0, 256, false),
+    GV("full2_gc_b256", 1, 2, 0, 3, 1, 0, 256, false),
+    GV("pers_gc", 0, 1, 0, 3, 1, 0, 512, false),
+    GV("full1_splitp_s0", 1, 1, 0, 0, 1, 0, 512, false),
+    GV("full2_splitp_s0", 1, 2, 0, 0, 1, 0, 512, false),
+    GV("pk_full1_gc", 1, 1, 0, 3, 1, 0, 512, true),
+    GV("pk_full1_gc_b256", 1, 1, 0, 3, 1, 0, 256, true),
+};
+
+}  // namespace exp
+}  // namespace kvecc
+
+extern "C" {
+
+__attribute__((visibility("default"))) int kvecc_exp_gread_count(void) {
+  return (int)(sizeof(kvecc::exp::kVariants) / sizeof(kvecc::exp::kVariants[0]));
+}
+
+__attribute__((visibility("default"))) const char *kvecc_exp_gread_name(int v) {
+  return kvecc::exp::kVariants[v].name;
+}
+
+// the fused Golay read of shim_read_batch (fp16 out, statistics on) through
+// variant v; per_cu: persistent workgroups per CU; lds_pad: dynamic LDS bytes
+__attribute__((visibility("default"))) int kvecc_exp_gread(int v, const void *k_cache, const void *v_cache,
+                                                          const float *k_scales, const float *v_scales,
+                                                          const int32_t *table, int64_t tstride, int64_t batch,
+                                                          int64_t ctx, int64_t hkv, int64_t d, int64_t block_size,
+                                                          int packed, void *k_out, void *v_out, uint64_t *stats,
+                                                          int per_cu, int lds_pad, void *stream) {
+  using namespace kvecc;
+  const exp::Variant &var = exp::kVariants[v];
+  ShimTileArgs a{};
+  a.cache[0] = k_cache;
+  a.cache[1] = v_cache;
+  a.scales[0] = k_scales;
+  a.scales[1] = v_scales;
+  a.out[0] = k_out;
+  a.out[1] = v_out;
+  a.table = table;
+  a.atab = golay_attn_table_dev();
+  a.stats = stats;
+  const int64_t g = (d + 2) / 3, gpr = cdiv(g, 4), lr = 12 * gpr;
+  a.tstride = (uint32_t)tstride;
+  a.hkv = (uint32_t)hkv;
+  a.d = (uint32_t)d;
+  a.g = (uint32_t)g;
+  a.layers = 1;
+  a.bs = (uint32_t)block_size;
+  a.layer = 0;
+  a.ctx = (uint32_t)ctx;
+  a.gpr = (uint32_t)gpr;
+  a.lr = (uint32_t)lr;
+  a.tr = (uint32_t)std::min<int64_t>({block_size, (kTileStage - 16) / (lr + 8), (int64_t)kWave * kTileGroups / gpr,
+                                      (int64_t)kWave, (int64_t)kWave * kTileChunks / (d / 8)});
+  a.tpb = (uint32_t)cdiv(block_size, a.tr);
+  a.nlb = (uint32_t)cdiv(ctx, block_size);
+  a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+  a.rowb = (uint32_t)(packed ? KVECC_GOLAY_PACKED_ROW(g) : 4 * g);
+  a.dyn = shim_dyn_slot(stream);
+  const int kw = var.block / kWave;
+  unsigned grid;
+  if (var.sched == 0)
+    grid = (unsigned)std::min<int64_t>(cdiv(a.units, kw), (int64_t)cu_count() * per_cu);
+  else
+    grid = (unsigned)cdiv(cdiv(a.units, var.chunk), kw);
+  KVECC_LAUNCH(var.kern, dim3(grid), dim3(var.block), (unsigned)lds_pad, as_stream(stream), a);
+  return check_launch("exp_gread");
+}
+
+}  // extern "C"
