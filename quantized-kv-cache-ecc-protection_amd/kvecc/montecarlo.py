@@ -218,6 +218,80 @@ class HipShard:
         caller.wait_stream(self.s_dec)
 
 
+class HostShard:
+    """The same shard on the host backend (kvecc.cpu_ops, C++ threads): the
+    sweep's CPU counterpart (BASELINE config 1's backend="cpu") and the check of
+    HipShard at the config's own shape.  Every step is the HIP shard's with the
+    host twin of its kernel, in the same order; counters land in a host int64
+    row.  Hamming(8,4) trials with and without interpolation share their
+    (seed, BER) injection, which is cached for the next trial."""
+
+    def __init__(self, cfg: MonteCarloConfig, rank: int, world: int, threads: int | None = None):
+        from . import cpu_ops
+        self.ops = cpu_ops
+        self.cfg = cfg
+        self.dev = torch.device("cpu")
+        self.threads = threads
+        b, l, h, d = cfg.shape
+        self.b0, self.b1 = shard_bounds(b, rank, world)
+        self.sb = self.b1 - self.b0
+        per_b = l * h * d
+        self.n_total, self.off = b * per_b, self.b0 * per_b
+        self.g = (d + 2) // 3
+        self.m_total, self.m_off = b * l * h * self.g, self.b0 * l * h * self.g
+        shape = (self.sb, l, h, d)
+        self.x = torch.zeros(shape, dtype=torch.uint8)
+        if self.sb:
+            cpu_ops.inject_into(self.x.view(-1), self.x.view(-1), 0.5, 4, cfg.data_seed,
+                                global_n=self.n_total, offset0=self.off, threads=threads)
+        self.cw8 = torch.empty(shape, dtype=torch.uint8)
+        self.cw32 = torch.empty((self.sb, l, h, self.g), dtype=torch.int32)
+        self.dec = torch.empty(shape, dtype=torch.uint8)
+        self.et = torch.empty(shape, dtype=torch.uint8)
+        self.itp = torch.empty(shape, dtype=torch.uint8)
+        self._h84 = None  # (ber, seed, injection stats) of the codewords in cw8
+
+    def run_trial(self, codec, ber, seed, row):
+        ops = self.ops
+        if self.sb == 0:
+            return row
+        x = self.x.view(-1)
+        st_inj, st_dec, st_cmp = ops.new_stats(), ops.new_stats(), ops.new_stats()
+        if codec == "golay":
+            ops.golay_encode_rows_into(self.x, self.cw32)
+            flat = self.cw32.view(-1)
+            ops.inject_into(flat, flat, ber, 24, seed, stats=st_inj, global_n=self.m_total,
+                            offset0=self.m_off, threads=self.threads)
+            self._h84 = None
+            ops.golay_decode_rows_into(self.cw32, self.dec, st_dec)
+            out = self.dec
+        else:
+            c = self.cw8.view(-1)
+            h84 = codec in ("hamming84", "hamming84_interp")
+            if h84 and self._h84 is not None and self._h84[:2] == (ber, seed):
+                st_inj.copy_(self._h84[2])
+            else:
+                (ops.hamming74_encode_into if codec == "hamming74" else ops.hamming84_encode_into)(x, c)
+                ops.inject_into(c, c, ber, N_BITS[codec], seed, stats=st_inj, global_n=self.n_total,
+                                offset0=self.off, threads=self.threads)
+                self._h84 = (ber, seed, st_inj.clone()) if h84 else None
+            if codec == "hamming74":
+                ops.hamming74_decode_into(c, self.dec.view(-1), None, st_dec)
+                out = self.dec
+            else:
+                ops.hamming84_decode_into(c, self.dec.view(-1), self.et.view(-1), st_dec)
+                out = self.dec
+                if codec == "hamming84_interp":
+                    _, l, h, d = self.cfg.shape
+                    ops.interpolate_into(self.dec.view(-1), self.et.view(-1), self.itp.view(-1), self.sb, l, h * d)
+                    out = self.itp
+        ops.count_ne_into(out.view(-1), x, st_cmp)
+        row[0:2] += ops.stats_totals(st_inj, 2).to(row.device)
+        row[2:4] += ops.stats_totals(st_dec, 2).to(row.device)
+        row[4:5] += ops.stats_totals(st_cmp, 1).to(row.device)
+        return row
+
+
 def _load_done(path):
     done = {}
     if path and os.path.exists(path):

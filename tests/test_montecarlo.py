@@ -265,3 +265,36 @@ def test_hip_sweep_gloo_world2_on_one_gpu_equals_single(gpu, tmp_path):
     res = _launch_ranks("gloo", 2, str(tmp_path / "gloo2.json"))
     assert res["backend"] == "gloo" and res["world"] == 2
     assert res["rows"] == _single_hip_rows(gpu)
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (2, 1), (3, 2)])
+def test_host_shard_matches_oracle_shard(world, rank):
+    """The host-backend shard (kvecc.cpu_ops) gives the oracle shard's counters,
+    including the cached Hamming(8,4) injection shared by the interpolating trial."""
+    cfg = mc.MonteCarloConfig(shape=(3, 40, 2, 32), bers=(1e-2, 0.05), seeds=(42, 7))
+    host = mc.HostShard(cfg, rank, world)
+    ora = OracleShard(cfg, rank, world)
+    assert np.array_equal(host.x.numpy(), ora.x)
+    for codec, ber, seed in cfg.trials():
+        a, b = torch.zeros(5, dtype=torch.int64), torch.zeros(5, dtype=torch.int64)
+        host.run_trial(codec, ber, seed, a)
+        ora.run_trial(codec, ber, seed, b)
+        assert a.tolist() == b.tolist(), (codec, ber, seed, world, rank)
+
+
+@pytest.mark.gpu
+def test_config5_full_shape_hip_sweep_equals_host_backend(gpu):
+    """BASELINE config 5 at its own shape, [8,4096,32,128]: the HIP sweep
+    (run_sweep over HipShard, trials pipelined over two streams, the per-head
+    rows kernels' dynamic schedule) against the host backend's shard, every
+    counter of every trial, for all four codecs at BER 1e-4 and 1e-2, seed 42
+    (evaluation/sweep.py:352-626; quantization_ecc_comparison.py:164-177)."""
+    cfg = mc.MonteCarloConfig(bers=(1e-4, 1e-2), seeds=(42,))
+    assert cfg.shape == (8, 4096, 32, 128)
+    rows_h, _ = mc.run_sweep(cfg, mc.HipShard(cfg, 0, 1, gpu))
+    rows_c, _ = mc.run_sweep(cfg, mc.HostShard(cfg, 0, 1))
+    assert len(rows_h) == len(rows_c) == 8
+    for a, b in zip(rows_h, rows_c):
+        assert a == b, (a, b)
+        assert a["flips"] > 0 and a["corrected"] > 0
+    assert any(r["mismatches"] > 0 for r in rows_h)  # residual errors are counted, not zero by accident

@@ -24,12 +24,15 @@ namespace kvecc {
 namespace exp {
 
 template <int SCHED, int CHUNK, int STAGE, int GATHER, int SPLITP, int PAD, int BLOCK, bool PACKED, int PCT = 65>
-__global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a) {
+__global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, const uint16_t *par16,
+                                                               const uint16_t *cor16) {
   using TO = __half;
   constexpr int kW = BLOCK / kWave;
   // GATHER 3: only the split parity tables in LDS; the correction entry comes
   // from the global table (16 KiB, cache-resident; ~79 % of lanes read entry 0)
-  constexpr int kTab = GATHER == 3 ? 128 : SPLITP ? 128 + 4096 : 8192;
+  // GATHER 4: uint16 tables, 8.25 KiB: split parity (12 bits) and the correction
+  // (data error | count << 12); the nibbles are spread by VALU
+  constexpr int kTab = GATHER == 3 ? 128 : GATHER == 4 ? (128 + 4096) / 2 : SPLITP ? 128 + 4096 : 8192;
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTab];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kW][kTileStage];
   __shared__ float scale_all[kW][kWave];
@@ -79,7 +82,13 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a) {
         return;
       }
     }
-    if (GATHER == 3) {
+    if (GATHER == 4) {
+      uint16_t *t16 = reinterpret_cast<uint16_t *>(tab);
+      for (int i = threadIdx.x; i < 128; i += BLOCK) t16[i] = par16[i < 64 ? i : (i - 64) << 6];
+      const u32x4 *s4 = reinterpret_cast<const u32x4 *>(cor16);
+      u32x4 *d4 = reinterpret_cast<u32x4 *>(t16 + 128);
+      for (int i = threadIdx.x; i < 512; i += BLOCK) d4[i] = s4[i];
+    } else if (GATHER == 3) {
       for (int i = threadIdx.x; i < 128; i += BLOCK) tab[i] = a.atab[i < 64 ? i : (i - 64) << 6];
     } else if (SPLITP) {
       for (int i = threadIdx.x; i < 128; i += BLOCK) tab[i] = a.atab[i < 64 ? i : (i - 64) << 6];
@@ -125,12 +134,22 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a) {
       const uint32_t q = it.q1[i];
       uint32_t sp[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const int c = c4;
         uint32_t cw = tile_cw<PACKED>(w[i], c);
         if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
         const char *tb = reinterpret_cast<const char *>(tab);
         uint32_t p, e;
-        if (GATHER == 2) {
+        if (GATHER == 4) {
+          const uint16_t *t16 = reinterpret_cast<const uint16_t *>(tab);
+          const uint32_t par = (uint32_t)t16[cw & 63u] ^ (uint32_t)t16[64 + ((cw >> 6) & 63u)];
+          const uint32_t c = t16[128 + (((cw >> 12) ^ par) & 0xFFFu)];  // error | count << 12
+          const uint32_t x = (cw ^ c) & 0xFFFu;
+          sp[c4] = (x & 0xFu) | (x & 0xF0u) << 4 | (x & 0xF00u) << 8;
+          const uint32_t n = c >> 12;  // 0-3 bits corrected, 4 = uncorrectable
+          cnt += n + (n >> 2) * 60u;  // (n & 3) | uncorrectable << 6
+          continue;
+        } else if (GATHER == 2) {
           p = cw;
           e = 0;
         } else if (GATHER == 3) {
@@ -190,9 +209,135 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a) {
   }
 }
 
+// Two tiles of codeword loads in flight per wave: while tile t is decoded and
+// stored, the loads of t + 1 (issued one tile earlier) and t + 2 (issued after
+// t's phase 1) are outstanding.  Persistent grid with the product's schedule.
+template <int BLOCK, bool PACKED, int PCT>
+__global__ __launch_bounds__(BLOCK) void golay_read_pf2_kernel(ShimTileArgs a, const uint16_t *, const uint16_t *) {
+  using TO = __half;
+  constexpr int kW = BLOCK / kWave;
+  __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kW][kTileStage];
+  __shared__ float scale_all[kW][kWave];
+  {
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(a.atab);
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(tab);
+#pragma unroll
+    for (int i = threadIdx.x; i < 2048; i += BLOCK) d4[i] = s4[i];
+  }
+  __syncthreads();
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  const uint32_t nwaves = gridDim.x * kW;
+  const uint32_t groups = a.tr * a.gpr;
+  constexpr int V = kVpl<TO>, NC = kTileChunks * 8 / V;
+  const uint32_t dv = a.d / V;
+  const uint32_t chunks = a.tr * dv;
+  TileItems it;
+#pragma unroll
+  for (int i = 0; i < kTileGroups; ++i) {
+    const uint32_t f = lane + kWave * i;
+    it.r1[i] = f / a.gpr;
+    it.q1[i] = f - it.r1[i] * a.gpr;
+  }
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const uint32_t v = lane + kWave * i;
+    const uint32_t r = v / dv, j = v - r * dv;
+    it.r2[i] = min(r, a.tr - 1);
+    it.j2[i] = it.r2[i] * a.lr + V * j;
+    it.o2[i] = (r * a.d + V * j) * (uint32_t)sizeof(TO);
+  }
+  uint32_t bits = 0, unc = 0;
+  const uint32_t gw = blockIdx.x * kW + wave;
+  if (gw >= a.units) return;
+  TileSchedule<true> sched;
+  sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
+  uint8_t *stage = stage_all[wave];
+  struct Buf {
+    ShimTile t;
+    u32x4 w[kTileGroups];
+    float s;
+    bool v;
+  };
+  Buf A, B;
+  uint32_t ulast = gw;  // the index of the most recently issued tile
+  bool done = false;    // the schedule ran out
+  auto refill = [&](Buf &x) {
+    x.v = false;
+    if (done) return;
+    ulast = sched.next(ulast, lane);
+    if (ulast >= a.units) {
+      done = true;
+      return;
+    }
+    x.v = true;
+    x.t = shim_tile(a, ulast);
+    tile_issue<PACKED>(a, x.t, lane, it, x.w, x.s);
+  };
+  A.v = true;
+  A.t = shim_tile(a, gw);
+  tile_issue<PACKED>(a, A.t, lane, it, A.w, A.s);
+  refill(B);
+  auto process = [&](Buf &x) {
+    scale_all[wave][lane] = x.s;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kTileGroups; ++i) {
+      if (i * kWave >= (int)groups) break;
+      const uint32_t q = it.q1[i];
+      uint32_t sp[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t cw = tile_cw<PACKED>(x.w[i], c);
+        if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
+        const char *tb = reinterpret_cast<const char *>(tab);
+        const uint32_t p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
+        const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 16384 + (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
+        sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
+        cnt += e >> 24;
+      }
+      if (it.r1[i] < a.tr) {
+        uint32_t *dst = reinterpret_cast<uint32_t *>(stage + it.r1[i] * a.lr + 12 * q);
+        dst[0] = sp[0] | sp[1] << 24;
+        dst[1] = sp[1] >> 8 | sp[2] << 16;
+        dst[2] = sp[2] >> 16 | sp[3] << 8;
+      }
+    }
+    bits += cnt & 63u;
+    unc += cnt >> 6;
+    wave_lds_sync();
+    const ShimTile t = x.t;
+    refill(x);  // the tile after the other buffer's
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      if (i * kWave >= (int)chunks) break;
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + it.j2[i]);
+      const uint32_t nb[2] = {src[0], src[1]};
+      tile_store(os, it.o2[i], dq16<TO>(nb, scale_all[wave][it.r2[i]], dead));
+    }
+    wave_lds_sync();
+  };
+  for (;;) {
+    process(A);
+    if (!B.v) break;
+    process(B);
+    if (!A.v) break;
+  }
+  bits = wave_sum(bits);
+  unc = wave_sum(unc);
+  if (lane == 0) {
+    uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
+    if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+  }
+}
+
 struct Variant {
   const char *name;
-  void (*kern)(ShimTileArgs);
+  void (*kern)(ShimTileArgs, const uint16_t *, const uint16_t *);
   int sched, chunk, block;
 };
 
@@ -247,6 +392,18 @@ static const Variant kVariants[] = {
     GV("full2_splitp_s0", 1, 2, 0, 0, 1, 0, 512, false),
     GV("pk_full1_gc", 1, 1, 0, 3, 1, 0, 512, true),
     GV("pk_full1_gc_b256", 1, 1, 0, 3, 1, 0, 256, true),
+    // uint16 tables (8.25 KiB), nibbles spread by VALU
+    GV("full1_u16", 1, 1, 0, 4, 0, 0, 512, false),
+    GV("full1_u16_b256", 1, 1, 0, 4, 0, 0, 256, false),
+    GV("full2_u16", 1, 2, 0, 4, 0, 0, 512, false),
+    GV("pers_u16", 0, 1, 0, 4, 0, 0, 512, false),
+    GV("full1_splitp_s0_b256", 1, 1, 0, 0, 1, 0, 256, false),
+    GV("pk_full1_u16", 1, 1, 0, 4, 0, 0, 512, true),
+    GV("pk_full1_splitp_s0", 1, 1, 0, 0, 1, 0, 512, true),
+    {"pf2", golay_read_pf2_kernel<512, false, 65>, 0, 1, 512},
+    {"pf2_b256", golay_read_pf2_kernel<256, false, 65>, 0, 1, 256},
+    {"pf2_p50", golay_read_pf2_kernel<512, false, 50>, 0, 1, 512},
+    {"pk_pf2", golay_read_pf2_kernel<512, true, 65>, 0, 1, 512},
 };
 
 }  // namespace exp
@@ -306,7 +463,8 @@ __attribute__((visibility("default"))) int kvecc_exp_gread(int v, const void *k_
     grid = (unsigned)std::min<int64_t>(cdiv(a.units, kw), (int64_t)cu_count() * per_cu);
   else
     grid = (unsigned)cdiv(cdiv(a.units, var.chunk), kw);
-  KVECC_LAUNCH(var.kern, dim3(grid), dim3(var.block), (unsigned)lds_pad, as_stream(stream), a);
+  KVECC_LAUNCH(var.kern, dim3(grid), dim3(var.block), (unsigned)lds_pad, as_stream(stream), a,
+               golay_parity_table_dev(), golay_correct_table_dev());
   return check_launch("exp_gread");
 }
 

@@ -269,6 +269,68 @@ def gen_shim(manifest):
     _save("shim_gpt2", manifest, {"model": cfg.to_dict(), "runs": params, "seq_len": 24}, **arrays)
 
 
+def gen_shim_fp16(manifest):
+    """SURVEY config 4 in its own dtype: the reference shim on an offline
+    random-init fp16 GPT-2 (2 layers, head_dim 32, 40 tokens = 2.5 blocks of 16),
+    Hamming(8,4) + interpolation at BER 1e-2 and 1e-3, and Golay at 1e-2.  Besides
+    logits and get_ecc_stats() it records, per layer, what ECCBackend.write was
+    given (the fp16 K/V projections) and the dequantized K/V that attend handed
+    to _run_attention (fp32 (q - 8) * scale, ecc_shim.py:1067-1071, before its
+    .to(q.dtype)), so the decode -> interpolate -> dequantize data path can be
+    pinned bit for bit, not only through the statistics."""
+    import torch
+    from transformers import GPT2Config, GPT2LMHeadModel
+    import kv_cache.ecc_shim as es
+    torch.manual_seed(1)
+    cfg = GPT2Config(n_layer=2, n_head=2, n_embd=64, n_positions=64, vocab_size=97)
+    model = GPT2LMHeadModel(cfg).eval().half()
+    ids = torch.randint(0, 97, (1, 40), generator=torch.Generator().manual_seed(5))
+    arrays = {"input_ids": ids.numpy()}
+    for k, v in model.state_dict().items():
+        arrays["w_" + k.replace(".", "__")] = v.numpy()
+    rec = {"write": [], "kv": []}
+    orig_write, orig_run = es.ECCBackend.write, es.ECCBackend._run_attention
+
+    def write(self, k, v, layer_idx, seq_id=0):
+        rec["write"].append((layer_idx, k.detach().clone(), v.detach().clone()))
+        return orig_write(self, k, v, layer_idx, seq_id)
+
+    def run_attention(self, q, k_float, v_float, device):
+        rec["kv"].append((k_float.detach().clone(), v_float.detach().clone()))
+        return orig_run(self, q, k_float, v_float, device)
+
+    es.ECCBackend.write, es.ECCBackend._run_attention = write, run_attention
+    params = []
+    try:
+        runs = [("hamming84", 1e-2, True), ("hamming84", 1e-3, True), ("golay", 1e-2, False)]
+        for i, (codec, ber, interp) in enumerate(runs):
+            rec["write"].clear()
+            rec["kv"].clear()
+            sc = es.ECCShimConfig(codec=codec, ber=ber, inject_errors=ber > 0, seed=42,
+                                  block_size=16, use_interpolation=interp)
+            t0 = time.time()
+            with torch.no_grad(), es.patch_model_with_ecc_attention(model, sc, num_blocks=16):
+                es.reset_ecc_cache(model)
+                out = model(ids)
+                st = es.get_ecc_stats(model)
+            assert out.logits.dtype == torch.float16
+            arrays[f"r{i}_logits"] = out.logits.numpy()
+            assert len(rec["write"]) == len(rec["kv"]) == cfg.n_layer
+            for (layer, k, v), (kf, vf) in zip(rec["write"], rec["kv"]):
+                assert k.dtype == torch.float16 and kf.dtype == torch.float32
+                arrays[f"r{i}_l{layer}_k_in"] = k.numpy()
+                arrays[f"r{i}_l{layer}_v_in"] = v.numpy()
+                arrays[f"r{i}_l{layer}_k_deq"] = kf.numpy()
+                arrays[f"r{i}_l{layer}_v_deq"] = vf.numpy()
+            params.append({"codec": codec, "ber": ber, "use_interpolation": interp,
+                           "stats": {k: int(v) for k, v in st.items()}})
+            print(f"    shim fp16 {codec} ber={ber} interp={interp}: {st} ({time.time() - t0:.1f}s)")
+    finally:
+        es.ECCBackend.write, es.ECCBackend._run_attention = orig_write, orig_run
+    _save("shim_gpt2_fp16", manifest, {"model": cfg.to_dict(), "runs": params, "seq_len": 40,
+                                       "dtype": "float16"}, **arrays)
+
+
 def gen_attention(manifest):
     """Pin paged_attention_ecc (kv_cache/attention_ecc.py:620-780).
 
@@ -367,7 +429,7 @@ def gen_attention(manifest):
 
 
 GENERATORS = {"hamming": gen_hamming, "golay": gen_golay, "inject": gen_inject,
-              "interp": gen_interp, "fused": gen_fused, "shim": gen_shim,
+              "interp": gen_interp, "fused": gen_fused, "shim": gen_shim, "shim_fp16": gen_shim_fp16,
               "attention": gen_attention}
 
 
