@@ -41,74 +41,41 @@ namespace kvecc {
 constexpr int kMaxSplit = 1024;   // context tokens per workgroup (upper bound)
 constexpr int kMaxSplits = 1024;  // splits per (batch, head)
 constexpr int kAttnMaxD = 256;
-#ifndef KVECC_ATTN_UNROLL
-#define KVECC_ATTN_UNROLL 4
-#endif
-// int32 Golay rows: 2 in flight measured 72.8 vs 80.0 us at 4 (H84 and packed
-// Golay lose with 2; every codec loses with 8): tools/exp/run_attn.py
-#ifndef KVECC_ATTN_GOLAY_UNROLL
-#define KVECC_ATTN_GOLAY_UNROLL 2
-#endif
-// Hamming(8,4): 2 rows in flight measured 56.9 / 57.1 us vs 60.3 / 60.0 at 4
-// (random / encoded caches, int8 table; tools/exp/run_attn.py)
-#ifndef KVECC_ATTN_H84_UNROLL
-#define KVECC_ATTN_H84_UNROLL 2
-#endif
-constexpr int kUnroll = KVECC_ATTN_UNROLL;  // token rows in flight per lane group (packed Golay)
-constexpr int kGolayUnroll = KVECC_ATTN_GOLAY_UNROLL;
-constexpr int kH84Unroll = KVECC_ATTN_H84_UNROLL;
-constexpr int kMaxUnroll = kUnroll > kGolayUnroll ? (kUnroll > kH84Unroll ? kUnroll : kH84Unroll)
-                                                  : (kGolayUnroll > kH84Unroll ? kGolayUnroll : kH84Unroll);
-// codeword words per lane of a token row (A/B knobs: tools/exp/run_attn.py)
-#ifndef KVECC_ATTN_H84_VEC
-#define KVECC_ATTN_H84_VEC 4
-#endif
-#ifndef KVECC_ATTN_GOLAY_VEC
-#define KVECC_ATTN_GOLAY_VEC 3
-#endif
-constexpr int kH84Vec = KVECC_ATTN_H84_VEC, kGolayVec = KVECC_ATTN_GOLAY_VEC;
+// Tuned constants (A/B history: DESIGN.md §3 "Paged decode attention";
+// tools/exp/run_attn.py and the experiment forks under tools/exp).
+// token rows in flight per lane group: packed Golay 4; int32 Golay 2 (72.8 vs
+// 80.0 us at 4); Hamming(8,4) 2 (56.9 / 57.1 us vs 60.3 / 60.0 at 4, random /
+// encoded caches); every codec loses with 8
+constexpr int kUnroll = 4, kGolayUnroll = 2, kH84Unroll = 2;
+constexpr int kMaxUnroll = 4;
+// codeword words per lane of a token row: H(8,4) 4 (16 codewords, one 16-byte
+// load; 8 and 32 per lane measured 57.6 and 65.0 us vs 56.9); Golay 3
+// codewords (43 -> 15 of 16 lanes busy; 6 per lane 114.0 vs 104.3 us)
+constexpr int kH84Vec = 4, kGolayVec = 3;
 // Cache rows go through raw buffer loads with 32-bit offsets when the caches
 // and scales are < 4 GiB (the BUF kernels): no 64-bit address arithmetic per
 // load, and reads past the row's last codeword need no clamp (inside the
 // buffer they read a neighbour row's words, which contribute nothing; past it
 // the hardware returns 0).  Golay 105.7 -> 82.1 us at [8,4096,32,128], H84
 // unchanged (tools/exp/run_attn.py).  Larger caches take 64-bit addressing.
-// packed-fp32 FMAs for the dot product and the V update
-#ifndef KVECC_ATTN_PK
-#define KVECC_ATTN_PK 1
-#endif
 constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
 // Packed Golay caches (KVECC_CODEC_GOLAY_PACKED, 3-byte codewords): a lane owns
 // 4 codewords = 12 bytes = 3 aligned dwords of its token row
 constexpr int kGolayPackedVec = 4;
-// Golay decode through the spread tables (golay_attn_table_dev: 32-bit entries,
+// Golay decodes through the spread tables (golay_attn_table_dev: 32-bit entries,
 // nibbles one per byte): per codeword 2 LDS reads + 9 VALU ops (address math,
 // one masked xor, three v_cvt_f32_ubyteN) instead of ~13 through the 16-bit
-// tables; 0 = the 16-bit tables (A/B: tools/exp/run_attn.py)
-#ifndef KVECC_ATTN_GOLAY_SPREAD
-#define KVECC_ATTN_GOLAY_SPREAD 1
-#endif
-// Hamming(8,4) decodes through a 256-entry LDS table of data(b) - 8: as int8
-// (ds_read_i8 + v_cvt_f32_i32; the 256 bytes are 64 dwords over 32 banks, so
-// random lookups conflict at most 2-way) or as fp32 (0; 256 dwords, ~3.5-way)
-#ifndef KVECC_ATTN_H84_LUT8
-#define KVECC_ATTN_H84_LUT8 1
-#endif
-typedef typename std::conditional<KVECC_ATTN_H84_LUT8 != 0, int8_t, float>::type h84_lut_t;
+// tables.  Hamming(8,4) decodes through a 256-entry LDS table of data(b) - 8
+// as int8 (ds_read_i8 + v_cvt_f32_i32; the 256 bytes are 64 dwords over 32
+// banks, so random lookups conflict at most 2-way, where an fp32 table's 256
+// dwords conflict ~3.5-way: 60.6 vs 63.5 us per call on random caches).
+typedef int8_t h84_lut_t;
 // Softmax in base 2: the query is pre-scaled by sm_scale * log2(e), so every
 // exponential is one v_exp_f32 (exp2) instead of expf's ~10-instruction range
-// reduction; the split maxima in the workspace are in the same log2 units
-#ifndef KVECC_ATTN_EXP2
-#define KVECC_ATTN_EXP2 1
-#endif
-__device__ __forceinline__ float attn_exp(float x) {
-#if KVECC_ATTN_EXP2
-  return __builtin_amdgcn_exp2f(x);  // exp2(-inf) = 0
-#else
-  return expf(x);
-#endif
-}
-constexpr float kAttnLogScale = KVECC_ATTN_EXP2 ? 1.4426950408889634f : 1.0f;  // log2(e)
+// reduction (Golay 76.0 -> 72.4 us); the split maxima in the workspace are in
+// the same log2 units
+__device__ __forceinline__ float attn_exp(float x) { return __builtin_amdgcn_exp2f(x); }  // exp2(-inf) = 0
+constexpr float kAttnLogScale = 1.4426950408889634f;  // log2(e)
 constexpr bool is_golay(int codec) { return codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED; }
 
 struct AttnArgs {
@@ -126,7 +93,7 @@ struct AttnArgs {
   float sm_scale;
   float empty_value;          // output when a (b, h) has no valid token
   const uint16_t *par, *cor;  // Golay tables
-  const uint32_t *atab;       // Golay spread tables (KVECC_ATTN_GOLAY_SPREAD)
+  const uint32_t *atab;       // Golay spread tables (golay_attn_table_dev)
   uint32_t *ctr;              // per-(batch, head group) split counters (attn_counter_slot), or
                               // null: a separate combine launch
 };
@@ -216,26 +183,18 @@ struct Chunk {
     } else {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        if (KVECC_ATTN_GOLAY_SPREAD) {
-          // P = spread(lo) | parity(lo) << 20; syndrome = (w >> 12) ^ parity,
-          // as a byte offset into the correction half: ((w >> 10) ^ (P >> 18)) & 0x3FFC
-          const uint32_t p = gtab[w[k] & 0xFFFu];
-          const uint32_t off = ((w[k] >> 10) ^ (p >> 18)) & 0x3FFCu;
-          const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab + 4096) + off);
-          // corrected nibbles, one per byte: (p ^ e) & 0x0F0F0F in one v_bitop3
-          // (0x28 = (S0 ^ S1) & S2); the conversions are written out because
-          // the compiler otherwise re-extracts each nibble with a shift and a mask
-          const uint32_t sp = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
-          asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(v[3 * k]) : "v"(sp));  // n, see kOffset
-          asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(v[3 * k + 1]) : "v"(sp));
-          asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(v[3 * k + 2]) : "v"(sp));
-        } else {
-          const uint16_t *t16 = reinterpret_cast<const uint16_t *>(gtab);
-          uint32_t cnt;
-          const uint32_t dw = golay_decode1(w[k], t16, t16 + 4096, cnt);
-#pragma unroll
-          for (int e = 0; e < 3; ++e) v[3 * k + e] = (float)__builtin_amdgcn_ubfe(dw, 4 * e, 4);  // n, see kOffset
-        }
+        // P = spread(lo) | parity(lo) << 20; syndrome = (w >> 12) ^ parity,
+        // as a byte offset into the correction half: ((w >> 10) ^ (P >> 18)) & 0x3FFC
+        const uint32_t p = gtab[w[k] & 0xFFFu];
+        const uint32_t off = ((w[k] >> 10) ^ (p >> 18)) & 0x3FFCu;
+        const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab + 4096) + off);
+        // corrected nibbles, one per byte: (p ^ e) & 0x0F0F0F in one v_bitop3
+        // (0x28 = (S0 ^ S1) & S2); the conversions are written out because
+        // the compiler otherwise re-extracts each nibble with a shift and a mask
+        const uint32_t sp = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
+        asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(v[3 * k]) : "v"(sp));  // n, see kOffset
+        asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(v[3 * k + 1]) : "v"(sp));
+        asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(v[3 * k + 2]) : "v"(sp));
       }
     }
   }
@@ -246,15 +205,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // sum_e q[e] * v[e] as packed FMAs (v_pk_fma_f32) into two independent lanes
 template <int E>
 __device__ __forceinline__ float dot(const float *q, const float *v) {
-  if (!KVECC_ATTN_PK) {
-    float a = 0.0f, b = 0.0f;
-#pragma unroll
-    for (int e = 0; e < E; e += 2) {
-      a = fmaf(q[e], v[e], a);
-      if (e + 1 < E) b = fmaf(q[e + 1], v[e + 1], b);
-    }
-    return a + b;
-  }
   f32x2 s = {0.0f, 0.0f};
 #pragma unroll
   for (int e = 0; e + 1 < E; e += 2) s = __builtin_elementwise_fma(f32x2{q[e], q[e + 1]}, f32x2{v[e], v[e + 1]}, s);
@@ -265,11 +215,6 @@ __device__ __forceinline__ float dot(const float *q, const float *v) {
 // acc[e] += p * v[e] as packed FMAs
 template <int E>
 __device__ __forceinline__ void axpy(float *acc, float p, const float *v) {
-  if (!KVECC_ATTN_PK) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] = fmaf(p, v[e], acc[e]);
-    return;
-  }
 #pragma unroll
   for (int e = 0; e + 1 < E; e += 2) {
     const f32x2 r = __builtin_elementwise_fma(f32x2{p, p}, f32x2{v[e], v[e + 1]}, f32x2{acc[e], acc[e + 1]});
@@ -299,14 +244,11 @@ __device__ __forceinline__ float ws_get(const float *p) {
 // folding all splits online, one thread per output value (29.5 vs 22.7 us), and
 // one wave per (b, h) with the weights by v_readlane (31.2 vs 22.5 us) -- fewer,
 // longer-lived waves each walking the splits serially.
-#ifndef KVECC_ATTN_COMBINE_PRELOAD
-#define KVECC_ATTN_COMBINE_PRELOAD 1
-#endif
 template <typename T, bool COHERENT = false>
 __device__ void combine_bh(const AttnArgs &a, int64_t bh, float *wt, float *bred) {
   const int64_t stride = a.d + 2;
   const float *ws = a.ws + bh * a.nsplit * stride;
-  if (KVECC_ATTN_COMBINE_PRELOAD && a.nsplit <= kBlock) {
+  if (a.nsplit <= kBlock) {
     // one memory round trip: thread s < nsplit loads its split's (m, l) while
     // thread d < head_dim loads its first kPre accumulators; the two block
     // reductions then run in LDS
@@ -385,60 +327,15 @@ __global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) 
   combine_bh<T>(a, blockIdx.x, wt, bred);
 }
 
-// All G > 1 heads of a group at once for the fused combine: P = kBlock / G
-// threads per head, one memory round trip (thread s < nsplit of a head loads
-// split s's (m, l); every thread the first kPre accumulators of its up to kR
-// outputs alongside), the reductions over the head's splits from LDS.  Needs
-// nsplit <= P and head_dim <= kR * P (combine_group_fits); sh: 3 kBlock floats.
-constexpr int kGroupOuts = 4;
-template <int G>
-__host__ __device__ constexpr bool combine_group_fits(int64_t nsplit, int64_t d) {
-  return G > 1 && nsplit <= kBlock / G && d <= kGroupOuts * (kBlock / G);
-}
-template <typename T, int G>
-__device__ void combine_group(const AttnArgs &a, int64_t bh0, float *sh) {
-  constexpr int P = kBlock / G, kR = kGroupOuts, kPre = 16;
-  const int t = threadIdx.x, h = t / P, u = t % P, ns = (int)a.nsplit, d = (int)a.d;
-  const int64_t stride = a.d + 2;
-  const float *ws = a.ws + (bh0 + h) * a.nsplit * stride;
-  float ov[kR][kPre];
-#pragma unroll
-  for (int r = 0; r < kR; ++r)
-#pragma unroll
-    for (int s = 0; s < kPre; ++s)
-      ov[r][s] = u + r * P < d && s < ns ? ws_get<true>(ws + s * stride + 2 + u + r * P) : 0.0f;
-  const float ms = u < ns ? ws_get<true>(ws + u * stride) : -INFINITY;
-  const float ls = u < ns ? ws_get<true>(ws + u * stride + 1) : 0.0f;
-  float *shm = sh, *shw = sh + kBlock, *shl = sh + 2 * kBlock;
-  shm[t] = ms;
-  shl[t] = ls;
-  __syncthreads();
-  const float *hm = shm + h * P, *hw = shw + h * P, *hl = shl + h * P;
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, hm[s]);
-  shw[t] = ms == -INFINITY ? 0.0f : attn_exp(ms - M);
-  __syncthreads();
-  float L = 0.0f;
-  for (int s = 0; s < ns; ++s) L += hw[s] * hl[s];
-  T *out = reinterpret_cast<T *>(a.out) + (bh0 + h) * a.d;
-#pragma unroll
-  for (int r = 0; r < kR; ++r) {
-    const int di = u + r * P;
-    if (di >= d) continue;
-    float acc = 0.0f;
-#pragma unroll
-    for (int s = 0; s < kPre; ++s) acc += ov[r][s] * (s < ns ? hw[s] : 0.0f);
-    for (int s = kPre; s < ns; ++s) acc += ws_get<true>(ws + s * stride + 2 + di) * hw[s];
-    out[di] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);
-  }
-}
-
 // Fused combine: the workgroup that finishes the last split of its (batch, head
 // group) -- counted on a.ctr[blockIdx.y] -- combines the group's G query heads
-// and resets the counter, saving the combine launch.  The workspace stores are
+// and resets the counter, saving the combine launch (the launcher uses it for
+// G = 1 only: with G heads the tail after the last split cost more than the
+// combine launch, even with all G heads combined in one round trip: 32q/8kv
+// 26.7 vs 22.3 us, profiles/r03/attn/attn_gqa19.log).  The workspace stores are
 // sc1 (ws_put) and every thread waits for its own before the count; the last
 // workgroup reads the entries with sc1 loads.  wt: kMaxSplits floats of LDS the
-// caller no longer needs (3 kBlock for G > 1).
+// caller no longer needs.
 //
 // Why no release/acquire: on gfx942/gfx950 an sc1 store (ws_put) is performed
 // at the memory side (it bypasses the non-coherent per-XCD L2 state for this
@@ -465,27 +362,12 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
   }
   __syncthreads();
   if (!last) return;
-  if constexpr (G > 1) {
-    if (combine_group_fits<G>(a.nsplit, a.d)) return combine_group<T, G>(a, bh0, wt);
-  }
   for (int j = 0; j < G; ++j) {
     if (j) __syncthreads();
     combine_bh<T, true>(a, bh0 + j, wt, bred);
   }
 }
 
-#ifndef KVECC_ATTN_GQA_PREFETCH
-#define KVECC_ATTN_GQA_PREFETCH 1
-#endif
-// minimum waves per SIMD the register allocation must allow (0: no bound)
-#ifndef KVECC_ATTN_MIN_WAVES
-#define KVECC_ATTN_MIN_WAVES 0
-#endif
-#if KVECC_ATTN_MIN_WAVES
-#define KVECC_ATTN_BOUNDS __launch_bounds__(kBlock, KVECC_ATTN_MIN_WAVES)
-#else
-#define KVECC_ATTN_BOUNDS __launch_bounds__(kBlock)
-#endif
 
 // GQA (G > 1): workgroup (split, y) serves the G query heads hg*G .. hg*G+G-1
 // of batch b = y / (H/G), which share one cache head: each K and V row is
@@ -493,7 +375,7 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
 // state and an accumulator per head), where one workgroup per query head read
 // and decoded every cache row H/Hkv times.
 template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1>
-__global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
+__global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
@@ -505,7 +387,7 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   // parity[4096] then correct[4096] as uint16 (16 KiB).  With the spread
   // tables the block-table slice (before the copy) and the merge buffer (after
   // the loop) live in the same LDS, which keeps 4 workgroups per CU.
-  constexpr bool kSpread = is_golay(CODEC) && KVECC_ATTN_GOLAY_SPREAD;
+  constexpr bool kSpread = is_golay(CODEC);
   constexpr int kTabWords = !is_golay(CODEC) ? 4 : kSpread ? 8192 : 4096;
   static_assert(!kSpread || (TP * W * E <= kTabWords && kMaxSplit + 1 <= kTabWords), "LDS aliasing");
   __shared__ __attribute__((aligned(16))) uint32_t gtab[kTabWords];
@@ -615,7 +497,7 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
   // GQA workgroups (G > 1) do G times the arithmetic per row and have a
   // quarter of MHA's rows: they issue the next iteration's rows before using
   // this one's (MHA measured no gain from that in round 1)
-  constexpr bool kPrefetch = G > 1 && CODEC == KVECC_CODEC_H84 && KVECC_ATTN_GQA_PREFETCH;
+  constexpr bool kPrefetch = G > 1 && CODEC == KVECC_CODEC_H84;
   C pkc[U], pvc[U];
   float pks[U], pvs[U];
   bool pok[U];
@@ -785,49 +667,27 @@ __global__ KVECC_ATTN_BOUNDS void paged_attn_split_kernel(AttnArgs a) {
 // per lane on its 8 scores (head maxima across the 4 lanes of a head with two
 // xor-shuffles), the workgroup's 4 waves merge through LDS, and the split goes
 // to the workspace of the combine kernel above.
-#ifndef KVECC_ATTN_MFMA
-#define KVECC_ATTN_MFMA 1
-#endif
-// the last split of each (batch, head group) combines it (combine_if_last);
-// 0: a separate combine launch
-#ifndef KVECC_ATTN_FUSED_COMBINE
-#define KVECC_ATTN_FUSED_COMBINE 1
-#endif
-// 1: also for G > 1 query heads per workgroup where combine_group fits (one
-// round trip for all G heads): 32q/8kv H(8,4) 26.7 us against 22.3 with the
-// combine launch, Golay 30.2 / 29.4 (profiles/r03/attn/attn_gqa19.log)
-#ifndef KVECC_ATTN_FUSED_COMBINE_GQA
-#define KVECC_ATTN_FUSED_COMBINE_GQA 0
-#endif
-// 1: issue the next step's loads before this step's math (191 VGPRs at D = 128:
-// 2 waves per SIMD; 32q/8kv measured 29.8 us against 22.9 without)
-#ifndef KVECC_ATTN_MFMA_PREFETCH
-#define KVECC_ATTN_MFMA_PREFETCH 0
-#endif
-#ifndef KVECC_ATTN_MFMA_WG_PER_CU
-#define KVECC_ATTN_MFMA_WG_PER_CU 4
-#endif
+// Fused combine: the last split of each (batch, head group) combines it
+// (combine_if_last) -- for one query head per workgroup only (see
+// kvecc_paged_attention).  Issuing the next step's loads before this step's
+// math took the kernel to 191 VGPRs (2 waves per SIMD): 32q/8kv 29.8 us
+// against 22.9 without.  4 workgroups per CU for the H(8,4) kernel.
+constexpr int kMfmaWgPerCu = 4;
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kMfmaStep = 32;  // tokens per wave step
 
-// Decoded values as MFMA operands.  KVECC_ATTN_MFMA_SUBNORM (default): the
-// table's nibble n (0..15) goes into an f16 half as is -- the subnormal
-// n * 2^-24, exact -- so a pair costs one v_perm; the kernel scales the
-// products by 2^24 and folds the -8 out as -8 * sum(q) (scores) and
-// -8 * sum(p) (outputs).  0: f16 1024 + n by an OR of 0x6400, then one
-// v_pk_add_f16 of -1032 per pair: (n - 8) itself.
-#ifndef KVECC_ATTN_MFMA_SUBNORM
-#define KVECC_ATTN_MFMA_SUBNORM 1
-#endif
-constexpr float kMfmaValScale = KVECC_ATTN_MFMA_SUBNORM ? 16777216.0f : 1.0f;  // 2^24
-constexpr float kMfmaValOffset = KVECC_ATTN_MFMA_SUBNORM ? 8.0f : 0.0f;
+// Decoded values as MFMA operands: the table's nibble n (0..15) goes into an
+// f16 half as is -- the subnormal n * 2^-24, exact -- so a pair costs one
+// v_perm; the kernel scales the products by 2^24 and folds the -8 out as
+// -8 * sum(q) (scores) and -8 * sum(p) (outputs).  (f16 1024 + n by an OR of
+// 0x6400 and one v_pk_add_f16 of -1032 per pair measured within noise.)
+constexpr float kMfmaValScale = 16777216.0f;  // 2^24
+constexpr float kMfmaValOffset = 8.0f;
 // two table values (data nibbles 0..15) -> f16 operand pair, lo in bits 0..15
 __device__ __forceinline__ uint32_t nib_pair_f16(uint32_t lo, uint32_t hi) {
-  if (KVECC_ATTN_MFMA_SUBNORM) return __builtin_amdgcn_perm(hi, lo, 0x0c040c00u);  // [0, hi, 0, lo]
-  const f16x2 h = __builtin_bit_cast(f16x2, (lo | hi << 16) | 0x64006400u);  // 1024 + n
-  return __builtin_bit_cast(uint32_t, h + f16x2{(_Float16)-1032.0f, (_Float16)-1032.0f});
+  return __builtin_amdgcn_perm(hi, lo, 0x0c040c00u);  // [0, hi, 0, lo]
 }
 
 // NB contiguous bytes (2, 4, 8, 16 or 32) at byte offset off -> dwords w
@@ -915,14 +775,12 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
     qop[kk] = __builtin_bit_cast(f16x8, v);
   }
   float qsum = 0.0f;  // sum of head n's query over all d (the offset fold)
-  if (KVECC_ATTN_MFMA_SUBNORM) {
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk)
+  for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) qsum += (float)qop[kk][e];
-    qsum += __shfl_xor(qsum, 16, kWave);
-    qsum += __shfl_xor(qsum, 32, kWave);
-  }
+    for (int e = 0; e < 8; ++e) qsum += (float)qop[kk][e];
+  qsum += __shfl_xor(qsum, 16, kWave);
+  qsum += __shfl_xor(qsum, 32, kWave);
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t krs =
@@ -969,16 +827,9 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
     }
   };
   constexpr int kStride = kWaves * kMfmaStep;
-  Step nxt;
-  if (KVECC_ATTN_MFMA_PREFETCH && wave * kMfmaStep < ntok) load_step(wave * kMfmaStep, nxt);
   for (int i0 = wave * kMfmaStep; i0 < ntok; i0 += kStride) {
     Step cur;
-    if (KVECC_ATTN_MFMA_PREFETCH) {
-      cur = nxt;
-      if (i0 + kStride < ntok) load_step(i0 + kStride, nxt);  // next step's loads fly during this one
-    } else {
-      load_step(i0, cur);
-    }
+    load_step(i0, cur);
     const int32_t *rv = cur.rv;
     const float *ks = cur.ks, *vs = cur.vs;
     auto &kw = cur.kw;
@@ -1434,14 +1285,11 @@ static int attn_vec(int codec, int64_t d, bool gqa = false) {
 // query heads per workgroup: the GQA kernels cover buffer-addressed caches with
 // lane groups of 8-32 lanes per row (head_dim 64-256) and G in {2, 4} dividing
 // H / Hkv (G 8 would hold 8 query rows and accumulators per lane); else 1
-#ifndef KVECC_ATTN_GQA
-#define KVECC_ATTN_GQA 1
-#endif
 static int attn_heads_per_wg(int codec, int64_t d, int64_t g, int64_t heads, int64_t kv_heads, bool buf) {
   const int64_t group = heads / kv_heads;
   const int vec = attn_vec(codec, d, true);
   const int w = pow2_at_least((g + vec - 1) / vec);
-  if (!KVECC_ATTN_GQA || !buf || w < 8 || w > 32 || (codec == KVECC_CODEC_H84 && d % 8 != 0)) return 1;
+  if (!buf || w < 8 || w > 32 || (codec == KVECC_CODEC_H84 && d % 8 != 0)) return 1;
   const int gmax = codec == KVECC_CODEC_GOLAY_PACKED ? 2 : 4;  // packed: 4 codewords per lane
   return group % 4 == 0 && gmax >= 4 ? 4 : group % 2 == 0 ? 2 : 1;
 }
@@ -1527,21 +1375,16 @@ static int launch_mfma(int codec, const AttnArgs &a, int64_t batch, int gm, hipS
 // query heads per workgroup of the MFMA kernels (0: not applicable): caches under
 // 4 GiB, fp16 queries (16-byte aligned), a group of >= 2 query heads per cache
 // head; Hamming(8,4) at head_dim 32 / 64 / 128, Golay (int32 or packed) at head_dim 128
-#ifndef KVECC_ATTN_MFMA_GOLAY
-#define KVECC_ATTN_MFMA_GOLAY 1
-#endif
 // workgroups per CU of the Golay kernel's split choice (157 VGPRs, 49-73 KiB of
 // LDS): 2 measured 30.6 vs 34.2 us at 4 (32q/8kv; profiles/r03/attn/attn_gqa14.log)
-#ifndef KVECC_ATTN_MFMA_GOLAY_WG_PER_CU
-#define KVECC_ATTN_MFMA_GOLAY_WG_PER_CU 2
-#endif
+constexpr int kMfmaGolayWgPerCu = 2;
 static int attn_mfma_heads(int codec, int q_dtype, const void *query, int64_t d, int64_t heads,
                            int64_t kv_heads, bool buf) {
   const int64_t group = heads / kv_heads;
   const bool h84 = codec == KVECC_CODEC_H84 && (d == 32 || d == 64 || d == 128);
-  const bool golay = KVECC_ATTN_MFMA_GOLAY && (codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED) &&
+  const bool golay = (codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED) &&
                      d == 128;
-  if (!KVECC_ATTN_MFMA || !(h84 || golay) || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) || group < 2)
+  if (!(h84 || golay) || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) || group < 2)
     return 0;
   return group % 16 == 0 ? 16 : group % 8 == 0 ? 8 : group % 4 == 0 ? 4 : group % 2 == 0 ? 2 : 0;
 }
@@ -1556,12 +1399,9 @@ static int launch_codec(int codec, const AttnArgs &a, int64_t batch, int gq, hip
 }
 
 // tokens per workgroup: the largest power of two <= kMaxSplit that still gives
-// >= KVECC_ATTN_WG_PER_CU workgroups per CU (small batch*heads decode steps
-// split finer)
-#ifndef KVECC_ATTN_WG_PER_CU
-#define KVECC_ATTN_WG_PER_CU 4
-#endif
-static int64_t choose_split(int64_t bh, int64_t max_context_len, int per_cu = KVECC_ATTN_WG_PER_CU) {
+// >= per_cu workgroups per CU (small batch*heads decode steps split finer); 8
+// per CU made every codec 1-15 % slower
+static int64_t choose_split(int64_t bh, int64_t max_context_len, int per_cu = 4) {
   // longer splits amortise each workgroup's fixed work (table staging, the
   // group merge); measured best at 1024 for both codecs at [8,4096,32,128]
   const int64_t top = kMaxSplit;
@@ -1653,10 +1493,9 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     gq = attn_heads_per_wg(codec, head_dim, a.g, heads, kv_heads, fits);
     gm = attn_mfma_heads(codec, q_dtype, query, head_dim, heads, kv_heads, fits);
   }
-  if (gm)  // KVECC_ATTN_MFMA_WG_PER_CU workgroups per CU, never finer than the workspace allows
+  if (gm)  // kMfma*WgPerCu workgroups per CU, never finer than the workspace allows
     a.split = std::max(choose_split(batch * heads / gm, max_context_len,
-                                    codec != KVECC_CODEC_H84 ? KVECC_ATTN_MFMA_GOLAY_WG_PER_CU
-                                                               : KVECC_ATTN_MFMA_WG_PER_CU),
+                                    codec != KVECC_CODEC_H84 ? kMfmaGolayWgPerCu : kMfmaWgPerCu),
                        choose_split(std::max<int64_t>(1, batch * heads / 4), max_context_len));
   else
     a.split = choose_split(batch * heads / gq, max_context_len);
@@ -1673,13 +1512,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   // combined serially, 26.9 with one wave per head, 26.7 (against 22.3) with all
   // G heads in one round trip (combine_group; profiles/r03/attn/).
   const int gw = gm ? gm : gq;  // query heads per workgroup
-  const bool group_fits = gw == 2    ? combine_group_fits<2>(a.nsplit, head_dim)
-                          : gw == 4  ? combine_group_fits<4>(a.nsplit, head_dim)
-                          : gw == 8  ? combine_group_fits<8>(a.nsplit, head_dim)
-                          : gw == 16 ? combine_group_fits<16>(a.nsplit, head_dim)
-                                     : false;
-  if (KVECC_ATTN_FUSED_COMBINE && (gw == 1 || (KVECC_ATTN_FUSED_COMBINE_GQA && group_fits)) &&
-      batch * heads <= kAttnCtrPerSlot) {
+  if (gw == 1 && batch * heads <= kAttnCtrPerSlot) {
     a.ctr = attn_counter_slot(stream);
     if (!a.ctr) return KVECC_EHIP;
   }

@@ -30,27 +30,12 @@
 
 namespace kvecc {
 
-// geometry (A/B knobs: tools/exp/run_golay_geom.py)
-#ifndef KVECC_GOLAY_GROUPS
-#define KVECC_GOLAY_GROUPS 2
-#endif
-#ifndef KVECC_GOLAY_DEC_BLOCK
-#define KVECC_GOLAY_DEC_BLOCK 512
-#endif
-#ifndef KVECC_GOLAY_ENC_BLOCK
-#define KVECC_GOLAY_ENC_BLOCK 1024
-#endif
-#ifndef KVECC_GOLAY_DEC_PER_CU
-#define KVECC_GOLAY_DEC_PER_CU 32
-#endif
-#ifndef KVECC_GOLAY_ENC_PER_CU
-#define KVECC_GOLAY_ENC_PER_CU 16
-#endif
-#ifndef KVECC_GOLAY_ROWS_PER_CU  // register-tile row kernels (512 threads, ~50 KB LDS)
-#define KVECC_GOLAY_ROWS_PER_CU 2
-#endif
-constexpr int kGroups = KVECC_GOLAY_GROUPS;         // 4-codeword groups per lane per tile
-constexpr int kDecBlock = KVECC_GOLAY_DEC_BLOCK, kEncBlock = KVECC_GOLAY_ENC_BLOCK;  // threads per workgroup
+// geometry (tuned by interleaved cold-cache A/B: tools/exp/run_golay_geom.py,
+// profiles/r01/golay/geometry_ab.log; DESIGN.md §3 Golay decode)
+constexpr int kGroups = 2;                          // 4-codeword groups per lane per tile
+constexpr int kDecBlock = 512, kEncBlock = 1024;    // threads per workgroup
+constexpr int kDecPerCu = 32, kEncPerCu = 16;       // workgroups per CU (grid-strided)
+constexpr int kRowsPerCu = 2;                       // register-tile row kernels (512 threads, ~50 KB LDS)
 constexpr int kDecTile = kDecBlock * kGroups * 4;   // 4096 codewords
 constexpr int kEncTile = kEncBlock * kGroups * 4;   // 8192 codewords
 constexpr int kWaveCw = kWave * kGroups * 4;        // codewords per wave per tile
@@ -484,9 +469,6 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
 // current tile's stores.  Per-lane offsets are 32-bit inside a tile, tile
 // bases 64-bit and wave-uniform (descriptors in SGPRs).
 // dynamic tail schedule (kvecc_internal.h TileSchedule), as the fused reads
-#ifndef KVECC_GOLAY_ROWS_DYN
-#define KVECC_GOLAY_ROWS_DYN 1
-#endif
 constexpr int kRegBlock = 512;
 constexpr int kRegWaves = kRegBlock / kWave;
 constexpr int kRegGroups = 4;        // 4-codeword groups per lane per tile (max)
@@ -502,7 +484,7 @@ struct RegRowsArgs {
   uint32_t d, g, gpr, lr, tr;
   const void *tab;  // decode: spread tables (uint32[8192]); encode: parity (uint16[4096])
   uint64_t *stats;
-  uint32_t *dyn;    // work-counter slot (KVECC_GOLAY_ROWS_DYN; ntiles < 2^32)
+  uint32_t *dyn;    // work-counter slot of the dynamic tail (ntiles < 2^32)
 };
 
 struct RegItems {
@@ -547,9 +529,8 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
   int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
   if (t >= a.ntiles) return;  // no workgroup barrier below
   const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
-  constexpr bool kDyn = KVECC_GOLAY_ROWS_DYN;
-  TileSchedule<kDyn> sched;
-  if (kDyn) sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
+  TileSchedule sched;
+  sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
   u32x4 w[kRegGroups];
   auto issue = [&](int64_t tt) {
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
@@ -588,7 +569,7 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
     }
     wave_lds_sync();
     const int64_t cur = t;
-    t = kDyn ? (int64_t)sched.next((uint32_t)t, lane) : t + tstride;
+    t = (int64_t)sched.next((uint32_t)t, lane);
     const bool more = t < a.ntiles;
     if (more) issue(t);
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
@@ -635,9 +616,8 @@ __global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRow
   int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
   if (t >= a.ntiles) return;
   const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
-  constexpr bool kDyn = KVECC_GOLAY_ROWS_DYN;
-  TileSchedule<kDyn> sched;
-  if (kDyn) sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
+  TileSchedule sched;
+  sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
   u32x4 v[kRegChunks];
   auto issue = [&](int64_t tt) {
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
@@ -658,7 +638,7 @@ __global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRow
     }
     wave_lds_sync();
     const int64_t cur = t;
-    t = kDyn ? (int64_t)sched.next((uint32_t)t, lane) : t + tstride;
+    t = (int64_t)sched.next((uint32_t)t, lane);
     const bool more = t < a.ntiles;
     if (more) issue(t);
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
@@ -727,7 +707,7 @@ KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, in
   if (aligned(triplets, 4) && aligned(codewords, 16)) {
     int64_t ntiles = m / kEncTile;
     if (ntiles > 0) {
-      unsigned g = grid_for(ntiles, 1, KVECC_GOLAY_ENC_PER_CU);  // grid-strided
+      unsigned g = grid_for(ntiles, 1, kEncPerCu);  // grid-strided
       KVECC_LAUNCH(golay_encode_kernel, dim3(g), dim3(kEncBlock), 0, st,
                          reinterpret_cast<const uint32_t *>(triplets),
                          reinterpret_cast<u32x4 *>(codewords), ntiles, par);
@@ -755,7 +735,7 @@ KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, ui
   if (aligned(codewords, 16) && aligned(triplets, 4) && (!counts || aligned(counts, 4))) {
     int64_t ntiles = m / kDecTile;
     if (ntiles > 0) {
-      unsigned g = grid_for(ntiles, 1, KVECC_GOLAY_DEC_PER_CU);  // grid-strided
+      unsigned g = grid_for(ntiles, 1, kDecPerCu);  // grid-strided
       auto c = reinterpret_cast<const u32x4 *>(codewords);
       auto t = reinterpret_cast<uint32_t *>(triplets);
       auto n = reinterpret_cast<uint32_t *>(counts);
@@ -789,11 +769,11 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
   int64_t g = (d + 2) / 3;
   const RegGeom rg = reg_geom(d, g, true);
   if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 16) &&
-      (!KVECC_GOLAY_ROWS_DYN || cdiv(rows, rg.tr) < (1LL << 31))) {
+      cdiv(rows, rg.tr) < (1LL << 31)) {
     RegRowsArgs a{nibbles, codewords, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
                   par, nullptr};
-    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
+    if (!(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * kRowsPerCu);
     KVECC_LAUNCH(golay_encode_rows_reg_kernel, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
     return check_launch("golay_encode_rows");
   }
@@ -823,13 +803,13 @@ KVECC_API int kvecc_golay_decode_rows(const int32_t *codewords, uint8_t *nibbles
   int64_t g = (d + 2) / 3;
   const RegGeom rg = reg_geom(d, g, false);
   if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 4) &&
-      (!KVECC_GOLAY_ROWS_DYN || cdiv(rows, rg.tr) < (1LL << 31))) {
+      cdiv(rows, rg.tr) < (1LL << 31)) {
     const uint32_t *atab = golay_attn_table_dev();
     if (!atab) return KVECC_EHIP;
     RegRowsArgs a{codewords, nibbles, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
                   atab, stats};
-    if (KVECC_GOLAY_ROWS_DYN && !(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * KVECC_GOLAY_ROWS_PER_CU);
+    if (!(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
+    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * kRowsPerCu);
     if (stats)
       KVECC_LAUNCH(golay_decode_rows_reg_kernel<true>, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
     else

@@ -119,80 +119,11 @@ __global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restr
   }
 }
 
-// strip path (inner % 16 == 0): work item = (o, strip of kStrip rows, column
-// chunk).  A lane walks its strip in kRows-row blocks and carries the last two
-// q rows of a block into the next, so a q row is fetched once per strip plus
-// a one-row halo at each strip end (2 / kStrip extra instead of 2 / kRows).
-#ifndef KVECC_INTERP_STRIP
-#define KVECC_INTERP_STRIP 0  // rows per strip; 0 = the row-block kernel above
-#endif
-constexpr int kStrip = KVECC_INTERP_STRIP;
-
-template <bool RECORD>
-__global__ __launch_bounds__(kBlock) void interp_strip_kernel(const u32x4 *__restrict__ q,
-                                                              const u32x4 *__restrict__ err,
-                                                              u32x4 *__restrict__ out, int64_t len,
-                                                              uint32_t chunks, uint32_t strips,
-                                                              uint32_t items,
-                                                              const int32_t *__restrict__ gate,
-                                                              int32_t *__restrict__ flags,
-                                                              int32_t epoch) {
-  const bool pass = !RECORD && gate != nullptr && *gate == 0;
-  uint32_t dbl = 0, over = 0;
-  for (uint32_t it = blockIdx.x * kBlock + threadIdx.x; it < items; it += gridDim.x * kBlock) {
-    const uint32_t c = it % chunks, t = it / chunks;
-    const uint32_t sidx = t % strips, o = t / strips;
-    const int64_t l0 = (int64_t)sidx * kStrip;
-    const int64_t l1 = min<int64_t>(l0 + kStrip, len);
-    const u32x4 *qb = q + (int64_t)o * len * chunks + c;  // (o, l = 0, c)
-    const u32x4 *eb = err + (int64_t)o * len * chunks + c;
-    u32x4 *ob = out + (int64_t)o * len * chunks + c;
-    if (pass) {
-      for (int64_t l = l0; l < l1; ++l) st_stream(ob + l * chunks, ld_stream(qb + l * chunks));
-      continue;
-    }
-    u32x4 prev = ld_stream(qb + (l0 > 0 ? l0 - 1 : 0) * chunks);
-    u32x4 cur = ld_stream(qb + l0 * chunks);
-    int64_t l = l0;
-    for (; l + kRows <= l1; l += kRows) {
-      u32x4 qr[kRows + 2], er[kRows];
-      qr[0] = prev;
-      qr[1] = cur;
-#pragma unroll
-      for (int k = 1; k <= kRows; ++k) qr[k + 1] = ld_stream(qb + (l + k < len ? l + k : len - 1) * chunks);
-#pragma unroll
-      for (int k = 0; k < kRows; ++k) er[k] = ld_stream(eb + (l + k) * chunks);
-#pragma unroll
-      for (int k = 0; k < kRows; ++k) {
-        st_stream(ob + (l + k) * chunks, interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
-        if (RECORD) {
-          dbl |= seen_double(er[k]);
-          over |= seen_over15(qr[k + 1]);
-        }
-      }
-      prev = qr[kRows];
-      cur = qr[kRows + 1];
-    }
-    for (; l < l1; ++l) {  // ragged end of the strip
-      const u32x4 next = ld_stream(qb + (l + 1 < len ? l + 1 : len - 1) * chunks);
-      const u32x4 e = ld_stream(eb + l * chunks);
-      st_stream(ob + l * chunks, interp_vec(cur, prev, next, e));
-      if (RECORD) {
-        dbl |= seen_double(e);
-        over |= seen_over15(cur);
-      }
-      prev = cur;
-      cur = next;
-    }
-  }
-  if (RECORD) {
-    const bool d = __syncthreads_or(dbl != 0), o = __syncthreads_or(over != 0);
-    if (threadIdx.x == 0) {
-      if (d) flags[0] = epoch;
-      if (o) flags[1] = epoch;
-    }
-  }
-}
+// (Strips -- a lane walking 16-128 rows of its column chunk and carrying the
+// last two q rows from block to block, so the halo costs 2/strip instead of
+// 2/8 -- took 80.4-83.4 us against 76.8 for the row blocks above: the longer
+// dependent chain per lane costs more than the 12.5 % of re-fetched bytes, most
+// of which hit L2; profiles/r02/interp_strips.log.)
 
 // scalar path: one element per lane
 template <bool RECORD>
@@ -332,15 +263,7 @@ template <bool RECORD>
 static void launch_interp(const uint8_t *q, const uint8_t *err, uint8_t *out, int64_t outer,
                           int64_t len, int64_t inner, const int32_t *gate, int32_t *flags,
                           int32_t epoch, hipStream_t st) {
-  if (kStrip > 0 && inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16) &&
-      outer * cdiv(len, kStrip) * (inner / 16) <= 0xFFFFFFFFLL) {
-    const int64_t chunks = inner / 16, strips = cdiv(len, kStrip);
-    const int64_t items = outer * strips * chunks;
-    KVECC_LAUNCH((interp_strip_kernel<RECORD>), dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0, st,
-                 reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
-                 reinterpret_cast<u32x4 *>(out), len, (uint32_t)chunks, (uint32_t)strips, (uint32_t)items,
-                 gate, flags, epoch);
-  } else if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
+  if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
     const int64_t chunks = inner / 16;
     const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
     KVECC_LAUNCH((interp_vec_kernel<RECORD>), dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0,

@@ -288,26 +288,20 @@ __device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32
   }
 }
 
-#ifndef KVECC_SHIM_DYN_PROBE
-#define KVECC_SHIM_DYN_PROBE 0
-#endif
-#ifndef KVECC_SHIM_TILE_DYN_STATIC_PCT
-#define KVECC_SHIM_TILE_DYN_STATIC_PCT 75
-#endif
-// The dynamic tile schedule of one wave (shim.hip KVECC_SHIM_TILE_DYN, golay.hip
-// KVECC_GOLAY_ROWS_DYN): its first tile
-// is gw, next() gives the following ones (>= units: none left).  Counter c
-// serves the W_c waves gw = c (mod kDynCounters) with its K_c tiles; every
-// such wave stops after its first failed grab, so the failed grabs return
-// K_c .. K_c + W_c - 1, and the wave that draws the last of them is the last
-// to touch the counter: it resets it to 0 for the next launch.  (A "done"
-// counter shared by all waves instead serialised their exits: ~40 us.)
-template <bool DYN>
+// The dynamic tile schedule of one wave (the fused reads in shim.hip, the
+// per-head rows in golay.hip, the packed Golay decode): its first tile is gw,
+// next() gives the following ones (>= units: none left).  A wave takes the first
+// `pct` % of its even share statically (gw, gw + nwaves, ...), then tiles
+// from the launch's work counters: counter c serves the W_c waves gw = c (mod
+// kDynCounters) with its K_c tiles (base + k kDynCounters + c); every such wave
+// stops after its first failed grab, so the failed grabs return K_c .. K_c +
+// W_c - 1, and the wave that draws the last of them is the last to touch the
+// counter: it resets it to 0 for the next launch on this counter slot (a "done"
+// counter shared by all waves instead serialised their exits: ~40 us).
+constexpr uint32_t kTileStaticPct = 75;  // the rows and packed kernels' static share
 struct TileSchedule {
   uint32_t gw, nwaves, units, cidx, sidx, gk, last_k, nstatic;
   uint32_t *ctr;
-  // a bijection of [0, nwaves) for power-of-two nwaves (probe 3 only)
-  __device__ __forceinline__ uint32_t perm(uint32_t w) const { return (w * 2654435761u) & (nwaves - 1); }
   __device__ __forceinline__ uint32_t grab(uint32_t lane) {
     // the offset is an opaque (per-lane) zero: with a provably uniform address
     // the atomic optimizer rewrites the add into a broadcast of its result
@@ -320,36 +314,24 @@ struct TileSchedule {
     return k;  // lane 0's; next() broadcasts it when the tile is needed
   }
   __device__ __forceinline__ void init(uint32_t units_, uint32_t *dyn, uint32_t gw_, uint32_t nwaves_,
-                                       uint32_t lane, uint32_t pct = KVECC_SHIM_TILE_DYN_STATIC_PCT) {
+                                       uint32_t lane, uint32_t pct = kTileStaticPct) {
     gw = gw_;
     nwaves = nwaves_;
     units = units_;
     sidx = 1;
-    // static tiles per wave: DYN_STATIC_PCT % of the even share, at least 1
+    // static tiles per wave: pct % of the even share, at least 1
     nstatic = max(1u, (uint32_t)(pct * ((units + nwaves - 1) / nwaves) / 100));
-    if (DYN || KVECC_SHIM_DYN_PROBE) {
-      cidx = gw % kDynCounters;
-      ctr = dyn + kDynStride * cidx;
-      const uint32_t base = nstatic * nwaves;
-      const uint32_t kc = units > base + cidx ? (units - base - cidx + kDynCounters - 1) / kDynCounters : 0u;
-      const uint32_t active = min(nwaves, units);  // waves with a first tile (gw < active)
-      const uint32_t wc = (active - cidx + kDynCounters - 1) / kDynCounters;  // >= 1: this wave
-      last_k = kc + wc - 1;
-      gk = grab(lane);
-    }
+    cidx = gw % kDynCounters;
+    ctr = dyn + kDynStride * cidx;
+    const uint32_t base = nstatic * nwaves;
+    const uint32_t kc = units > base + cidx ? (units - base - cidx + kDynCounters - 1) / kDynCounters : 0u;
+    const uint32_t active = min(nwaves, units);  // waves with a first tile (gw < active)
+    const uint32_t wc = (active - cidx + kDynCounters - 1) / kDynCounters;  // >= 1: this wave
+    last_k = kc + wc - 1;
+    gk = grab(lane);
   }
   __device__ __forceinline__ uint32_t next(uint32_t cur, uint32_t lane) {
-#if KVECC_SHIM_DYN_PROBE == 1  // experiment: static schedule plus one atomic per tile on the counters
-    gk += grab(lane);
-    return cur + nwaves;
-#endif
-    if (!DYN) return cur + nwaves;
-#if KVECC_SHIM_DYN_PROBE == 3  // experiment: the static order with waves scrambled over tiles in each round
-    {
-      const uint32_t r = (cur - perm(gw)) / nwaves + 1;
-      return r * nwaves + perm(gw);
-    }
-#endif
+    (void)cur;
     const uint32_t S = nstatic;
     if (sidx < S) {
       const uint32_t t = gw + sidx * nwaves;

@@ -176,15 +176,10 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_kernel(
 // already in registers, and reads its 24-byte groups back as 8-byte LDS reads
 // (lane stride 6 dwords: conflict-free).  43.6 vs 44.9 us for the direct
 // 8-byte-load kernel above (tools/exp/run_packed.py); taken for 16-B aligned
-// codewords (KVECC_PACKED_DEC_STAGED=0 restores the direct kernel).
-#ifndef KVECC_PACKED_DEC_STAGED
-#define KVECC_PACKED_DEC_STAGED 1
-#endif
+// codewords past the wave-tile kernel's 2 GiB range.
 // workgroups per CU of the decode grid (a cap: smaller grids loop over tiles,
 // staging the 16 KiB of tables once per workgroup instead of once per tile)
-#ifndef KVECC_PACKED_DEC_PER_CU
-#define KVECC_PACKED_DEC_PER_CU 32
-#endif
+constexpr int kPkDecPerCu = 32;
 constexpr int kPkWaveBytes = kPkWaveCw * 3;  // 3072
 template <bool WITH_FLAGS, bool WITH_STATS>
 __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
@@ -255,35 +250,18 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
 // (error data | bits << 24 | uncorrectable << 31), data = (c ^ e) & 0xFFF in one
 // v_bitop3, the statistics as a 32-bit sum of entries (bits 24-30: corrected
 // bits of <= 8 codewords) and the flag bits shifted in with v_alignbit.
-#ifndef KVECC_PACKED_DEC_V2
-#define KVECC_PACKED_DEC_V2 1
-#endif
-#ifndef KVECC_PACKED_DEC_V2_PER_CU
-#define KVECC_PACKED_DEC_V2_PER_CU 2
-#endif
-#ifndef KVECC_PACKED_DEC_DYN
-#define KVECC_PACKED_DEC_DYN 1
-#endif
+constexpr int kPk2PerCu = 2;  // workgroups per CU of the persistent grid
 constexpr int kPk2Block = 512;
 constexpr int kPk2Waves = kPk2Block / kWave;
 // groups of 8 codewords per lane per wave tile (2: 1024 codewords, 3 KiB);
 // 4 and 6 measured 41.0 and 52.4 us against 39.2 (profiles/r03/packed/pk_ab7.log)
-#ifndef KVECC_PACKED_DEC_GROUPS
-#define KVECC_PACKED_DEC_GROUPS 2
-#endif
-constexpr int kPk2Groups = KVECC_PACKED_DEC_GROUPS;
+constexpr int kPk2Groups = 2;
 constexpr int kPk2TileCw = kWave * 8 * kPk2Groups;  // codewords per wave tile
 constexpr int kPk2TileBytes = kPk2TileCw * 3;       // 3 KiB per 2 groups
 constexpr int kPk2Vec = kPk2TileBytes / 16 / kWave;  // 16-byte loads per lane
-// uncorrectable flags (one byte per group of 8 codewords): staged in LDS and
-// stored as 16-byte stores by the first kPk2Groups * 4 lanes, instead of one
-// byte store per lane per group (needs a 16-byte aligned flag buffer).
-// Measured no faster (38.4 vs 38.1 us at the bench's M, BER 1e-2;
-// profiles/r03/packed/pk_flags16_ab.log): the byte stores are not the limit.
-#ifndef KVECC_PACKED_DEC_FLAGS16
-#define KVECC_PACKED_DEC_FLAGS16 0
-#endif
-
+// The uncorrectable flags (one byte per group of 8 codewords, one byte store
+// per lane per group) staged in LDS and stored 16 bytes per lane instead
+// measured no faster (38.4 vs 38.1 us, profiles/r03/packed/pk_flags16_ab.log).
 struct PkDecArgs {
   const uint8_t *cw;
   uint32_t *nib;
@@ -292,14 +270,12 @@ struct PkDecArgs {
   const uint8_t *tab;  // golay_pk_table_dev()
   uint64_t *stats;
   uint32_t *dyn;
-  uint32_t flags16;  // flags staged and stored 16 bytes per lane
 };
 
 template <bool WITH_FLAGS, bool WITH_STATS>
 __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkDecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tab[24576];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kPk2Waves][kPk2TileBytes];
-  __shared__ __attribute__((aligned(16))) uint8_t flag_all[kPk2Waves][kPk2Groups * kWave];
   for (int i = threadIdx.x; i < 24576 / 16; i += kPk2Block)
     reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
   __syncthreads();
@@ -307,9 +283,8 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
   const uint32_t gw = blockIdx.x * kPk2Waves + wave, nwaves = gridDim.x * kPk2Waves;
   if (gw >= a.units) return;  // no workgroup barrier below
   uint8_t *stage = stage_all[wave];
-  constexpr bool kDyn = KVECC_PACKED_DEC_DYN;
-  TileSchedule<kDyn> sched;
-  if (kDyn) sched.init(a.units, a.dyn, gw, nwaves, lane);
+  TileSchedule sched;
+  sched.init(a.units, a.dyn, gw, nwaves, lane);
   // whole codeword buffer (< 2 GiB, checked on the host); nt loads
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t *>(a.cw), 0, (int)(a.units * (uint32_t)kPk2TileBytes), 0x00020000);
@@ -328,7 +303,7 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
     for (int k = 0; k < kPk2Vec; ++k) reinterpret_cast<u32x4 *>(stage)[lane + kWave * k] = nxt[k];
     wave_lds_sync();
     const uint32_t cur = t;
-    t = kDyn ? sched.next(t, lane) : t + nwaves;
+    t = sched.next(t, lane);
     const bool more = t < a.units;
     if (more) issue(t);
 #pragma unroll
@@ -362,19 +337,7 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
       nib_pack8(d, n);
       const uint32_t grp = cur * (kPk2TileCw / 8) + g * kWave + lane;  // group of 8 codewords
       st_stream(reinterpret_cast<u32x3v *>(a.nib + (size_t)grp * 3), u32x3v{n[0], n[1], n[2]});
-      if (WITH_FLAGS) {
-        if (a.flags16)
-          flag_all[wave][g * kWave + lane] = (uint8_t)fl;
-        else
-          st_stream(a.flags + grp, (uint8_t)fl);
-      }
-    }
-    if (WITH_FLAGS && a.flags16) {  // the tile's kPk2Groups * 64 flag bytes
-      wave_lds_sync();
-      constexpr uint32_t kFl = kPk2Groups * kWave / 16;
-      if (lane < kFl)
-        st_stream(reinterpret_cast<u32x4 *>(a.flags + (size_t)cur * (kPk2Groups * kWave)) + lane,
-                  reinterpret_cast<const u32x4 *>(flag_all[wave])[lane]);
+      if (WITH_FLAGS) st_stream(a.flags + grp, (uint8_t)fl);
     }
     if (!more) break;
     wave_lds_sync();
@@ -479,19 +442,12 @@ __global__ __launch_bounds__(kHpBlock) void h84_encode_packed_kernel(const u32x2
 // 16 values per lane.  The packing works on pairs of words with v_perm, and the
 // statistics come from the packed ErrorType word (2 bits per value: 1 =
 // corrected single, 2 = double) instead of per-word popcounts: ~25 % fewer VALU
-// ops than packing and counting word by word (KVECC_H84_PACKED_PERM=0), which
-// the counters showed this kernel spending most of its time on.
-#ifndef KVECC_H84_PACKED_PERM
-#define KVECC_H84_PACKED_PERM 1
-#endif
-// chunks per lane per grid-stride step (2: both loads issued first), and the
-// grid's workgroups per CU
-#ifndef KVECC_H84_PACKED_UNROLL
-#define KVECC_H84_PACKED_UNROLL 1
-#endif
-#ifndef KVECC_H84_PACKED_GRID_PER_CU
-#define KVECC_H84_PACKED_GRID_PER_CU 32
-#endif
+// ops than packing and counting word by word, which the counters showed this
+// kernel spending most of its time on.  Grid-stride, 32 workgroups per CU: 16 /
+// 64 / 128 per CU, two chunks' loads in flight per lane, and persistent 4-chunk
+// wave tiles with the dynamic tail all measured slower (43.4-52.7 and 48.2 us
+// against 41.9; profiles/r03/packed/h84_packed_grid_unroll_ab.log).
+constexpr int kHpGridPerCu = 32;
 template <bool WITH_TYPES, bool WITH_STATS>
 __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4 *__restrict__ cw,
                                                                      u32x2 *__restrict__ nib,
@@ -501,139 +457,38 @@ __global__ __launch_bounds__(kHpBlock) void h84_decode_packed_kernel(const u32x4
   uint32_t n1 = 0, n2 = 0;
   auto chunk = [&](const u32x4 c, int64_t i) {
     const uint32_t w[4] = {c.x, c.y, c.z, c.w};
-    if (KVECC_H84_PACKED_PERM) {
-      uint32_t y[4], z[4];
+    uint32_t y[4], z[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const HammingTables tb(w[k]);
-        const uint32_t d = (w[k] ^ (tb.fx & tb.pe_rep)) & 0x0F0F0F0Fu;  // correct only SINGLE (pe && nz)
-        const uint32_t pe = tb.pe(), nz = tb.nz();
-        const uint32_t t = pe | (pe ^ nz) << 1;  // per byte, hamming84_triton.py:185-187
-        y[k] = d | d >> 4;  // bytes 0 and 2: (v0 | v1 << 4), (v2 | v3 << 4)
-        z[k] = t | t >> 6;  // bytes 0 and 2: (t0 | t1 << 2), (t2 | t3 << 2)
-      }
-      // bytes 0 and 2 of each word, two words per v_perm
-      const uint32_t n01 = __builtin_amdgcn_perm(y[1], y[0], 0x06040200u);
-      const uint32_t n23 = __builtin_amdgcn_perm(y[3], y[2], 0x06040200u);
-      st_stream(nib + i, u32x2{n01, n23});
-      if (WITH_TYPES || WITH_STATS) {
-        uint32_t r01 = __builtin_amdgcn_perm(z[1], z[0], 0x06040200u);  // 4-bit fields, one per byte
-        uint32_t r23 = __builtin_amdgcn_perm(z[3], z[2], 0x06040200u);
-        r01 |= r01 >> 4;
-        r23 |= r23 >> 4;
-        const uint32_t tw = __builtin_amdgcn_perm(r23, r01, 0x06040200u);  // 16 x 2 bits, value j at 2j
-        if (WITH_TYPES) st_stream(types + i, tw);
-        if (WITH_STATS) {
-          const uint32_t hi = tw >> 1;
-          n1 += __builtin_popcount(tw & ~hi & 0x55555555u);  // type 1: single, corrected
-          n2 += __builtin_popcount(hi & ~tw & 0x55555555u);  // type 2: double, detected
-        }
-      }
-      return;
+    for (int k = 0; k < 4; ++k) {
+      const HammingTables tb(w[k]);
+      const uint32_t d = (w[k] ^ (tb.fx & tb.pe_rep)) & 0x0F0F0F0Fu;  // correct only SINGLE (pe && nz)
+      const uint32_t pe = tb.pe(), nz = tb.nz();
+      const uint32_t t = pe | (pe ^ nz) << 1;  // per byte, hamming84_triton.py:185-187
+      y[k] = d | d >> 4;  // bytes 0 and 2: (v0 | v1 << 4), (v2 | v3 << 4)
+      z[k] = t | t >> 6;  // bytes 0 and 2: (t0 | t1 << 2), (t2 | t3 << 2)
     }
-    uint32_t d[4], t[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) h84_decode4(w[k], d[k], t[k], n1, n2);
-    st_stream(nib + i, u32x2{nib_pack4(d[0]) | nib_pack4(d[1]) << 16,
-                             nib_pack4(d[2]) | nib_pack4(d[3]) << 16});
-    if (WITH_TYPES)
-      st_stream(types + i, type_pack4(t[0]) | type_pack4(t[1]) << 8 | type_pack4(t[2]) << 16 |
-                               type_pack4(t[3]) << 24);
+    // bytes 0 and 2 of each word, two words per v_perm
+    const uint32_t n01 = __builtin_amdgcn_perm(y[1], y[0], 0x06040200u);
+    const uint32_t n23 = __builtin_amdgcn_perm(y[3], y[2], 0x06040200u);
+    st_stream(nib + i, u32x2{n01, n23});
+    if (WITH_TYPES || WITH_STATS) {
+      uint32_t r01 = __builtin_amdgcn_perm(z[1], z[0], 0x06040200u);  // 4-bit fields, one per byte
+      uint32_t r23 = __builtin_amdgcn_perm(z[3], z[2], 0x06040200u);
+      r01 |= r01 >> 4;
+      r23 |= r23 >> 4;
+      const uint32_t tw = __builtin_amdgcn_perm(r23, r01, 0x06040200u);  // 16 x 2 bits, value j at 2j
+      if (WITH_TYPES) st_stream(types + i, tw);
+      if (WITH_STATS) {
+        const uint32_t hi = tw >> 1;
+        n1 += __builtin_popcount(tw & ~hi & 0x55555555u);  // type 1: single, corrected
+        n2 += __builtin_popcount(hi & ~tw & 0x55555555u);  // type 2: double, detected
+      }
+    }
   };
   const int64_t stride = (int64_t)gridDim.x * kHpBlock;
   int64_t i = (int64_t)blockIdx.x * kHpBlock + threadIdx.x;
-  if constexpr (KVECC_H84_PACKED_UNROLL > 1) {  // two chunks' loads in flight per lane
-    for (; i + stride < n16; i += 2 * stride) {
-      const u32x4 c0 = ld_stream(cw + i), c1 = ld_stream(cw + i + stride);
-      chunk(c0, i);
-      chunk(c1, i + stride);
-    }
-  }
   for (; i < n16; i += stride) chunk(ld_stream(cw + i), i);
   if (WITH_STATS) flush_stats2<kHpBlock>(stats, n1, n2);
-}
-
-// Wave-tile decode (the default): a wave owns tiles of 64 lanes x kHp2Chunks
-// 16-value chunks (chunk k of a tile at lane + 64 k, so every wave-instruction
-// moves one contiguous 1 KiB / 512 B / 256 B span), all of a tile's loads
-// issued together and the next tile's before this one's stores, over a
-// persistent grid with the fused reads' dynamic tail (TileSchedule).
-#ifndef KVECC_H84_PACKED_V2
-#define KVECC_H84_PACKED_V2 0
-#endif
-#ifndef KVECC_H84_PACKED_CHUNKS
-#define KVECC_H84_PACKED_CHUNKS 4
-#endif
-#ifndef KVECC_H84_PACKED_PER_CU
-#define KVECC_H84_PACKED_PER_CU 8
-#endif
-constexpr int kHp2Chunks = KVECC_H84_PACKED_CHUNKS;
-constexpr int kHp2Block = 256;
-constexpr int kHp2Waves = kHp2Block / kWave;
-constexpr uint32_t kHp2TileChunks = kWave * kHp2Chunks;  // 16-value chunks per wave tile
-
-struct HpDecArgs {
-  const uint8_t *cw;
-  u32x2 *nib;
-  uint32_t *types;
-  uint32_t units;  // wave tiles
-  uint64_t *stats;
-  uint32_t *dyn;
-};
-
-template <bool WITH_TYPES, bool WITH_STATS>
-__global__ __launch_bounds__(kHp2Block) void h84_decode_packed_wave_kernel(HpDecArgs a) {
-  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
-  const uint32_t gw = blockIdx.x * kHp2Waves + wave, nwaves = gridDim.x * kHp2Waves;
-  if (gw >= a.units) return;
-  constexpr bool kDyn = KVECC_PACKED_DEC_DYN;
-  TileSchedule<kDyn> sched;
-  if (kDyn) sched.init(a.units, a.dyn, gw, nwaves, lane);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t *>(a.cw), 0, (int)(a.units * kHp2TileChunks * 16u), 0x00020000);
-  uint32_t t = gw;
-  u32x4 c[kHp2Chunks];
-  auto issue = [&](uint32_t tt) {
-#pragma unroll
-    for (int k = 0; k < kHp2Chunks; ++k)
-      c[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           rs, 16u * (tt * kHp2TileChunks + lane + kWave * k), 0, 2));
-  };
-  issue(t);
-  uint32_t n1 = 0, n2 = 0;
-  for (;;) {
-    u32x2 nb[kHp2Chunks];
-    uint32_t tb[kHp2Chunks];
-#pragma unroll
-    for (int k = 0; k < kHp2Chunks; ++k) {
-      const uint32_t w[4] = {c[k].x, c[k].y, c[k].z, c[k].w};
-      uint32_t d[4], ty[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) h84_decode4(w[j], d[j], ty[j], n1, n2);
-      nb[k] = u32x2{nib_pack4(d[0]) | nib_pack4(d[1]) << 16, nib_pack4(d[2]) | nib_pack4(d[3]) << 16};
-      tb[k] = type_pack4(ty[0]) | type_pack4(ty[1]) << 8 | type_pack4(ty[2]) << 16 | type_pack4(ty[3]) << 24;
-    }
-    const uint32_t cur = t;
-    t = kDyn ? sched.next(t, lane) : t + nwaves;
-    const bool more = t < a.units;
-    if (more) issue(t);
-#pragma unroll
-    for (int k = 0; k < kHp2Chunks; ++k) {
-      const size_t i = (size_t)cur * kHp2TileChunks + lane + kWave * k;
-      st_stream(a.nib + i, nb[k]);
-      if (WITH_TYPES) st_stream(a.types + i, tb[k]);
-    }
-    if (!more) break;
-  }
-  if (WITH_STATS) {
-    n1 = wave_sum(n1);
-    n2 = wave_sum(n2);
-    if (lane == 0) {
-      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
-      if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
-      if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
-    }
-  }
 }
 
 // tails and unaligned buffers, byte accesses: encode one thread per value,
@@ -706,15 +561,14 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
   const int64_t wave_tiles = m / kPk2TileCw;
-  if (KVECC_PACKED_DEC_V2 && aligned(nibbles, 4) && aligned(codewords, 16) && wave_tiles > 0 &&
+  if (aligned(nibbles, 4) && aligned(codewords, 16) && wave_tiles > 0 &&
       wave_tiles * kPk2TileBytes < ((int64_t)1 << 31)) {
     const uint8_t *tab = golay_pk_table_dev();
-    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot(stream) : nullptr;
-    if (!tab || (KVECC_PACKED_DEC_DYN && !dyn)) return KVECC_EHIP;
+    uint32_t *dyn = shim_dyn_slot(stream);
+    if (!tab || !dyn) return KVECC_EHIP;
     const PkDecArgs a{codewords, reinterpret_cast<uint32_t *>(nibbles), uncorrectable, (uint32_t)wave_tiles,
-                      tab, stats, dyn,
-                      (uint32_t)(KVECC_PACKED_DEC_FLAGS16 && uncorrectable && aligned(uncorrectable, 16))};
-    const dim3 grid(grid_for(wave_tiles, kPk2Waves, KVECC_PACKED_DEC_V2_PER_CU)), block(kPk2Block);
+                      tab, stats, dyn};
+    const dim3 grid(grid_for(wave_tiles, kPk2Waves, kPk2PerCu)), block(kPk2Block);
     if (uncorrectable && stats)
       KVECC_LAUNCH((golay_decode_packed_wave_kernel<true, true>), grid, block, 0, st, a);
     else if (uncorrectable)
@@ -724,10 +578,10 @@ KVECC_API int kvecc_golay_decode_packed(const uint8_t *codewords, uint8_t *nibbl
     else
       KVECC_LAUNCH((golay_decode_packed_wave_kernel<false, false>), grid, block, 0, st, a);
     done = wave_tiles * kPk2TileCw;
-  } else if (KVECC_PACKED_DEC_STAGED && aligned(nibbles, 4) && aligned(codewords, 16)) {
+  } else if (aligned(nibbles, 4) && aligned(codewords, 16)) {
     const int64_t ntiles = m / kPkTile;
     if (ntiles > 0) {
-      const dim3 grid(grid_for(ntiles, 1, KVECC_PACKED_DEC_PER_CU)), block(kPkBlock);
+      const dim3 grid(grid_for(ntiles, 1, kPkDecPerCu)), block(kPkBlock);
       const uint32_t *c = reinterpret_cast<const uint32_t *>(codewords);
       uint32_t *n = reinterpret_cast<uint32_t *>(nibbles);
       if (uncorrectable && stats)
@@ -800,29 +654,11 @@ KVECC_API int kvecc_hamming84_decode_packed(const uint8_t *codewords, uint8_t *n
   if (!nibbles || !codewords) return set_error(KVECC_EINVAL, "hamming84_decode_packed: null pointer");
   hipStream_t st = as_stream(stream);
   int64_t done = 0;
-  const int64_t hp_tiles = n / (16 * (int64_t)kHp2TileChunks);
-  if (KVECC_H84_PACKED_V2 && aligned(nibbles, 8) && aligned(codewords, 16) &&
-      (!error_types || aligned(error_types, 4)) && hp_tiles > 0 && n < ((int64_t)1 << 31)) {
-    uint32_t *dyn = KVECC_PACKED_DEC_DYN ? shim_dyn_slot(stream) : nullptr;
-    if (KVECC_PACKED_DEC_DYN && !dyn) return KVECC_EHIP;
-    const HpDecArgs a{codewords, reinterpret_cast<u32x2 *>(nibbles), reinterpret_cast<uint32_t *>(error_types),
-                      (uint32_t)hp_tiles, stats, dyn};
-    const dim3 grid(grid_for(hp_tiles, kHp2Waves, KVECC_H84_PACKED_PER_CU)), block(kHp2Block);
-    if (error_types && stats)
-      KVECC_LAUNCH((h84_decode_packed_wave_kernel<true, true>), grid, block, 0, st, a);
-    else if (error_types)
-      KVECC_LAUNCH((h84_decode_packed_wave_kernel<true, false>), grid, block, 0, st, a);
-    else if (stats)
-      KVECC_LAUNCH((h84_decode_packed_wave_kernel<false, true>), grid, block, 0, st, a);
-    else
-      KVECC_LAUNCH((h84_decode_packed_wave_kernel<false, false>), grid, block, 0, st, a);
-    done = hp_tiles * 16 * (int64_t)kHp2TileChunks;
-  }
   if (done < n && aligned(nibbles, 8) && aligned(codewords, 16) && (!error_types || aligned(error_types, 4))) {
     const int64_t n16 = (n - done) / 16;
     if (n16 > 0) {
-      const dim3 grid(grid_for(n16, kHpBlock, KVECC_H84_PACKED_GRID_PER_CU)), block(kHpBlock);
-      const int64_t i0 = done / 16;  // after the wave tiles
+      const dim3 grid(grid_for(n16, kHpBlock, kHpGridPerCu)), block(kHpBlock);
+      const int64_t i0 = done / 16;
       const u32x4 *c = reinterpret_cast<const u32x4 *>(codewords) + i0;
       u32x2 *o = reinterpret_cast<u32x2 *>(nibbles) + i0;
       uint32_t *t = error_types ? reinterpret_cast<uint32_t *>(error_types) + i0 : nullptr;

@@ -281,9 +281,7 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
 
 // fp16/bf16 decode+dequant workgroups per CU (grid cap): 64 measured best
 // against 16 / 32 / 256 (73.4 vs 77.8 / 74.4 / 103.3 us fp16; profiles/r03/dd_ab2.log)
-#ifndef KVECC_DD_PER_CU
-#define KVECC_DD_PER_CU 64
-#endif
+constexpr int kDdPerCu = 64;
 template <typename TO>
 static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t rows, int64_t d,
                       int zero_doubles, uint64_t *stats, hipStream_t st) {
@@ -297,7 +295,7 @@ static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t
     // [8,4096,32,128]): fp16/bf16 1 access and 64 workgroups per CU, 86.8 ->
     // 76.2 us; fp32 4 accesses and 128 per CU, 131.8 -> 119.5 us
     if (sizeof(TO) == 2)
-      KVECC_LAUNCH((decode_dequant_wide_kernel<TO, 1>), dim3(grid_for(total, kBlock, KVECC_DD_PER_CU)),
+      KVECC_LAUNCH((decode_dequant_wide_kernel<TO, 1>), dim3(grid_for(total, kBlock, kDdPerCu)),
                    dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o, nchunk,
                    shift, total, zero_doubles, stats);
     else

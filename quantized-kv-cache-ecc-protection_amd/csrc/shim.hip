@@ -259,89 +259,38 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 // (row, 8-value chunk) items are the same for every tile: computed once.  HBM
 // traffic is the algorithm's: 4 B (3 B packed) per codeword in, d * sizeof(TO)
 // per row out, 4 B of scale per row.
-#ifndef KVECC_SHIM_TILE_NT
-#define KVECC_SHIM_TILE_NT 1     // non-temporal output stores and codeword loads
-#endif
-// workgroups per CU (LDS: 32 KiB table + a 2.25 KiB tile per wave); 2 beat 3
-// by 6-12 % at [8,4096,32,128] (tools/exp/run_shim_read.py)
-#ifndef KVECC_SHIM_TILE_PER_CU
-#define KVECC_SHIM_TILE_PER_CU 2
-#endif
-#ifndef KVECC_SHIM_TILE_BLOCK
-#define KVECC_SHIM_TILE_BLOCK 512
-#endif
-#ifndef KVECC_SHIM_TILE_NODECODE
-#define KVECC_SHIM_TILE_NODECODE 0
-#endif
-#ifndef KVECC_SHIM_TILE_TPI
-#define KVECC_SHIM_TILE_TPI 1
-#endif
-// Work distribution.  CHUNK 0: a persistent grid of PER_CU workgroups per CU,
-// wave w taking tiles w, w + nwaves, ...  CHUNK P > 0: wave w takes the P
-// consecutive tiles [w P, w P + P), and the grid covers every tile once, so
-// workgroups retire and are replaced in dispatch order; LDS_PAD bytes of
-// dynamic LDS per workgroup cap the workgroups per CU.  (BYTES_*: the same for
-// the byte-codec kernel, which has no tables to stage per workgroup.)
-#ifndef KVECC_SHIM_TILE_CHUNK
-#define KVECC_SHIM_TILE_CHUNK 0
-#endif
-#ifndef KVECC_SHIM_TILE_LDS_PAD
-#define KVECC_SHIM_TILE_LDS_PAD 0
-#endif
-// The byte-codec read without interpolation runs the full grid, one tile per
-// wave, 4 workgroups per CU (16 KiB of dynamic LDS on its 20 KiB): H(8,4) ->
-// fp16 at [8,4096,32,128] 137.6-138.6 us against 147.2 persistent with the
-// dynamic tail (8 workgroups per CU 138.6, 2: 174.2, 1: 261.4; 2 tiles per wave
-// 145.9).  The interpolating read keeps the persistent grid (172.1 full grid vs
-// 158.9: it prefetches the next tile's rows and halo behind the current one;
-// tools/exp/run_read_ab.py, profiles/r03/fused/read_ab11.log).
-#ifndef KVECC_SHIM_BYTES_CHUNK
-#define KVECC_SHIM_BYTES_CHUNK 1
-#endif
-#ifndef KVECC_SHIM_BYTES_LDS_PAD
-#define KVECC_SHIM_BYTES_LDS_PAD 16384
-#endif
-#ifndef KVECC_SHIM_BYTES_INTERP_CHUNK
-#define KVECC_SHIM_BYTES_INTERP_CHUNK KVECC_SHIM_TILE_CHUNK
-#endif
-// DYN (CHUNK 0): a wave takes the first DYN_STATIC_PCT % of its even share of
-// tiles statically (w, w + nwaves, ...) and the rest from work counters
-// (kDynCounters per launch, counter c handing out tiles base + k kDynCounters
-// + c in turn), one atomic per tile, issued a tile ahead.  With equal static
-// shares the waves of one launch finished 119-166 us apart at
-// [8,4096,32,128] (mean 143 us; tools/exp/run_wave_times.py): memory latency
-// is not even across the chip.  Tiles handed out dynamically go to whichever
-// CU asks, which costs locality (a static order with the waves scrambled over
-// the tiles of each round ran 8 % slower), so the dynamic part is the tail:
-// 25 % of the tiles measured 150.9 us against 169.9 static and 160-161 with
-// 50 or 75 % dynamic (Golay int32 -> fp16; profiles/r03/fused/).
-#ifndef KVECC_SHIM_TILE_DYN
-#define KVECC_SHIM_TILE_DYN 1
-#endif
-#ifndef KVECC_SHIM_BYTES_DYN
-#define KVECC_SHIM_BYTES_DYN KVECC_SHIM_TILE_DYN
-#endif
-// the fused reads' static share (the other TileSchedule users keep
-// KVECC_SHIM_TILE_DYN_STATIC_PCT = 75): 65 % ran Golay 161.0 / packed 147.0 /
-// H(8,4)+interp 156.2 us against 161.6 / 148.0 / 159.8 at 75 and 166-168 /
-// 153-155 / 164-166 at 85-90 (profiles/r03/fused/static_pct_ab1.log)
-#ifndef KVECC_SHIM_READ_STATIC_PCT
-#define KVECC_SHIM_READ_STATIC_PCT 65
-#endif
-constexpr int kTileBlock = KVECC_SHIM_TILE_BLOCK;  // 8 waves per workgroup
-constexpr int kTileTPI = KVECC_SHIM_TILE_TPI;      // tiles in flight per wave
+// Tuned constants of the wave-tile reads (A/B history: DESIGN.md §3, the
+// experiment forks under tools/exp).  None of them changes a result.
+//   * 512-thread workgroups, 2 per CU for the Golay kernel (LDS: 32 KiB of
+//     tables + a 2.25 KiB tile per wave): beat 3 per CU (24 waves) and 256-thread
+//     variants by 6-12 % (tools/exp/run_shim_read.py); r04 re-checked 256 x 3,
+//     384 x 2, 768 x 1, 1024 x 1 (161-168 us vs 160.8, profiles/r04/fused/).
+//   * non-temporal codeword loads and output stores (-5 %).
+//   * the byte-codec read without interpolation runs the full grid, one tile
+//     per wave, capped at 4 workgroups per CU by 16 KiB of dynamic LDS: H(8,4)
+//     -> fp16 at [8,4096,32,128] 137.6-138.6 us against 147.2 persistent (8 per
+//     CU 138.6, 2: 174.2, 1: 261.4); the interpolating read and the Golay read
+//     keep the persistent grid with the dynamic tail (172.1 vs 158.9 full grid
+//     for interpolation; Golay full grids 162-335 us, profiles/r04/fused/).
+//   * dynamic tail: a wave takes the first 65 % of its even share of tiles
+//     statically (w, w + nwaves, ...) and the rest from per-launch work
+//     counters (TileSchedule, kvecc_internal.h), one atomic per tile issued a
+//     tile ahead.  With equal static shares the waves of one launch finished
+//     119-166 us apart (mean 143 us; memory latency is not even across the
+//     chip), and handing tiles to whichever CU asks costs locality (a static
+//     order with the waves scrambled over the tiles of each round ran 8 %
+//     slower), so the dynamic part is the tail: 65 % ran Golay 161.0 / packed
+//     147.0 / H(8,4)+interp 156.2 us against 161.6 / 148.0 / 159.8 at 75 and
+//     166-168 / 153-155 / 164-166 at 85-90 (profiles/r03/fused/static_pct_ab1.log).
+constexpr int kTileBlock = 512;                    // 8 waves per workgroup
 constexpr int kTileWaves = kTileBlock / kWave;
+constexpr int kShimTilePerCu = 2;                  // Golay / interpolating reads: persistent grid
+constexpr int kShimBytesLdsPad = 16384;            // plain byte-codec read: caps 4 workgroups per CU
+constexpr uint32_t kShimReadStaticPct = 65;        // static share of the dynamic-tail schedule
 constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
 constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
 constexpr int kTileChunks = 5;                     // 8-value output chunks per lane per tile (max)
-constexpr int kTileAux = KVECC_SHIM_TILE_NT ? 2 : 0;  // buffer-load cache policy: nt
-// Golay read tables in LDS.  SPLITP: the parity half (data -> spread data |
-// parity << 20, linear over GF(2)) as two 64-entry tables, XORed, with the
-// 16 KiB correction half: 16.5 KiB instead of 32 KiB per workgroup.
-#ifndef KVECC_SHIM_GOLAY_SPLITP
-#define KVECC_SHIM_GOLAY_SPLITP 0
-#endif
-constexpr int kGolayTabWords = KVECC_SHIM_GOLAY_SPLITP ? 128 + 4096 : 8192;
+constexpr int kTileAux = 2;                        // buffer cache policy: nt
 
 struct ShimTileArgs {
   const void *cache[2];
@@ -362,61 +311,6 @@ struct ShimTileArgs {
 };
 
 
-
-// KVECC_SHIM_TILE_DYN == 2 (experiment): the schedule at workgroup granularity.
-// Group g is the kTileWaves consecutive tiles g kTileWaves + wave; the
-// workgroup takes its first DYN_STATIC_PCT % of groups statically (blockIdx,
-// blockIdx + nwg, ...) and the rest from the counters, wave 0 grabbing one
-// group ahead and handing it to the other waves through LDS at a workgroup
-// barrier per tile.  Counter c serves workgroups blockIdx = c (mod
-// kDynCounters); its last user resets it, as in TileSchedule.
-struct WgSchedule {
-  uint32_t ngroups, nwg, sidx, nstatic, cidx, gk, last_k, it, base;
-  uint32_t *ctr;
-  __device__ __forceinline__ uint32_t grab(uint32_t lane) {
-    uint32_t z;
-    asm("v_mov_b32 %0, 0" : "=v"(z));
-    uint32_t k = 0;
-    if (lane == 0) k = __hip_atomic_fetch_add(ctr + z, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return k;
-  }
-  __device__ __forceinline__ void init(const ShimTileArgs &a, uint32_t wave, uint32_t lane) {
-    ngroups = (a.units + kTileWaves - 1) / kTileWaves;
-    nwg = gridDim.x;
-    sidx = 1;
-    it = 0;
-    nstatic = max(1u, (uint32_t)(KVECC_SHIM_TILE_DYN_STATIC_PCT * ((ngroups + nwg - 1) / nwg) / 100));
-    base = nstatic * nwg;
-    cidx = blockIdx.x % kDynCounters;
-    ctr = a.dyn + kDynStride * cidx;
-    const uint32_t kc = ngroups > base + cidx ? (ngroups - base - cidx + kDynCounters - 1) / kDynCounters : 0u;
-    const uint32_t active = min(nwg, ngroups);
-    const uint32_t wc = (active - cidx + kDynCounters - 1) / kDynCounters;
-    last_k = kc + wc - 1;
-    if (wave == 0) gk = grab(lane);
-  }
-  // the workgroup's next group (>= ngroups: none); every wave calls it
-  __device__ __forceinline__ uint32_t next(uint32_t *slot, uint32_t wave, uint32_t lane) {
-    if (sidx < nstatic) {
-      const uint32_t g = blockIdx.x + sidx * nwg;
-      ++sidx;
-      if (g < ngroups) return g;
-      sidx = nstatic;
-    }
-    ++it;
-    if (wave == 0) {
-      const uint32_t k = __builtin_amdgcn_readfirstlane(gk);
-      const uint32_t g = base + k * kDynCounters + cidx;
-      if (g < ngroups)
-        gk = grab(lane);
-      else if (k == last_k && lane == 0)
-        __hip_atomic_exchange(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0) slot[it & 1] = g;
-    }
-    __syncthreads();  // slot[it & 1] written; slot[(it + 1) & 1] is not rewritten before the next barrier
-    return __builtin_amdgcn_readfirstlane(slot[it & 1]);
-  }
-};
 
 // a wave's tile: rows [row0, row0 + rows) of one cache side (wave-uniform)
 struct ShimTile {
@@ -521,32 +415,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_out(const ShimTileArgs &a
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)uni(t.rows * a.d * (uint32_t)sizeof(TO)), 0x00020000);
 }
 
-// timing experiment (tools/exp/run_wave_times.py): each wave's first-tile start
-// and exit times (s_memrealtime, 100 MHz) into a buffer set by kvecc_exp_wave_times
-#ifndef KVECC_SHIM_WAVE_TIMES
-#define KVECC_SHIM_WAVE_TIMES 0
-#endif
-#if KVECC_SHIM_WAVE_TIMES
-__device__ uint64_t *g_wave_times;
-extern "C" __attribute__((visibility("default"))) int kvecc_exp_wave_times(void *buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_wave_times), &buf, sizeof(buf)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 template <typename TO, bool STATS, bool PACKED>
 __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t tab[kGolayTabWords];
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileTPI][kTileStage];
-  // row scales of the staged tiles: written in phase 1, read in phase 2 (a
+  __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  // row scales of the staged tile: written in phase 1, read in phase 2 (a
   // scale kept in a register across the next tile's prefetch made the compiler
   // wait for that prefetch before phase 2)
-  __shared__ float scale_all[kTileWaves][kTileTPI][kWave];
-  if (KVECC_SHIM_GOLAY_SPLITP) {  // parity half as two 64-entry tables (it is GF(2)-linear)
-    for (int i = threadIdx.x; i < 128; i += kTileBlock) tab[i] = a.atab[i < 64 ? i : (i - 64) << 6];
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab + 4096);
-    u32x4 *dst = reinterpret_cast<u32x4 *>(tab + 128);
-    for (int i = threadIdx.x; i < 1024; i += kTileBlock) dst[i] = src[i];
-  } else {
+  __shared__ float scale_all[kTileWaves][kWave];
+  {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(tab);
 #pragma unroll
@@ -588,157 +465,87 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
     }
   }
   uint32_t bits = 0, unc = 0;
-
-  // kTileTPI tiles per iteration: u, u + ustep, ...; all their loads in flight
-  constexpr uint32_t kChunk = KVECC_SHIM_TILE_CHUNK;
-  static_assert(kChunk == 0 || kTileTPI == 1, "chunked tiles take one tile per iteration");
-  constexpr bool kDyn = KVECC_SHIM_TILE_DYN == 1 && kChunk == 0 && kTileTPI == 1;
-  constexpr bool kWgDyn = KVECC_SHIM_TILE_DYN == 2 && kChunk == 0 && kTileTPI == 1;
+  // waves retire independently: no workgroup barrier below
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
-  uint32_t u = kChunk ? gw * kChunk : gw;
-  const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
-  const uint32_t ustep = kChunk ? 1u : nwaves;
-  // (no workgroup barrier below except WgSchedule's: waves retire independently)
-  if (!kWgDyn && u >= uend) return;
-  TileSchedule<kDyn> sched;
-  WgSchedule wsched;
-  __shared__ uint32_t wg_slot[2];
-  if (kWgDyn)
-    wsched.init(a, wave, lane);
-  else
-    sched.init(a.units, a.dyn, gw, nwaves, lane, KVECC_SHIM_READ_STATIC_PCT);
-#if KVECC_SHIM_DYN_PROBE == 3
-  u = sched.perm(gw);
-#endif
-#if KVECC_SHIM_WAVE_TIMES
-  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-  uint32_t n_tiles = 0;
-#endif
-  ShimTile cur[kTileTPI];
-  bool valid[kTileTPI];
-  u32x4 w[kTileTPI][kTileGroups];
-  float scale[kTileTPI];
-  auto fetch = [&](uint32_t u0) {
+  uint32_t u = gw;
+  if (u >= a.units) return;
+  TileSchedule sched;
+  sched.init(a.units, a.dyn, gw, nwaves, lane, kShimReadStaticPct);
+  ShimTile cur = shim_tile(a, u);
+  u32x4 w[kTileGroups];
+  float scale;
+  tile_issue<PACKED>(a, cur, lane, it, w, scale);
+  uint8_t *stage = stage_all[wave];
+  const char *tb = reinterpret_cast<const char *>(tab);
+  for (;;) {
+    // ---- phase 1: decode 4 codewords per group into the LDS tile ---------------
+    scale_all[wave][lane] = scale;
+    // (n & 3) | uncorrectable << 6 per codeword (the correction table's byte
+    // 3), summed over the lane's <= 16 codewords of the tile: no carry
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int k = 0; k < kTileTPI; ++k) {
-      valid[k] = u0 + k * ustep < uend;  // uniform
-      if (valid[k]) {
-        cur[k] = shim_tile(a, u0 + k * ustep);
-        tile_issue<PACKED>(a, cur[k], lane, it, w[k], scale[k]);
+    for (int i = 0; i < kTileGroups; ++i) {
+      if (i * kWave >= (int)groups) break;  // uniform
+      const uint32_t q = it.q1[i];
+      uint32_t sp[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t cw = tile_cw<PACKED>(w[i], c);
+        // a row's last group runs into the next row: that codeword decodes
+        // as 0 (no count), and its bytes land in the LDS row's padding
+        if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
+        const uint32_t p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
+        // syndrome = parity bits ^ parity(data), as a byte offset: ((cw >> 12 ^ p >> 20) & 0xFFF) * 4
+        const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 16384 + (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
+        sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
+        if (STATS) cnt += e >> 24;
+      }
+      if (it.r1[i] < a.tr) {  // groups past the tile's last row are never staged
+        uint32_t *dst = reinterpret_cast<uint32_t *>(stage + it.r1[i] * a.lr + 12 * q);
+        dst[0] = sp[0] | sp[1] << 24;
+        dst[1] = sp[1] >> 8 | sp[2] << 16;
+        dst[2] = sp[2] >> 16 | sp[3] << 8;
       }
     }
-  };
-  fetch(u);
-  for (;;) {
-    // ---- phase 1: decode 4 codewords per group into the LDS tiles -------------
-#pragma unroll
-    for (int k = 0; k < kTileTPI; ++k) {
-      if (!valid[k]) continue;
-      uint8_t *stage = stage_all[wave][k];
-      scale_all[wave][k][lane] = scale[k];
-      // (n & 3) | uncorrectable << 6 per codeword (the correction table's byte
-      // 3), summed over the lane's <= 16 codewords of the tile: no carry
-      uint32_t cnt = 0;
-#pragma unroll
-      for (int i = 0; i < kTileGroups; ++i) {
-        if (i * kWave >= (int)groups) break;  // uniform
-        const uint32_t q = it.q1[i];
-        uint32_t sp[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          uint32_t cw = tile_cw<PACKED>(w[k][i], c);
-          // a row's last group runs into the next row: that codeword decodes
-          // as 0 (no count), and its bytes land in the LDS row's padding
-          if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
-#if KVECC_SHIM_TILE_NODECODE  // memory-ceiling experiment: no table lookups (wrong values)
-          const uint32_t p = cw, e = 0;
-#else
-          const char *tb = reinterpret_cast<const char *>(tab);
-          uint32_t p;
-          if (KVECC_SHIM_GOLAY_SPLITP)  // entries of data bits 0-5 and 6-11, XORed
-            p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0xFCu)) ^
-                *reinterpret_cast<const uint32_t *>(tb + 256 + ((cw >> 4) & 0xFCu));
-          else
-            p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
-          // syndrome = parity bits ^ parity(data), as a byte offset: ((cw >> 12 ^ p >> 20) & 0xFFF) * 4
-          const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 4 * (kGolayTabWords - 4096) +
-                                                                 (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
-#endif
-          sp[c] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);  // (p ^ e) & mask
-          if (STATS) cnt += e >> 24;
-        }
-        if (it.r1[i] < a.tr) {  // groups past the tile's last row are never staged
-          uint32_t *dst = reinterpret_cast<uint32_t *>(stage + it.r1[i] * a.lr + 12 * q);
-          dst[0] = sp[0] | sp[1] << 24;
-          dst[1] = sp[1] >> 8 | sp[2] << 16;
-          dst[2] = sp[2] >> 16 | sp[3] << 8;
-        }
-      }
-      if (STATS) {
-        bits += cnt & 63u;
-        unc += cnt >> 6;
-      }
+    if (STATS) {
+      bits += cnt & 63u;
+      unc += cnt >> 6;
     }
     wave_lds_sync();
-    // ---- prefetch the next tiles' codewords and scales ---------------------------
-    ShimTile t[kTileTPI];
-    bool tv[kTileTPI];
-#pragma unroll
-    for (int k = 0; k < kTileTPI; ++k) {
-      t[k] = cur[k];
-      tv[k] = valid[k];
-    }
-#if KVECC_SHIM_WAVE_TIMES
-    ++n_tiles;
-#endif
-    bool more;
-    if (kWgDyn) {
-      const uint32_t g = wsched.next(wg_slot, wave, lane);
-      more = g < wsched.ngroups;  // uniform over the workgroup
-      u = g * kTileWaves + wave;
-      if (more) fetch(u);  // valid[] = u < units: a wave past the last tile idles, keeps the barriers
-    } else {
-      u = kDyn ? sched.next(u, lane) : u + kTileTPI * ustep;
-      more = u < uend;
-      if (more) fetch(u);
+    // ---- prefetch the next tile's codewords and scales ----------------------------
+    const ShimTile t = cur;
+    u = sched.next(u, lane);
+    const bool more = u < a.units;
+    if (more) {
+      cur = shim_tile(a, u);
+      tile_issue<PACKED>(a, cur, lane, it, w, scale);
     }
     // ---- phase 2: dequantize VPL values per lane, one 16-byte store each -------
     // (stores of rows past the tile fall outside its output descriptor: dropped)
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
 #pragma unroll
-    for (int k = 0; k < kTileTPI; ++k) {
-      if (!tv[k]) continue;
-      const uint8_t *stage = stage_all[wave][k];
-      const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t[k]);
-      const bool dead = t[k].row0 < 0;
-#pragma unroll
-      for (int i = 0; i < NC; ++i) {
-        if (i * kWave >= (int)chunks) break;  // uniform
-        uint32_t r, l, o = 0;
-        if (kItemsInRegs) {
-          r = it.r2[i];
-          l = it.j2[i];
-        } else {
-          const uint32_t v = lane + kWave * i;
-          const uint32_t rv = __umulhi(v, inv_dv), j = v - rv * dv;
-          r = min(rv, a.tr - 1);  // as it.r2: LDS reads stay inside the tile
-          l = r * a.lr + V * j;
-          o = (rv * a.d + V * j) * (uint32_t)sizeof(TO);
-        }
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + l);
-        const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
-        tile_store(os, kItemsInRegs ? it.o2[i] : o, dq16<TO>(nb, scale_all[wave][k][r], dead));
+    for (int i = 0; i < NC; ++i) {
+      if (i * kWave >= (int)chunks) break;  // uniform
+      uint32_t r, l, o;
+      if (kItemsInRegs) {
+        r = it.r2[i];
+        l = it.j2[i];
+        o = it.o2[i];
+      } else {
+        const uint32_t v = lane + kWave * i;
+        const uint32_t rv = __umulhi(v, inv_dv), j = v - rv * dv;
+        r = min(rv, a.tr - 1);  // as it.r2: LDS reads stay inside the tile
+        l = r * a.lr + V * j;
+        o = (rv * a.d + V * j) * (uint32_t)sizeof(TO);
       }
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(stage + l);
+      const uint32_t nb[2] = {src[0], V == 8 ? src[1] : 0u};
+      tile_store(os, o, dq16<TO>(nb, scale_all[wave][r], dead));
     }
     if (!more) break;
     wave_lds_sync();  // phase 2 reads done before the next phase 1 overwrites
   }
-#if KVECC_SHIM_WAVE_TIMES
-  if (lane == 0 && g_wave_times) {
-    g_wave_times[3 * gw] = t_start;
-    g_wave_times[3 * gw + 1] = __builtin_amdgcn_s_memrealtime();
-    g_wave_times[3 * gw + 2] = n_tiles;
-  }
-#endif
   if (STATS) {  // wave reduction, one atomic pair per wave
     bits = wave_sum(bits);
     unc = wave_sum(unc);
@@ -763,30 +570,13 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 // non-temporal stores.  A row in a missing block (table entry -1) reads as
 // zero codewords and outputs +0, as in the Golay kernel and the host twin.
 constexpr int kByteTileItems = 4;  // 16-value chunks per lane per phase (max)
-// memory/VALU-ceiling experiments for the interpolating read (wrong values;
-// A/B: tools/exp/run_shim_read_interp.py): no neighbour-row loads / no
-// interpolation arithmetic
-#ifndef KVECC_SHIM_INTERP_NOHALO
-#define KVECC_SHIM_INTERP_NOHALO 0
-#endif
-#ifndef KVECC_SHIM_INTERP_NOVALU
-#define KVECC_SHIM_INTERP_NOVALU 0
-#endif
 // Interpolation only changes a double error's value.  A tile whose decode saw
 // no double (a wave ballot in phase 1) dequantizes without the interpolation
-// arithmetic and the neighbour-row reads (SKIP; at BER 1e-3 ~95 % of tiles).
+// arithmetic and the neighbour-row reads (at BER 1e-3 ~95 % of tiles).
 // [8,4096,32,128] K+V fp16, per launch: 204 -> 177 us at BER 0, 199 -> 176 us
-// at 1e-3, 201 -> 206 us at 1e-2 (profiles/r02/interp_read/).  LAZY loads the
-// neighbour rows only when a double sits in the tile's first or last row
-// (synchronously, and from then on the wave prefetches them): 161 us at BER 0,
-// but 188 us at 1e-3 and 221 us at 1e-2, so it stays off.
-#ifndef KVECC_SHIM_INTERP_LAZY
-#define KVECC_SHIM_INTERP_LAZY 0
-#endif
-#ifndef KVECC_SHIM_INTERP_SKIP
-#define KVECC_SHIM_INTERP_SKIP 1
-#endif
-
+// at 1e-3, 201 -> 206 us at 1e-2 (profiles/r02/interp_read/).  Loading the
+// neighbour rows only when a double sits in a tile's first or last row ran 161
+// us at BER 0 but 188 / 221 us at 1e-3 / 1e-2, so every tile prefetches them.
 template <typename TO, int CODEC, bool INTERP, bool STATS, int CHUNK>
 __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
@@ -813,21 +603,19 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
   uint32_t n1 = 0, n2 = 0;
-  constexpr uint32_t kChunk = CHUNK;
-  constexpr bool kDyn = KVECC_SHIM_BYTES_DYN && kChunk == 0;
+  // CHUNK > 0: wave w takes the CHUNK tiles [w CHUNK, w CHUNK + CHUNK) of a
+  // full grid; 0: the persistent grid with the dynamic tail
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
-  uint32_t u = kChunk ? gw * kChunk : gw;
-  const uint32_t uend = kChunk ? min(a.units, u + kChunk) : a.units;
-  const uint32_t ustep = kChunk ? 1u : nwaves;
+  uint32_t u = CHUNK ? gw * CHUNK : gw;
+  const uint32_t uend = CHUNK ? min(a.units, u + CHUNK) : a.units;
   if (u >= uend) return;
-  TileSchedule<kDyn> sched;
-  sched.init(a.units, a.dyn, gw, nwaves, lane, KVECC_SHIM_READ_STATIC_PCT);
+  TileSchedule sched;
+  if (!CHUNK) sched.init(a.units, a.dyn, gw, nwaves, lane, kShimReadStaticPct);
 
   ShimTile cur;
   u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
   float scale;
-  bool eager = !KVECC_SHIM_INTERP_LAZY;  // prefetch neighbour rows (sticky once a tile needed them)
-  bool has_hw = false;                   // hw holds the current tile's neighbour rows
+  bool has_hw = false;  // hw holds the current tile's neighbour rows
   // neighbour rows of tile c: lanes [0, cpr) row pos0 - 1 (pos0 itself at the
   // context's start), [cpr, 2 cpr) row pos0 + rows (the last row at its end)
   auto load_halo = [&](const ShimTile &c) -> u32x4 {
@@ -867,7 +655,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
       if (i * kWave >= (int)items) break;  // uniform
       w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
     }
-    has_hw = INTERP && !KVECC_SHIM_INTERP_NOHALO && eager && cur.rows > 0;
+    has_hw = INTERP && cur.rows > 0;
     if (has_hw) hw = load_halo(cur);
   };
   // 4 codewords -> data | type << 4 per byte (and the statistics); `dbl`
@@ -894,7 +682,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     // ---- phase 1: decode into the LDS tile (row r at (r + INTERP) * d) --------
     const uint32_t off0 = INTERP ? a.d : 0u;
     scale_all[wave][lane] = scale;
-    bool dbl_any = false, dbl_edge = false;  // this lane saw a double / one in the first or last row
+    bool dbl_any = false;  // this lane saw a double
 #pragma unroll
     for (int i = 0; i < kByteTileItems; ++i) {
       if (i * kWave >= (int)items) break;  // uniform
@@ -908,18 +696,11 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
       const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
                      dec(w[i].w, real, dbl)};
       dbl_any |= dbl != 0;
-      dbl_edge |= dbl != 0 && (ir[i] == 0 || ir[i] + 1 == cur.rows);
       // (with interpolation, rows past the tile's end would overwrite the row below)
       if (ir[i] < (INTERP ? cur.rows : a.tr)) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
     }
-    // wave-uniform: interpolate this tile at all / does it need its neighbour rows
-    const bool tile_dbl = INTERP && (!KVECC_SHIM_INTERP_SKIP || __builtin_amdgcn_ballot_w64(dbl_any) != 0);
-    if (INTERP && KVECC_SHIM_INTERP_LAZY && !KVECC_SHIM_INTERP_NOHALO && !has_hw &&
-        __builtin_amdgcn_ballot_w64(dbl_edge) != 0) {
-      hw = load_halo(cur);  // waits here; later tiles prefetch theirs
-      has_hw = true;
-      eager = true;
-    }
+    // wave-uniform: does this tile hold a double error at all
+    const bool tile_dbl = INTERP && __builtin_amdgcn_ballot_w64(dbl_any) != 0;
     if (INTERP && has_hw && lane < 2 * cpr) {  // neighbours: row 0 above, row rows + 1 below
       uint32_t none = 0;
       const u32x4 d4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none),
@@ -929,7 +710,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     }
     wave_lds_sync();
     const ShimTile t = cur;
-    u = kDyn ? sched.next(u, lane) : u + ustep;
+    u = CHUNK ? u + 1 : sched.next(u, lane);
     const bool more = u < uend;
     if (more) fetch(u);
     // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
@@ -962,7 +743,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
         tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
       }
     };
-    if (INTERP && !KVECC_SHIM_INTERP_NOVALU && tile_dbl)
+    if (INTERP && tile_dbl)
       phase2(std::integral_constant<bool, true>{});
     else
       phase2(std::integral_constant<bool, false>{});
@@ -1043,13 +824,13 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
 // persistent grid
 static unsigned tile_grid(uint32_t units, uint32_t chunk) {
   if (chunk) return (unsigned)cdiv(cdiv(units, chunk), kTileWaves);
-  return (unsigned)std::min<int64_t>(cdiv(units, kTileWaves), (int64_t)cu_count() * KVECC_SHIM_TILE_PER_CU);
+  return (unsigned)std::min<int64_t>(cdiv(units, kTileWaves), (int64_t)cu_count() * kShimTilePerCu);
 }
 
 template <typename TO>
 static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = tile_grid(a.units, KVECC_SHIM_TILE_CHUNK);
-  constexpr unsigned pad = KVECC_SHIM_TILE_LDS_PAD;
+  const unsigned grid = tile_grid(a.units, 0);
+  constexpr unsigned pad = 0;
   if (a.stats && packed)
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), pad, st, a);
   else if (a.stats)
@@ -1062,9 +843,9 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
 
 template <typename TO, int CODEC, bool INTERP>
 static void launch_bytes_tiles_s(const ShimTileArgs &a, hipStream_t st) {
-  constexpr int kChunk = INTERP ? KVECC_SHIM_BYTES_INTERP_CHUNK : KVECC_SHIM_BYTES_CHUNK;
+  constexpr int kChunk = INTERP ? 0 : 1;  // interpolation: persistent; plain: full grid, one tile per wave
   const unsigned grid = tile_grid(a.units, kChunk);
-  const unsigned pad = kChunk ? KVECC_SHIM_BYTES_LDS_PAD : 0u;  // caps the workgroups per CU
+  const unsigned pad = kChunk ? kShimBytesLdsPad : 0u;  // caps the workgroups per CU
   if (a.stats)
     KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true, kChunk>), dim3(grid), dim3(kTileBlock), pad,
                  st, a);

@@ -52,6 +52,8 @@ def kernels(tmp_path_factory):
         if field("name") is None or field("vgpr_count") is None:
             continue
         out[field("name").group(1)] = {
+            "lds": int(field("group_segment_fixed_size").group(1)),
+            "block": int(field("max_flat_workgroup_size").group(1)),
             "vgpr": int(field("vgpr_count").group(1)),
             "agpr": int(ent.split("\n", 1)[0].strip()),
             "spill": int(field("vgpr_spill_count").group(1)) if field("vgpr_spill_count") else 0,
@@ -85,3 +87,56 @@ def test_hot_kernel_budgets(kernels, pattern, limit):
     hit = {k: v["vgpr"] + v["agpr"] for k, v in kernels.items() if re.search(pattern, k)}
     assert hit, pattern
     assert max(hit.values()) <= limit, hit
+
+
+# The tuned launch shapes the library ships (csrc/*.hip constants).
+# Each kernel's static LDS and workgroup size are fixed by those constants, so a
+# build with other values (an experiment's) fails here.
+SHIPPED = [
+    # fused Golay read: 512 threads, 32 KiB tables + 8 x (2304 B tile + 256 B scales)
+    (r"shim_read_golay_tiles_kernelI6__half", 512, 32768 + 8 * (2304 + 256)),
+    # fused byte-codec read: 512 threads, 8 x (2304 + 256) B (+16 KiB dynamic at launch)
+    (r"shim_read_bytes_tiles_kernelI6__half", 512, 8 * (2304 + 256)),
+    # packed Golay decode wave tiles: 512 threads, 24 KiB tables + 8 x 3 KiB stage
+    (r"golay_decode_packed_wave_kernel", 512, 24576 + 8 * 3072),
+    # per-head rows register tiles: 512 threads
+    (r"golay_decode_rows_reg_kernel", 512, None),
+    (r"^_ZN5kvecc19golay_decode_kernel", 512, None),
+    (r"^_ZN5kvecc19golay_encode_kernel", 1024, None),
+]
+
+
+@pytest.mark.parametrize("pattern,block,lds", SHIPPED)
+def test_shipped_launch_shapes(kernels, pattern, block, lds):
+    hit = {k: v for k, v in kernels.items() if re.search(pattern, k)}
+    assert hit, pattern
+    for k, v in hit.items():
+        assert v["block"] == block, (k, v)
+        if lds is not None:
+            assert v["lds"] == lds, (k, v)
+
+
+def test_no_experiment_switches_in_product_sources():
+    """The product sources carry no build-time switches (#if/#ifndef KVECC_*):
+    experiment variants live in tools/exp forks, so no -D can change what the
+    library computes.  The only KVECC_ preprocessor guard left is kvecc.h's own
+    include guard."""
+    csrc = os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd", "csrc")
+    bad = []
+    for f in sorted(os.listdir(csrc)):
+        for i, line in enumerate(open(os.path.join(csrc, f)), 1):
+            if re.match(r"\s*#\s*(if|ifdef|ifndef|elif)\b.*\bKVECC_", line):
+                bad.append(f"{f}:{i}: {line.strip()}")
+    assert not bad, bad
+
+
+def test_no_experiment_symbols_exported():
+    """libkvecc.so exports the C ABI of include/kvecc.h and nothing from the
+    experiment forks (kvecc_exp_*) or the round-3 wave-timing probe."""
+    readelf = os.path.join(LLVM, "llvm-readelf")
+    if not os.path.exists(LIB) or not os.path.exists(readelf):
+        pytest.skip("libkvecc.so or llvm-readelf missing")
+    syms = subprocess.run([readelf, "--dyn-syms", "-W", LIB], check=True, capture_output=True, text=True).stdout
+    assert "kvecc_golay_decode" in syms  # the C ABI is there
+    bad = [ln for ln in syms.splitlines() if "kvecc_exp_" in ln or "wave_times" in ln]
+    assert not bad, bad

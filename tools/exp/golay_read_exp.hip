@@ -62,7 +62,7 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
   const uint32_t gw = blockIdx.x * kW + wave;
   uint32_t u = SCHED ? gw * CHUNK : gw;
   const uint32_t uend = SCHED ? min(a.units, u + CHUNK) : a.units;
-  TileSchedule<SCHED == 0> sched;
+  TileSchedule sched;
   ShimTile cur;
   u32x4 w[kTileGroups];
   float scale;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(BLOCK) void golay_read_pf2_kernel(ShimTileArgs a, c
   uint32_t bits = 0, unc = 0;
   const uint32_t gw = blockIdx.x * kW + wave;
   if (gw >= a.units) return;
-  TileSchedule<true> sched;
+  TileSchedule sched;
   sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
   uint8_t *stage = stage_all[wave];
   struct Buf {
