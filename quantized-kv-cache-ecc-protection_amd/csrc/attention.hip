@@ -1338,6 +1338,7 @@ template <int D>
 static int launch_mfma_d(const AttnArgs &a, int64_t batch, int gm, hipStream_t st) {
   const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * a.heads / gm));
   switch (gm) {
+    case 1: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 1>), grid, dim3(kBlock), 0, st, a); break;
     case 2: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 2>), grid, dim3(kBlock), 0, st, a); break;
     case 4: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 4>), grid, dim3(kBlock), 0, st, a); break;
     case 8: KVECC_LAUNCH((paged_attn_h84_mfma_kernel<D, 8>), grid, dim3(kBlock), 0, st, a); break;
@@ -1373,8 +1374,8 @@ static int launch_mfma(int codec, const AttnArgs &a, int64_t batch, int gm, hipS
 }
 
 // query heads per workgroup of the MFMA kernels (0: not applicable): caches under
-// 4 GiB, fp16 queries (16-byte aligned), a group of >= 2 query heads per cache
-// head; Hamming(8,4) at head_dim 32 / 64 / 128, Golay (int32 or packed) at head_dim 128
+// 4 GiB, fp16 queries (16-byte aligned); Hamming(8,4) at head_dim 32 / 64 / 128
+// for any group, Golay (int32 or packed) at head_dim 128 for groups of >= 2
 // workgroups per CU of the Golay kernel's split choice (157 VGPRs, 49-73 KiB of
 // LDS): 2 measured 30.6 vs 34.2 us at 4 (32q/8kv; profiles/r03/attn/attn_gqa14.log)
 constexpr int kMfmaGolayWgPerCu = 2;
@@ -1384,8 +1385,15 @@ static int attn_mfma_heads(int codec, int q_dtype, const void *query, int64_t d,
   const bool h84 = codec == KVECC_CODEC_H84 && (d == 32 || d == 64 || d == 128);
   const bool golay = (codec == KVECC_CODEC_GOLAY || codec == KVECC_CODEC_GOLAY_PACKED) &&
                      d == 128;
-  if (!(h84 || golay) || q_dtype != KVECC_F16 || !buf || !aligned(query, 16) || group < 2)
-    return 0;
+  if (!(h84 || golay) || q_dtype != KVECC_F16 || !buf || !aligned(query, 16)) return 0;
+  // MHA (one query head per cache head): H(8,4) too, one of the 16 MFMA
+  // columns used -- the matrix cores take the dot products and the V update
+  // off the VALU, and the table lookups are the only per-value LDS work:
+  // [8,4096,32,128] 49.5 us per call against 54.6 for the VALU split kernel.
+  // Golay MHA stays on the VALU kernels (packed 76 vs 68 us, int32 86 vs 73:
+  // its per-codeword decode, not the arithmetic, is the work).
+  // (tools/exp/run_attn_exp.py, profiles/r04/attn/mfma_mha_ab.log)
+  if (group == 1) return h84 ? 1 : 0;
   return group % 16 == 0 ? 16 : group % 8 == 0 ? 8 : group % 4 == 0 ? 4 : group % 2 == 0 ? 2 : 0;
 }
 

@@ -250,7 +250,12 @@ __global__ __launch_bounds__(kPkBlock) void golay_decode_packed_staged_kernel(
 // (error data | bits << 24 | uncorrectable << 31), data = (c ^ e) & 0xFFF in one
 // v_bitop3, the statistics as a 32-bit sum of entries (bits 24-30: corrected
 // bits of <= 8 codewords) and the flag bits shifted in with v_alignbit.
-constexpr int kPk2PerCu = 2;  // workgroups per CU of the persistent grid
+// workgroups per CU of the persistent grid, and the dynamic tail's static
+// share: 2 per CU and 50 % measured 34.8-35.0 us against 35.0-35.3 at 75 %; 3
+// per CU (any share), 256- and 384-thread workgroups, LDS-DMA staging and
+// conflict-free table addresses were all no faster (profiles/r04/packed_dec_ab_*.log)
+constexpr int kPk2PerCu = 2;
+constexpr uint32_t kPk2StaticPct = 50;
 constexpr int kPk2Block = 512;
 constexpr int kPk2Waves = kPk2Block / kWave;
 // groups of 8 codewords per lane per wave tile (2: 1024 codewords, 3 KiB);
@@ -284,7 +289,7 @@ __global__ __launch_bounds__(kPk2Block) void golay_decode_packed_wave_kernel(PkD
   if (gw >= a.units) return;  // no workgroup barrier below
   uint8_t *stage = stage_all[wave];
   TileSchedule sched;
-  sched.init(a.units, a.dyn, gw, nwaves, lane);
+  sched.init(a.units, a.dyn, gw, nwaves, lane, kPk2StaticPct);
   // whole codeword buffer (< 2 GiB, checked on the host); nt loads
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t *>(a.cw), 0, (int)(a.units * (uint32_t)kPk2TileBytes), 0x00020000);

@@ -170,3 +170,31 @@ def test_quantizers_reject_unknown_scale_rule():
     for fn in ("kvecc_quantize_encode_rows", "kvecc_shim_write", "kvecc_cpu_quantize_encode_rows",
                "kvecc_cpu_shim_write"):
         assert "scale_rule" in header.split(fn + "(")[1].split(";")[0], fn
+
+
+@pytest.mark.gpu
+def test_short_or_wrong_stats_buffers_raise(gpu):
+    """The kernels add into slot (workgroup % KVECC_STATS_SLOTS) of the stats
+    buffer through a raw pointer: every wrapper checks the buffer (contiguous
+    int64, >= KVECC_STATS_WORDS elements, on the launch device) and raises
+    ValueError instead of letting a kernel write past it."""
+    import torch
+    from kvecc import ops
+    cw = ops.hamming84_encode(torch.randint(0, 16, (4096,), dtype=torch.uint8, device=gpu))
+    out = torch.empty_like(cw)
+    good = ops.new_stats(gpu)
+    bad = [good[:100], good.to(torch.int32), good.view(32, 16)[:, :8], ops.new_stats("cpu"),
+           torch.zeros(2 * good.numel(), dtype=torch.int64, device=gpu)[::2]]
+    ops.hamming84_decode_into(cw, out, None, good)
+    for st in bad:
+        with pytest.raises(ValueError):
+            ops.hamming84_decode_into(cw, out, None, st)
+    g = ops.golay_encode_rows(torch.randint(0, 16, (64, 128), dtype=torch.uint8, device=gpu))
+    rows = torch.empty(64, 128, dtype=torch.uint8, device=gpu)
+    with pytest.raises(ValueError):
+        ops.golay_decode_rows_into(g, rows, stats=good[:16])
+    pk = g.reshape(-1).view(torch.uint8).view(-1, 4)[:, :3].contiguous().view(-1)
+    nib = torch.empty((3 * g.numel() + 1) // 2, dtype=torch.uint8, device=gpu)
+    with pytest.raises(ValueError):
+        ops.golay_decode_packed_into(pk, nib, m=g.numel(), stats=good[:16])
+    torch.cuda.synchronize()

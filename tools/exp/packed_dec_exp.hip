@@ -128,6 +128,13 @@ static const Variant kVariants[] = {
     {"pk_p50", pkdec_exp_kernel<0, false, 512, 50>, 512},
     {"pk_p90", pkdec_exp_kernel<0, false, 512, 90>, 512},
     {"pk_cfree_glds", pkdec_exp_kernel<1, true, 512, 75>, 512},
+    {"pk_p60", pkdec_exp_kernel<0, false, 512, 60>, 512},
+    {"pk_p65", pkdec_exp_kernel<0, false, 512, 65>, 512},
+    {"pk_p85", pkdec_exp_kernel<0, false, 512, 85>, 512},
+    {"pk_p40", pkdec_exp_kernel<0, false, 512, 40>, 512},
+    {"pk_b256_p50", pkdec_exp_kernel<0, false, 256, 50>, 256},
+    {"pk_b384", pkdec_exp_kernel<0, false, 384, 75>, 384},
+    {"pk_b384_p50", pkdec_exp_kernel<0, false, 384, 50>, 384},
 };
 
 }  // namespace exp

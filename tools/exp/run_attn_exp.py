@@ -1,0 +1,98 @@
+"""Paged attention: the product (kvecc_paged_attention) against the matrix-core
+kernels forced at G query heads per workgroup (tools/exp/attn_exp.hip,
+libattnx.so), [B=8, ctx 4096, D=128], fp16 queries, random cache bytes (the
+bench's worst case for the decode tables), MHA (32/32) and GQA (32q/8kv).
+Times: mean per call over ITERS back-to-back calls bracketed by events, after
+100 warm-up calls; outputs compared with the product's (max abs diff).
+
+usage: python tools/exp/run_attn_exp.py [codec ...]
+"""
+import ctypes
+import math
+import os
+import sys
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd"))
+import torch  # noqa: E402
+
+from kvecc import ops  # noqa: E402
+from kvecc.memory_layout import kv_cache_pair  # noqa: E402
+
+ITERS = int(os.environ.get("ITERS", "100"))
+B, CTX, D, BS = 8, 4096, 128, 16
+# (label, G, per_cu, fused)
+VARIANTS = [("mfma_g1_cu4", 1, 4, 1), ("mfma_g1_cu2", 1, 2, 1), ("mfma_g1_cu8", 1, 8, 1),
+            ("mfma_g1_cu4_nofuse", 1, 4, 0)]
+GQA_VARIANTS = [("mfma_g4_cu4", 4, 4, 0), ("mfma_g4_cu8", 4, 8, 0), ("mfma_g4_cu2", 4, 2, 0),
+                ("mfma_g2_cu4", 2, 4, 0)]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    lib = ctypes.CDLL(os.path.join(REPO, "tools", "exp", "libattnx.so"))
+    fn = lib.kvecc_exp_paged_attention_mfma
+    vp, i64, ci, f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
+    fn.argtypes = [ci, ci, ci] + [vp] * 9 + [i64] * 9 + [f32, ci, vp, vp]
+    codes = {"hamming84": 2, "golay": 3, "golay_packed": 4}
+    for codec in (sys.argv[1:] or ["hamming84", "golay_packed", "golay"]):
+        for heads, kvh, variants in ((32, 32, VARIANTS), (32, 8, GQA_VARIANTS)):
+            g = torch.Generator(device=dev).manual_seed(0)
+            nb = CTX // BS
+            blocks = B * nb
+            per = D if codec == "hamming84" else (D + 2) // 3
+            if codec == "golay_packed":
+                per = (3 * per + 3) // 4 * 4
+            kc, vc = kv_cache_pair((blocks, 1, kvh, BS * per), torch.int32 if codec == "golay" else torch.uint8, dev)
+            kc.random_(0, 1 << 24 if codec == "golay" else 256, generator=g)
+            vc.copy_(kc.roll(1, 0))
+            ks = torch.rand(blocks, 1, kvh, BS, device=dev, generator=g)
+            vs = torch.rand_like(ks)
+            table = torch.randperm(blocks, device=dev, generator=g).to(torch.int32).view(B, nb)
+            lens = torch.full((B,), CTX, dtype=torch.int32, device=dev)
+            q = torch.randn(B, heads, D, device=dev, generator=g).half()
+            ws = torch.empty(B * heads * 64 * (D + 2), dtype=torch.float32, device=dev)
+            ref = torch.empty_like(q)
+            out = torch.empty_like(q)
+            s = torch.cuda.current_stream().cuda_stream
+            sm = 1 / math.sqrt(D)
+
+            def prod():
+                ops.paged_attention_into(q, kc, vc, table, lens, ks, vs, ref, 0, BS, sm, codec, CTX)
+
+            def var(G, per_cu, fused):
+                def run():
+                    rc = fn(G, per_cu, fused, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), table.data_ptr(),
+                            lens.data_ptr(), ks.data_ptr(), vs.data_ptr(), out.data_ptr(), B, heads, kvh, D,
+                            blocks, 1, 0, BS, nb, CTX, sm, codes[codec], ws.data_ptr(), s)
+                    assert rc == 0
+                return run
+
+            runs = [("product", prod)] + [(lab, var(G, pc, fu)) for lab, G, pc, fu in variants]
+            res = {}
+            for _ in range(2):  # two interleaved passes, the second reported
+                for lab, run in runs:
+                    for _ in range(100):
+                        run()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(ITERS):
+                        run()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    res[lab] = e0.elapsed_time(e1) * 1e3 / ITERS
+            prod()
+            torch.cuda.synchronize()
+            for lab, run in runs:
+                diff = 0.0
+                if lab != "product":
+                    run()
+                    torch.cuda.synchronize()
+                    diff = float((out.float() - ref.float()).abs().max())
+                print(f"{codec:13s} {heads}q/{kvh}kv {lab:20s} {res[lab]:7.2f} us/call  maxdiff {diff:.3g}",
+                      flush=True)
+            del kc, vc, ws
+
+
+if __name__ == "__main__":
+    main()
