@@ -841,17 +841,35 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), pad, st, a);
 }
 
+// workgroups of `kern` resident per CU at `block` threads (registers, LDS),
+// at most `cap`: a persistent grid larger than what is resident runs its
+// excess after the first workgroups finish (the fp32-output interpolating read
+// takes 131 VGPRs: one 512-thread workgroup per CU, not kShimTilePerCu)
+static int resident_per_cu(const void *kern, int block, size_t lds, int cap) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, block, lds) != hipSuccess || n < 1) return cap;
+  return std::min(n, cap);
+}
+
+template <typename TO, int CODEC, bool INTERP, bool STATS>
+static void launch_bytes_tiles_k(const ShimTileArgs &a, hipStream_t st) {
+  constexpr int kChunk = INTERP ? 0 : 1;  // interpolation: persistent; plain: full grid, one tile per wave
+  const auto kern = shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, STATS, kChunk>;
+  const unsigned pad = kChunk ? kShimBytesLdsPad : 0u;  // caps the workgroups per CU
+  unsigned grid = tile_grid(a.units, kChunk);
+  if (!kChunk) {
+    static const int per_cu = resident_per_cu(reinterpret_cast<const void *>(kern), kTileBlock, pad, kShimTilePerCu);
+    grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * per_cu);
+  }
+  KVECC_LAUNCH(kern, dim3(grid), dim3(kTileBlock), pad, st, a);
+}
+
 template <typename TO, int CODEC, bool INTERP>
 static void launch_bytes_tiles_s(const ShimTileArgs &a, hipStream_t st) {
-  constexpr int kChunk = INTERP ? 0 : 1;  // interpolation: persistent; plain: full grid, one tile per wave
-  const unsigned grid = tile_grid(a.units, kChunk);
-  const unsigned pad = kChunk ? kShimBytesLdsPad : 0u;  // caps the workgroups per CU
   if (a.stats)
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, true, kChunk>), dim3(grid), dim3(kTileBlock), pad,
-                 st, a);
+    launch_bytes_tiles_k<TO, CODEC, INTERP, true>(a, st);
   else
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, false, kChunk>), dim3(grid), dim3(kTileBlock), pad,
-                 st, a);
+    launch_bytes_tiles_k<TO, CODEC, INTERP, false>(a, st);
 }
 
 template <typename TO>

@@ -135,7 +135,9 @@ def test_paged_attention_cache_past_4g(gpu, codec):
     """Caches over 4 GiB take the 64-bit-addressed attention kernels (smaller
     ones use 32-bit buffer offsets).  The sequence's blocks sit past the 4 GiB
     mark; the result must equal the same blocks copied into a small cache,
-    which runs the buffer-load kernels (~9 GB of HBM)."""
+    which runs the buffer-load kernels (~9 GB of HBM).  Hamming(8,4) uses fp32
+    queries: fp16 MHA queries would send the small cache to the matrix-core
+    kernel (different summation order), fp32 keeps both on the same kernel."""
     import math
     from kvecc import ops
     heads, d, bs, ctx, batch = 8, 128, 16, 1000, 2
@@ -163,7 +165,8 @@ def test_paged_attention_cache_past_4g(gpu, codec):
     vs_big[used] = vs_small
     perm = torch.randperm(batch * nb, device=gpu, generator=g).to(torch.int32).view(batch, nb)
     lens = torch.tensor([ctx, ctx - 37], dtype=torch.int32, device=gpu)
-    q = torch.randn(batch, heads, d, device=gpu, generator=g).half()
+    q = torch.randn(batch, heads, d, device=gpu, generator=g)
+    q = q if codec == "hamming84" else q.half()
     outs = []
     for kc, vc, ks, vs, table in ((big_k, big_v, ks_big, vs_big, perm + (num_blocks - batch * nb)),
                                   (small_k, small_v, ks_small, vs_small, perm)):

@@ -1,0 +1,311 @@
+// bytes_read_exp.hip -- experimental variants of the fused Hamming(8,4) read
+// (csrc/shim.hip shim_read_bytes_tiles_kernel), NOT shipped: this file
+// #includes shim.hip for its tile helpers; tools/exp/run_bytes_read_exp.py
+// times them against the product (kvecc_shim_read_batch) in one process.
+//
+// kvecc_exp_bytes_read: the product kernel at other work distributions (CHUNK
+// tiles per wave on a full grid, or the persistent grid at other per-CU
+// counts; `lds_pad` bytes of dynamic LDS cap the workgroups per CU).
+//
+// kvecc_exp_bytes_read_ip: the interpolating read (fp16 out, statistics on,
+// persistent grid + dynamic tail) rewritten with
+//   TBL3   the tile's block-table entry and its two neighbour rows' entries
+//          loaded together (one scalar round trip before the tile's loads
+//          issue; the product waits for the tile's entry, issues the tile,
+//          then waits again for the neighbours')
+//   HBUF   the neighbour rows by two buffer loads (uniform descriptors) instead
+//          of a 64-bit-addressed global load
+//   WPE    amdgpu_waves_per_eu minimum (register budget; 1 = none)
+//   DC     the head size as a compile-time constant (0: runtime, the product)
+//   ORDER  1: tiles heads fastest (golay_read_exp.hip tile_at)
+#include "../../quantized-kv-cache-ecc-protection_amd/csrc/shim.hip"
+
+namespace kvecc {
+namespace exp {
+
+template <bool INTERP, int CHUNK>
+static void launch_bytes_exp(const ShimTileArgs &a, unsigned lds_pad, int per_cu, hipStream_t st) {
+  const unsigned grid = CHUNK ? (unsigned)cdiv(cdiv(a.units, CHUNK), kTileWaves)
+                              : (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * per_cu);
+  KVECC_LAUNCH((shim_read_bytes_tiles_kernel<__half, KVECC_CODEC_H84, INTERP, true, CHUNK>), dim3(grid),
+               dim3(kTileBlock), lds_pad, st, a);
+}
+
+template <bool TBL3, bool HBUF, int WPE, int DC = 0, int ORDER = 0>
+__global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void bytes_read_ip_kernel(
+    ShimTileArgs a) {
+  using TO = __half;
+  const uint32_t kd = DC ? (uint32_t)DC : a.d;  // DC: the head size as a compile-time constant
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ float scale_all[kTileWaves][kWave];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  uint8_t *stage = stage_all[wave];
+  const uint32_t nwaves = gridDim.x * kTileWaves;
+  const uint32_t cpr = kd / 16;
+  const uint32_t items = a.tr * cpr;
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
+  uint32_t i2r[NI2], i2c[NI2];
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    ir[i] = f / cpr;
+    ic[i] = f - ir[i] * cpr;
+  }
+#pragma unroll
+  for (int i = 0; i < NI2; ++i) {
+    const uint32_t f = lane + kWave * i;
+    i2r[i] = f / (cpr * 16 / V);
+    i2c[i] = f - i2r[i] * (cpr * 16 / V);
+  }
+  uint32_t n1 = 0, n2 = 0;
+  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  uint32_t u = gw;
+  if (u >= a.units) return;
+  TileSchedule sched;
+  sched.init(a.units, a.dyn, gw, nwaves, lane, kShimReadStaticPct);
+
+  ShimTile cur;
+  u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
+  float scale;
+  bool has_hw = false;
+  auto fetch = [&](uint32_t uu) {
+    // the tile (shim_tile) and its neighbour rows' positions
+    const uint32_t per_side = a.units / 2;
+    const uint32_t side = uu >= per_side ? 1u : 0u;
+    uint32_t v = uu - side * per_side;
+    uint32_t ch, lb, bh, b, h;
+    if (ORDER == 0) {
+      ch = v % a.tpb;
+      v /= a.tpb;
+      lb = v % a.nlb;
+      bh = v / a.nlb;
+      b = bh / a.hkv;
+      h = bh - b * a.hkv;
+    } else {  // heads fastest
+      h = v % a.hkv;
+      v /= a.hkv;
+      ch = v % a.tpb;
+      v /= a.tpb;
+      lb = v % a.nlb;
+      b = v / a.nlb;
+      bh = b * a.hkv + h;
+    }
+    cur.side = side;
+    cur.bh = bh;
+    cur.pos0 = lb * a.bs + ch * a.tr;
+    cur.rows = cur.pos0 < a.ctx ? min(min(a.tr, a.bs - ch * a.tr), a.ctx - cur.pos0) : 0u;
+    const uint32_t pa = cur.pos0 > 0 ? cur.pos0 - 1 : 0u, pb = min(cur.pos0 + cur.rows, a.ctx - 1);
+    const int32_t *trow = a.table + (int64_t)b * a.tstride;
+    int32_t blk, ba = -1, bb = -1;
+    if (TBL3) {
+      blk = ld_scalar(trow + lb);
+      ba = ld_scalar(trow + pa / a.bs);
+      bb = ld_scalar(trow + pb / a.bs);
+    } else {
+      blk = ld_scalar(trow + lb);
+    }
+    cur.row0 = blk < 0 ? -1 : (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + ch * a.tr;
+    const bool live = cur.row0 >= 0;
+    const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + (live ? cur.row0 : 0) * (int64_t)kd);
+    const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + (live ? cur.row0 : 0)));
+    const uint32_t nrows = uni(live ? cur.rows : 0u);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * kd), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ss =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+    scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * kd + 16 * ic[i], 0, 2));
+    }
+    has_hw = cur.rows > 0;
+    if (!has_hw) return;
+    if (!TBL3) {
+      ba = ld_scalar(trow + pa / a.bs);
+      bb = ld_scalar(trow + pb / a.bs);
+    }
+    const int64_t rowa = (((int64_t)ba * a.layers + a.layer) * a.hkv + h) * a.bs + (pa - pa / a.bs * a.bs);
+    const int64_t rowb = (((int64_t)bb * a.layers + a.layer) * a.hkv + h) * a.bs + (pb - pb / a.bs * a.bs);
+    const bool below = lane >= cpr;
+    if (HBUF) {
+      const char *c = reinterpret_cast<const char *>(a.cache[side]);
+      const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char *>(uni(c + (ba >= 0 ? rowa : 0) * (int64_t)kd)), 0, ba >= 0 ? (int)kd : 0, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char *>(uni(c + (bb >= 0 ? rowb : 0) * (int64_t)kd)), 0, bb >= 0 ? (int)kd : 0, 0x00020000);
+      hw = u32x4{0u, 0u, 0u, 0u};
+      if (!below)
+        hw = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, 16 * lane, 0, 2));
+      else if (lane < 2 * cpr)
+        hw = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, 16 * (lane - cpr), 0, 2));
+    } else {
+      const int32_t bl = below ? bb : ba;
+      hw = u32x4{0u, 0u, 0u, 0u};
+      if (lane < 2 * cpr && bl >= 0)
+        hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[side]) +
+                                                       (below ? rowb : rowa) * kd) +
+                       (below ? lane - cpr : lane));
+    }
+  };
+  auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
+    uint32_t q = cw, t = 0, s1 = 0, s2 = 0;
+    h84_decode4(cw, q, t, s1, s2);
+    if (count) {
+      n1 += s1;
+      n2 += s2;
+      dbl |= s2;
+    }
+    return q | t << 4;
+  };
+  fetch(u);
+  for (;;) {
+    const uint32_t off0 = kd;
+    scale_all[wave][lane] = scale;
+    bool dbl_any = false;
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;
+      const bool real = ir[i] < cur.rows;
+      uint32_t dbl = 0;
+      const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
+                     dec(w[i].w, real, dbl)};
+      dbl_any |= dbl != 0;
+      if (ir[i] < cur.rows) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * kd + 16 * ic[i]) = d4;
+    }
+    const bool tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+    if (has_hw && lane < 2 * cpr) {
+      uint32_t none = 0;
+      const u32x4 d4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none),
+                     dec(hw.w, false, none)};
+      const uint32_t r = lane >= cpr ? cur.rows + 1 : 0u;
+      *reinterpret_cast<u32x4 *>(stage + r * kd + 16 * (lane >= cpr ? lane - cpr : lane)) = d4;
+    }
+    wave_lds_sync();
+    const ShimTile t = cur;
+    u = sched.next(u, lane);
+    const bool more = u < a.units;
+    if (more) fetch(u);
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
+    auto phase2 = [&](auto interp_c) {
+      constexpr bool IP = decltype(interp_c)::value;
+#pragma unroll
+      for (int i = 0; i < NI2; ++i) {
+        if (i * kWave >= (int)(items * 16 / V)) break;
+        const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
+        const uint8_t *row = stage + off0 + r * kd + V * c;
+        uint32_t q[2] = {0u, 0u};
+#pragma unroll
+        for (int k = 0; k < V / 4; ++k) {
+          const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+          if (IP) {
+            const uint32_t up = reinterpret_cast<const uint32_t *>(row - kd)[k];
+            const uint32_t dn = reinterpret_cast<const uint32_t *>(row + kd)[k];
+            q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+          } else {
+            q[k] = v & 0x0F0F0F0Fu;
+          }
+        }
+        tile_store(os, (i2r[i] * kd + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+      }
+    };
+    if (tile_dbl)
+      phase2(std::integral_constant<bool, true>{});
+    else
+      phase2(std::integral_constant<bool, false>{});
+    if (!more) break;
+    wave_lds_sync();
+  }
+  n1 = wave_sum(n1);
+  n2 = wave_sum(n2);
+  if (lane == 0) {
+    uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+    if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
+  }
+}
+
+struct IpVariant {
+  const char *name;
+  void (*kern)(ShimTileArgs);
+};
+static const IpVariant kIpVariants[] = {
+    {"ip", bytes_read_ip_kernel<false, false, 1>},      {"ip_tbl3", bytes_read_ip_kernel<true, false, 1>},
+    {"ip_hbuf", bytes_read_ip_kernel<false, true, 1>},  {"ip_tbl3_hbuf", bytes_read_ip_kernel<true, true, 1>},
+    {"ip_w6", bytes_read_ip_kernel<false, false, 6>},   {"ip_tbl3_hbuf_w6", bytes_read_ip_kernel<true, true, 6>},
+    {"ip_d128", bytes_read_ip_kernel<false, false, 1, 128>},
+    {"ip_tbl3_d128", bytes_read_ip_kernel<true, false, 1, 128>},
+    {"ip_tbl3_hbuf_d128", bytes_read_ip_kernel<true, true, 1, 128>},
+    {"ip_tbl3_d128_w6", bytes_read_ip_kernel<true, false, 6, 128>},
+    {"ip_hm", bytes_read_ip_kernel<false, false, 1, 0, 1>},
+    {"ip_tbl3_hm", bytes_read_ip_kernel<true, false, 1, 0, 1>},
+};
+
+static ShimTileArgs bytes_args(int interp, const void *k_cache, const void *v_cache, const float *k_scales,
+                               const float *v_scales, const int32_t *table, int64_t tstride, int64_t batch,
+                               int64_t ctx, int64_t hkv, int64_t d, int64_t block_size, void *k_out, void *v_out,
+                               uint64_t *stats, void *stream) {
+  ShimTileArgs a{};
+  a.cache[0] = k_cache;
+  a.cache[1] = v_cache;
+  a.scales[0] = k_scales;
+  a.scales[1] = v_scales;
+  a.out[0] = k_out;
+  a.out[1] = v_out;
+  a.table = table;
+  a.stats = stats;
+  a.tstride = (uint32_t)tstride;
+  a.hkv = (uint32_t)hkv;
+  a.d = a.g = a.lr = a.rowb = (uint32_t)d;
+  a.layers = 1;
+  a.bs = (uint32_t)block_size;
+  a.layer = 0;
+  a.ctx = (uint32_t)ctx;
+  const int64_t cpr = d / 16;
+  a.tr = (uint32_t)std::min<int64_t>({block_size, (int64_t)kTileStage / d - (interp ? 2 : 0), (int64_t)kWave,
+                                      (int64_t)kWave * kByteTileItems / cpr});
+  a.tpb = (uint32_t)cdiv(block_size, a.tr);
+  a.nlb = (uint32_t)cdiv(ctx, block_size);
+  a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+  a.dyn = shim_dyn_slot(stream);
+  return a;
+}
+
+}  // namespace exp
+}  // namespace kvecc
+
+#define EXP_API extern "C" __attribute__((visibility("default")))
+#define BYTES_PARAMS                                                                                              \
+  const void *k_cache, const void *v_cache, const float *k_scales, const float *v_scales, const int32_t *table, \
+      int64_t tstride, int64_t batch, int64_t ctx, int64_t hkv, int64_t d, int64_t block_size, void *k_out,       \
+      void *v_out, uint64_t *stats, void *stream
+
+EXP_API int kvecc_exp_bytes_read(int interp, int chunk, int per_cu, int lds_pad, BYTES_PARAMS) {
+  using namespace kvecc;
+  const ShimTileArgs a = exp::bytes_args(interp, k_cache, v_cache, k_scales, v_scales, table, tstride, batch, ctx,
+                                         hkv, d, block_size, k_out, v_out, stats, stream);
+  hipStream_t st = as_stream(stream);
+  const unsigned pad = (unsigned)lds_pad;
+#define BX(I, C) \
+  if (interp == I && chunk == C) exp::launch_bytes_exp<I, C>(a, pad, per_cu, st);
+  BX(0, 0) BX(0, 1) BX(0, 2) BX(0, 4) BX(1, 0) BX(1, 1) BX(1, 2) BX(1, 4) BX(1, 8)
+#undef BX
+  return check_launch("exp_bytes_read");
+}
+
+EXP_API int kvecc_exp_bytes_ip_count(void) {
+  return (int)(sizeof(kvecc::exp::kIpVariants) / sizeof(kvecc::exp::kIpVariants[0]));
+}
+EXP_API const char *kvecc_exp_bytes_ip_name(int v) { return kvecc::exp::kIpVariants[v].name; }
+
+EXP_API int kvecc_exp_bytes_read_ip(int v, int per_cu, BYTES_PARAMS) {
+  using namespace kvecc;
+  const ShimTileArgs a = exp::bytes_args(1, k_cache, v_cache, k_scales, v_scales, table, tstride, batch, ctx, hkv,
+                                         d, block_size, k_out, v_out, stats, stream);
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * per_cu);
+  KVECC_LAUNCH(exp::kIpVariants[v].kern, dim3(grid), dim3(kTileBlock), 0, as_stream(stream), a);
+  return check_launch("exp_bytes_read_ip");
+}

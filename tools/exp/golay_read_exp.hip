@@ -23,7 +23,34 @@
 namespace kvecc {
 namespace exp {
 
-template <int SCHED, int CHUNK, int STAGE, int GATHER, int SPLITP, int PAD, int BLOCK, bool PACKED, int PCT = 65>
+// ORDER 1: tile u -> (side, b, lb, ch, h), heads fastest: the waves of one
+// window read whole physical blocks (all heads of a block are contiguous in
+// the cache) instead of one head's 2.75 KB slice of randomly placed blocks;
+// the outputs (one 4 KiB [pos, d] tile per wave) land 1 MiB apart instead of
+// contiguous.  0: the product's order (shim_tile), lb fastest.
+template <int ORDER>
+__device__ __forceinline__ ShimTile tile_at(const ShimTileArgs &a, uint32_t u) {
+  if (ORDER == 0) return shim_tile(a, u);
+  ShimTile t;
+  const uint32_t per_side = a.units / 2;
+  t.side = u >= per_side ? 1u : 0u;
+  u -= t.side * per_side;
+  const uint32_t h = u % a.hkv;
+  u /= a.hkv;
+  const uint32_t ch = u % a.tpb;
+  u /= a.tpb;
+  const uint32_t lb = u % a.nlb;
+  const uint32_t b = u / a.nlb;
+  t.bh = b * a.hkv + h;
+  t.pos0 = lb * a.bs + ch * a.tr;
+  t.rows = t.pos0 < a.ctx ? min(min(a.tr, a.bs - ch * a.tr), a.ctx - t.pos0) : 0u;
+  const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + lb);
+  t.row0 = blk < 0 ? -1 : (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + ch * a.tr;
+  return t;
+}
+
+template <int SCHED, int CHUNK, int STAGE, int GATHER, int SPLITP, int PAD, int BLOCK, bool PACKED, int PCT = 65,
+          int ORDER = 0>
 __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, const uint16_t *par16,
                                                                const uint16_t *cor16) {
   using TO = __half;
@@ -107,14 +134,14 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
     __syncthreads();
     if (!active) return;
     if (SCHED == 0) sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
-    cur = shim_tile(a, u);
+    cur = tile_at<ORDER>(a, u);
     tile_issue<PACKED>(a, cur, lane, it, w, scale);
   } else {
     // the first tile's loads go out before the tables (a full grid has no
     // inactive waves; a persistent one may: they still help stage)
     if (active) {
       if (SCHED == 0) sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
-      cur = shim_tile(a, u);
+      cur = tile_at<ORDER>(a, u);
       tile_issue<PACKED>(a, cur, lane, it, w, scale);
     }
     stage_tables();
@@ -185,7 +212,7 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
     u = SCHED == 0 ? sched.next(u, lane) : u + 1;
     const bool more = u < uend;
     if (more) {
-      cur = shim_tile(a, u);
+      cur = tile_at<ORDER>(a, u);
       tile_issue<PACKED>(a, cur, lane, it, w, scale);
     }
     const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
@@ -400,6 +427,12 @@ static const Variant kVariants[] = {
     GV("full1_splitp_s0_b256", 1, 1, 0, 0, 1, 0, 256, false),
     GV("pk_full1_u16", 1, 1, 0, 4, 0, 0, 512, true),
     GV("pk_full1_splitp_s0", 1, 1, 0, 0, 1, 0, 512, true),
+    // heads-fastest tile order
+    {"pers_hm", golay_read_exp_kernel<0, 1, 0, 0, 0, 0, 512, false, 65, 1>, 0, 1, 512},
+    {"pers_hm_p50", golay_read_exp_kernel<0, 1, 0, 0, 0, 0, 512, false, 50, 1>, 0, 1, 512},
+    {"full1_u16_hm", golay_read_exp_kernel<1, 1, 0, 4, 0, 0, 512, false, 65, 1>, 1, 1, 512},
+    {"full2_u16_hm", golay_read_exp_kernel<1, 2, 0, 4, 0, 0, 512, false, 65, 1>, 1, 2, 512},
+    {"pk_pers_hm", golay_read_exp_kernel<0, 1, 0, 0, 0, 0, 512, true, 65, 1>, 0, 1, 512},
     {"pf2", golay_read_pf2_kernel<512, false, 65>, 0, 1, 512},
     {"pf2_b256", golay_read_pf2_kernel<256, false, 65>, 0, 1, 256},
     {"pf2_p50", golay_read_pf2_kernel<512, false, 50>, 0, 1, 512},
