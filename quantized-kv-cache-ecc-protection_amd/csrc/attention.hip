@@ -60,8 +60,11 @@ constexpr int kH84Vec = 4, kGolayVec = 3;
 // unchanged (tools/exp/run_attn.py).  Larger caches take 64-bit addressing.
 constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data format
 // Packed Golay caches (KVECC_CODEC_GOLAY_PACKED, 3-byte codewords): a lane owns
-// 4 codewords = 12 bytes = 3 aligned dwords of its token row
-constexpr int kGolayPackedVec = 4;
+// 3 codewords = 9 bytes of its token row, loaded as the 3 aligned dwords that
+// hold them and realigned (v_alignbyte): 43 codewords -> 15 of 16 lanes busy.
+// 4 codewords per lane (12 bytes, 3 aligned dwords, no realignment) left 5 of
+// 16 lanes idle: 68.0 vs 62.8 us per MHA call (profiles/r04/attn/packed_vec_ab.log)
+constexpr int kGolayPackedVec = 3;
 // Golay decodes through the spread tables (golay_attn_table_dev: 32-bit entries,
 // nibbles one per byte): per codeword 2 LDS reads + 9 VALU ops (address math,
 // one masked xor, three v_cvt_f32_ubyteN) instead of ~13 through the 16-bit
@@ -126,11 +129,17 @@ struct Chunk {
         for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0);
       }
     } else if constexpr (CODEC == KVECC_CODEC_GOLAY_PACKED) {
-      static_assert(CODEC != KVECC_CODEC_GOLAY_PACKED || VEC == 4, "packed lanes own 4 codewords");
+      static_assert(CODEC != KVECC_CODEC_GOLAY_PACKED || VEC == 4 || VEC == 3, "packed lanes own 3 or 4 codewords");
       // past the row's end: a neighbour row's bytes (masked by q = 0) or 0
-      const uint32_t off = (uint32_t)row * a.rowb + 12u * c;
-      const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
-      unpack3(v[0], v[1], v[2]);
+      if constexpr (VEC == 4) {
+        const uint32_t off = (uint32_t)row * a.rowb + 12u * c;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+        unpack3(v[0], v[1], v[2]);
+      } else {  // 9 bytes at 9c: the 3 dwords holding them, realigned
+        const uint32_t off = (uint32_t)row * a.rowb + 9u * c;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off & ~3u, 0, 0);
+        unpack9(v[0], v[1], v[2], off & 3u);
+      }
     } else {
       const uint32_t off = ((uint32_t)row * (uint32_t)a.g + VEC * c) * 4u;
 #pragma unroll
@@ -156,7 +165,12 @@ struct Chunk {
     } else if constexpr (CODEC == KVECC_CODEC_GOLAY_PACKED) {
       const uint32_t *p = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(cache) + row * a.rowb);
       const int last = (int)(a.rowb / 4) - 1;  // clamp inside the row
-      unpack3(p[min(3 * c, last)], p[min(3 * c + 1, last)], p[min(3 * c + 2, last)]);
+      if constexpr (VEC == 4) {
+        unpack3(p[min(3 * c, last)], p[min(3 * c + 1, last)], p[min(3 * c + 2, last)]);
+      } else {
+        const int w0 = 9 * c / 4;
+        unpack9(p[min(w0, last)], p[min(w0 + 1, last)], p[min(w0 + 2, last)], (uint32_t)(9 * c) & 3u);
+      }
     } else {
       const int32_t *p = reinterpret_cast<const int32_t *>(cache) + row * a.g;
 #pragma unroll
@@ -169,6 +183,14 @@ struct Chunk {
     w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbyte(d1, d0, 3);
     w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbyte(d2, d1, 2);
     w[3 < VEC ? 3 : 0] = d2 >> 8;
+  }
+  // 3 little-endian 3-byte codewords starting at byte `sh` (0-3) of 3 dwords
+  __device__ __forceinline__ void unpack9(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t sh) {
+    const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh), x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t x2 = d2 >> (8 * sh);
+    w[0] = x0;
+    w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbyte(x1, x0, 3);
+    w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbyte(x2, x1, 2);
   }
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
@@ -374,14 +396,19 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
 // loaded and decoded once and used G times (a dot product, an online softmax
 // state and an accumulator per head), where one workgroup per query head read
 // and decoded every cache row H/Hkv times.
-template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1>
+template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1, int UR = 0>
 __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
   // cache row of each token of the split (-1 = no block / past the split),
   // padded so the unrolled loop reads it without bounds checks
-  constexpr int U = CODEC == KVECC_CODEC_GOLAY ? kGolayUnroll : CODEC == KVECC_CODEC_H84 ? kH84Unroll : kUnroll;
+  // (UR > 0: another count, for the experiment forks)
+  constexpr int U = UR > 0                        ? UR
+                    : CODEC == KVECC_CODEC_GOLAY ? kGolayUnroll
+                    : CODEC == KVECC_CODEC_H84   ? kH84Unroll
+                                                 : kUnroll;
+  static_assert(U <= kMaxUnroll, "rows in flight");
   __shared__ int32_t rows[kMaxSplit + (kMaxUnroll - 1) * kBlock];
   // Golay tables copied from the device: the 32 KiB spread tables, or
   // parity[4096] then correct[4096] as uint16 (16 KiB).  With the spread
@@ -1290,7 +1317,7 @@ static int attn_heads_per_wg(int codec, int64_t d, int64_t g, int64_t heads, int
   const int vec = attn_vec(codec, d, true);
   const int w = pow2_at_least((g + vec - 1) / vec);
   if (!buf || w < 8 || w > 32 || (codec == KVECC_CODEC_H84 && d % 8 != 0)) return 1;
-  const int gmax = codec == KVECC_CODEC_GOLAY_PACKED ? 2 : 4;  // packed: 4 codewords per lane
+  const int gmax = codec == KVECC_CODEC_GOLAY_PACKED ? 2 : 4;  // packed: G = 2 (the realigned loads' registers)
   return group % 4 == 0 && gmax >= 4 ? 4 : group % 2 == 0 ? 2 : 1;
 }
 
@@ -1327,7 +1354,7 @@ static int launch_attn(const AttnArgs &a, int64_t batch, int gq, hipStream_t st)
   } else if constexpr (CODEC == KVECC_CODEC_GOLAY) {
     rc = launch_split_g<T, CODEC, kGolayVec>(a, batch, gq, st);  // 3 codewords per lane: 43 -> 15 of 16 lanes
   } else {
-    rc = launch_split_g<T, CODEC, kGolayPackedVec>(a, batch, gq, st);  // 4 codewords per lane: 43 -> 11 of 16
+    rc = launch_split_g<T, CODEC, kGolayPackedVec>(a, batch, gq, st);  // 3 codewords per lane: 43 -> 15 of 16
   }
   if (rc != KVECC_OK) return rc;
   if (!a.ctr) launch_combine<T>(a, batch, st);

@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--bs", type=int, default=16)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=100,
-                    help="untimed calls first (a few ms of work: clocks ramp up on a cold GPU)")
+                    help="untimed calls first, repeated until --warmup-s seconds have passed")
+    ap.add_argument("--warmup-s", type=float, default=0.5,
+                    help="minimum warm-up time: the clocks take a few hundred ms to ramp on an idle GPU "
+                         "(100 calls = 7 ms read 10-15 %% slow)")
+    ap.add_argument("--passes", type=int, default=5, help="timed passes of --iters calls; the median is reported")
     args = ap.parse_args()
     from kvecc import ops
     dev = torch.device("cuda:0")
@@ -54,16 +58,25 @@ def main():
     out = torch.empty_like(q)
     call = lambda: ops.paged_attention_into(q, kc, vc, table, lens, ks, vs, out, 0, args.bs,  # noqa
                                             1 / math.sqrt(args.d), args.codec, args.ctx)
-    for _ in range(args.warmup):
-        call()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record()
-    for _ in range(args.iters):
-        call()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / args.iters
+    import statistics
+    import time
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(args.warmup):
+            call()
+        torch.cuda.synchronize()
+        if time.perf_counter() - t0 >= args.warmup_s:
+            break
+    passes = []
+    for _ in range(args.passes):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        passes.append(e0.elapsed_time(e1) / args.iters)
+    ms = statistics.median(passes)
     tokens = args.batch * args.ctx
     cw_bytes = 2 * tokens * args.kv_heads * per * kc.element_size()
     bytes_ = cw_bytes + 2 * tokens * args.kv_heads * 4 + table.numel() * 4
@@ -71,6 +84,7 @@ def main():
     print(json.dumps({"kernel": "paged_attention", "codec": args.codec, "batch": args.batch,
                       "heads": args.heads, "kv_heads": args.kv_heads, "head_dim": args.d,
                       "ctx": args.ctx, "ms_per_call": ms, "bytes_per_call": bytes_,
+                      "pass_ms": [round(x, 5) for x in passes],
                       "achieved_gbs": gbs, "hbm_frac": gbs / 8000.0,
                       "includes": "split kernel + combine kernel + workspace alloc"}))
 

@@ -3,6 +3,9 @@
 // does not: the matrix-core kernels for one query head per cache head (MHA,
 // G = 1: one of the 16 MFMA columns used), with other split sizes.
 // tools/exp/run_attn_exp.py times them against kvecc_paged_attention.
+// kvecc_exp_paged_attention_packed: the packed-Golay MHA split kernel with VEC
+// codewords per lane (the product: 4, 11 of 16 lanes busy at D = 128; 3: 15 of 16,
+// 9-byte unaligned lane chunks realigned with v_alignbyte).
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/attention.hip"
 
 namespace kvecc {
@@ -79,6 +82,60 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_mfma(
     default: exp::launch_mfma_g<4>(codec, a, batch, st); break;
   }
   return check_launch("exp_paged_attention_mfma");
+}
+
+// packed Golay, fp16 queries, G = 1, fused combine; vec 3 or 4 (32 / 33: 3 with 2 / 3 rows in flight)
+__attribute__((visibility("default"))) int kvecc_exp_paged_attention_packed(
+    int vec, int per_cu, const void *query, const void *k_cache, const void *v_cache, const int32_t *block_table,
+    const int32_t *context_lens, const float *k_scales, const float *v_scales, void *out, int64_t batch,
+    int64_t heads, int64_t kv_heads, int64_t head_dim, int64_t num_blocks, int64_t block_size, int64_t max_blocks,
+    int64_t max_context_len, float sm_scale, float *workspace, void *stream) {
+  using namespace kvecc;
+  AttnArgs a;
+  a.q = query;
+  a.k_cache = k_cache;
+  a.v_cache = v_cache;
+  a.table = block_table;
+  a.ctx_lens = context_lens;
+  a.k_scales = k_scales;
+  a.v_scales = v_scales;
+  a.ws = workspace;
+  a.out = out;
+  a.heads = heads;
+  a.kv_heads = kv_heads;
+  a.d = head_dim;
+  a.g = (head_dim + 2) / 3;
+  a.rowb = (uint32_t)KVECC_GOLAY_PACKED_ROW(a.g);
+  a.layers = 1;
+  a.layer = 0;
+  a.bs = block_size;
+  a.max_blocks = max_blocks;
+  a.sm_scale = sm_scale;
+  a.empty_value = 0.0f;
+  const int64_t rows_total = num_blocks * kv_heads * block_size;
+  a.cache_bytes = (uint32_t)(rows_total * a.rowb);
+  a.scale_bytes = (uint32_t)(rows_total * 4);
+  a.split = choose_split(batch * heads, max_context_len, per_cu);
+  a.nsplit = cdiv(max_context_len, a.split);
+  a.ctr = attn_counter_slot(stream);
+  a.par = golay_parity_table_dev();
+  a.cor = golay_correct_table_dev();
+  a.atab = golay_attn_table_dev();
+  const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * heads));
+  hipStream_t st = as_stream(stream);
+  if (vec == 3)
+    KVECC_LAUNCH((paged_attn_split_kernel<__half, KVECC_CODEC_GOLAY_PACKED, 3, 16, true, 1>), grid, dim3(kBlock), 0,
+                 st, a);
+  else if (vec == 32)  // 3 codewords per lane, 2 rows in flight
+    KVECC_LAUNCH((paged_attn_split_kernel<__half, KVECC_CODEC_GOLAY_PACKED, 3, 16, true, 1, 2>), grid, dim3(kBlock),
+                 0, st, a);
+  else if (vec == 33)  // 3 codewords per lane, 3 rows in flight
+    KVECC_LAUNCH((paged_attn_split_kernel<__half, KVECC_CODEC_GOLAY_PACKED, 3, 16, true, 1, 3>), grid, dim3(kBlock),
+                 0, st, a);
+  else
+    KVECC_LAUNCH((paged_attn_split_kernel<__half, KVECC_CODEC_GOLAY_PACKED, 4, 16, true, 1>), grid, dim3(kBlock), 0,
+                 st, a);
+  return check_launch("exp_paged_attention_packed");
 }
 
 }  // extern "C"

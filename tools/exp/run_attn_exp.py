@@ -6,6 +6,7 @@ Times: mean per call over ITERS back-to-back calls bracketed by events, after
 100 warm-up calls; outputs compared with the product's (max abs diff).
 
 usage: python tools/exp/run_attn_exp.py [codec ...]
+       python tools/exp/run_attn_exp.py packed_vec   (packed Golay MHA, 3 vs 4 codewords per lane)
 """
 import ctypes
 import math
@@ -35,6 +36,10 @@ def main():
     vp, i64, ci, f32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float
     fn.argtypes = [ci, ci, ci] + [vp] * 9 + [i64] * 9 + [f32, ci, vp, vp]
     codes = {"hamming84": 2, "golay": 3, "golay_packed": 4}
+    pk = lib.kvecc_exp_paged_attention_packed
+    pk.argtypes = [ci, ci] + [vp] * 8 + [i64] * 8 + [f32, vp, vp]
+    if sys.argv[1:] == ["packed_vec"]:
+        return packed_vec(dev, pk)
     for codec in (sys.argv[1:] or ["hamming84", "golay_packed", "golay"]):
         for heads, kvh, variants in ((32, 32, VARIANTS), (32, 8, GQA_VARIANTS)):
             g = torch.Generator(device=dev).manual_seed(0)
@@ -92,6 +97,63 @@ def main():
                 print(f"{codec:13s} {heads}q/{kvh}kv {lab:20s} {res[lab]:7.2f} us/call  maxdiff {diff:.3g}",
                       flush=True)
             del kc, vc, ws
+
+
+def packed_vec(dev, pk):
+    heads = kvh = 32
+    g = torch.Generator(device=dev).manual_seed(0)
+    nb = CTX // BS
+    blocks = B * nb
+    per = (3 * ((D + 2) // 3) + 3) // 4 * 4
+    kc, vc = kv_cache_pair((blocks, 1, kvh, BS * per), torch.uint8, dev)
+    kc.random_(0, 256, generator=g)
+    vc.copy_(kc.roll(1, 0))
+    ks = torch.rand(blocks, 1, kvh, BS, device=dev, generator=g)
+    vs = torch.rand_like(ks)
+    table = torch.randperm(blocks, device=dev, generator=g).to(torch.int32).view(B, nb)
+    lens = torch.full((B,), CTX, dtype=torch.int32, device=dev)
+    q = torch.randn(B, heads, D, device=dev, generator=g).half()
+    ws = torch.empty(B * heads * 64 * (D + 2), dtype=torch.float32, device=dev)
+    ref = torch.empty_like(q)
+    out = torch.empty_like(q)
+    s = torch.cuda.current_stream().cuda_stream
+    sm = 1 / math.sqrt(D)
+
+    def prod():
+        ops.paged_attention_into(q, kc, vc, table, lens, ks, vs, ref, 0, BS, sm, "golay_packed", CTX)
+
+    def var(vec, per_cu):
+        def run():
+            rc = pk(vec, per_cu, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), table.data_ptr(), lens.data_ptr(),
+                    ks.data_ptr(), vs.data_ptr(), out.data_ptr(), B, heads, kvh, D, blocks, BS, nb, CTX, sm,
+                    ws.data_ptr(), s)
+            assert rc == 0
+        return run
+
+    runs = [("product", prod), ("vec4_cu4", var(4, 4)), ("vec3_cu4", var(3, 4)), ("vec3_cu2", var(3, 2)),
+            ("vec3_u2_cu4", var(32, 4)), ("vec3_u3_cu4", var(33, 4)), ("vec3_u2_cu2", var(32, 2))]
+    res = {}
+    for _ in range(3):
+        for lab, run in runs:
+            for _ in range(50):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(ITERS):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            res.setdefault(lab, []).append(e0.elapsed_time(e1) * 1e3 / ITERS)
+    prod()
+    torch.cuda.synchronize()
+    for lab, run in runs:
+        diff = 0.0
+        if lab != "product":
+            run()
+            torch.cuda.synchronize()
+            diff = float((out.float() - ref.float()).abs().max())
+        print(f"golay_packed  32q/32kv {lab:12s} {min(res[lab]):7.2f} us/call (passes {', '.join(f'{x:.1f}' for x in res[lab])})"
+              f"  maxdiff {diff:.3g}", flush=True)
 
 
 if __name__ == "__main__":
