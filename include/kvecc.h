@@ -92,7 +92,9 @@ KVECC_API int kvecc_init_device(int device);
  * that can overlap never share counters.  The first launch on a new stream
  * takes a slot from a pool that grows outside captures only;
  * kvecc_reserve_counter_slots(device, n) makes n slots available for the
- * captures to come (kvecc_init_device keeps a reserve of 32). */
+ * captures to come (kvecc_init_device keeps a reserve of 32).  A graph keeps
+ * its slots for every replay: replay one graph on one stream at a time (two
+ * overlapping replays of the same graph would share counters). */
 KVECC_API int kvecc_reserve_counter_slots(int device, int n);
 /* Diagnostic (synchronises the device): slots handed out, and how many counter
  * words of all slots are non-zero -- 0 whenever no launch is in flight. */

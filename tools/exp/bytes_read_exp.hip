@@ -7,6 +7,9 @@
 // tiles per wave on a full grid, or the persistent grid at other per-CU
 // counts; `lds_pad` bytes of dynamic LDS cap the workgroups per CU).
 //
+// kvecc_exp_bytes_read_ipwg: the interpolating read on a full grid, neighbour
+// rows exchanged between the waves of a workgroup (bytes_read_ipwg_kernel).
+//
 // kvecc_exp_bytes_read_ip: the interpolating read (fp16 out, statistics on,
 // persistent grid + dynamic tail) rewritten with
 //   TBL3   the tile's block-table entry and its two neighbour rows' entries
@@ -228,6 +231,186 @@ __global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE)
   }
 }
 
+// Full grid, one tile per wave, neighbour rows exchanged inside the workgroup:
+// its 8 waves hold 8 consecutive tiles of the static order (mostly 8 adjacent
+// blocks of one sequence), so a tile's row above is the previous wave's last
+// decoded row and its row below the next wave's first, read from their LDS
+// stages after one workgroup barrier.  Only a tile that holds a double (~5 % at
+// BER 1e-3) needs them at all; of those, only wave 0's row above and wave 7's
+// row below come from memory (a synchronous load).  The clamps at the context's
+// ends are the product's (the tile's own first / last row).
+//   FLAGS false: one workgroup barrier after phase 1 (every wave waits for the
+//   slowest); true: each wave clears its LDS word, one barrier at the start
+//   (before any load: nothing in flight to wait for), then publishes "phase 1
+//   done" in the word, and only a wave that needs a neighbour's row spins on
+//   that neighbour's word
+template <typename TO, bool STATS, bool FLAGS = false>
+__global__ __launch_bounds__(kTileBlock) void bytes_read_ipwg_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ float scale_all[kTileWaves][kWave];
+  __shared__ uint32_t done[kTileWaves];
+  constexpr uint32_t tag = 1;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  uint8_t *stage = stage_all[wave];
+  const uint32_t cpr = a.d / 16;
+  const uint32_t items = a.tr * cpr;
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
+  uint32_t i2r[NI2], i2c[NI2];
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    ir[i] = f / cpr;
+    ic[i] = f - ir[i] * cpr;
+  }
+#pragma unroll
+  for (int i = 0; i < NI2; ++i) {
+    const uint32_t f = lane + kWave * i;
+    i2r[i] = f / (cpr * 16 / V);
+    i2c[i] = f - i2r[i] * (cpr * 16 / V);
+  }
+  uint32_t n1 = 0, n2 = 0;
+  auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
+    uint32_t q = cw, t = 0, s1 = 0, s2 = 0;
+    h84_decode4(cw, q, t, s1, s2);
+    if (count) {
+      if (STATS) {
+        n1 += s1;
+        n2 += s2;
+      }
+      dbl |= s2;
+    }
+    return q | t << 4;
+  };
+  if (FLAGS) {  // LDS holds whatever the last workgroup left: clear before anyone looks
+    if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&done[wave]) = 0u;
+    __syncthreads();
+  }
+  const uint32_t u = blockIdx.x * kTileWaves + wave;
+  const bool active = u < a.units;  // every wave reaches the barrier
+  ShimTile t;
+  t.rows = 0;
+  t.row0 = -1;
+  t.pos0 = t.side = t.bh = 0;
+  bool tile_dbl = false;
+  const uint32_t off0 = a.d;  // tile row r at (r + 1) d; rows 0 and rows + 1: the neighbours
+  if (active) {
+    t = shim_tile(a, u);
+    const bool live = t.row0 >= 0;
+    const uint32_t side = uni(t.side);
+    const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + (live ? t.row0 : 0) * (int64_t)a.d);
+    const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + (live ? t.row0 : 0)));
+    const uint32_t nrows = uni(live ? t.rows : 0u);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.d), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ss =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+    const float scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
+    u32x4 w[kByteTileItems];
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
+    }
+    scale_all[wave][lane] = scale;
+    bool dbl_any = false;
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;
+      const bool real = ir[i] < t.rows;
+      uint32_t dbl = 0;
+      const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
+                     dec(w[i].w, real, dbl)};
+      dbl_any |= dbl != 0;
+      if (real) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
+    }
+    tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+  }
+  if (FLAGS) {
+    wave_lds_sync();  // this wave's decoded rows are in LDS
+    if (lane == 0) *reinterpret_cast<volatile uint32_t *>(&done[wave]) = tag;
+  } else {
+    __syncthreads();  // every wave's decoded rows are in LDS
+  }
+  if (active && t.rows > 0) {
+    if (tile_dbl) {  // wave-uniform: the neighbour rows into stage rows 0 and rows + 1
+      const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
+      const bool ext_a = !top_clamp && wave == 0;                // row above in the previous workgroup
+      const bool ext_b = !bot_clamp && wave == kTileWaves - 1;   // row below in the next one
+      const bool below = lane >= cpr;
+      const uint32_t l = below ? lane - cpr : lane;
+      u32x4 hw{0u, 0u, 0u, 0u};
+      if (ext_a || ext_b) {  // one side at most (kTileWaves > 1)
+        const uint32_t bh = uni(t.bh), b = bh / a.hkv, h = bh - b * a.hkv;
+        const uint32_t pos = uni(ext_a ? t.pos0 - 1 : t.pos0 + t.rows);
+        const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + pos / a.bs);
+        if (blk >= 0 && l < cpr && below == ext_b) {
+          const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - pos / a.bs * a.bs);
+          hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[uni(t.side)]) +
+                                                         row * a.d) + l);
+        }
+        uint32_t none = 0;
+        hw = u32x4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none), dec(hw.w, false, none)};
+      }
+      if (FLAGS) {  // wait for the neighbours whose rows this tile reads (uniform)
+        const bool need_a = !top_clamp && !ext_a, need_b = !bot_clamp && !ext_b;
+        if (need_a)
+          while (*reinterpret_cast<volatile uint32_t *>(&done[wave - 1]) != tag) __builtin_amdgcn_s_sleep(1);
+        if (need_b)
+          while (*reinterpret_cast<volatile uint32_t *>(&done[wave + 1]) != tag) __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane < 2 * cpr) {
+        u32x4 v = hw;
+        if (below ? !ext_b : !ext_a) {
+          const uint8_t *src = below ? (bot_clamp ? stage + t.rows * a.d : stage_all[wave + 1] + off0)
+                                     : (top_clamp ? stage + off0 : stage_all[wave - 1] + a.tr * a.d);
+          v = reinterpret_cast<const u32x4 *>(src)[l];
+        }
+        *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;
+      }
+      wave_lds_sync();
+    }
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
+    auto phase2 = [&](auto interp_c) {
+      constexpr bool IP = decltype(interp_c)::value;
+#pragma unroll
+      for (int i = 0; i < NI2; ++i) {
+        if (i * kWave >= (int)(items * 16 / V)) break;
+        const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
+        const uint8_t *row = stage + off0 + r * a.d + V * c;
+        uint32_t q[2] = {0u, 0u};
+#pragma unroll
+        for (int k = 0; k < V / 4; ++k) {
+          const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+          if (IP) {
+            const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+            const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+            q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+          } else {
+            q[k] = v & 0x0F0F0F0Fu;
+          }
+        }
+        tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+      }
+    };
+    if (tile_dbl)
+      phase2(std::integral_constant<bool, true>{});
+    else
+      phase2(std::integral_constant<bool, false>{});
+  }
+  if (STATS) {
+    n1 = wave_sum(n1);
+    n2 = wave_sum(n2);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + ((blockIdx.x * kTileWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+      if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
+    }
+  }
+}
+
 struct IpVariant {
   const char *name;
   void (*kern)(ShimTileArgs);
@@ -308,4 +491,21 @@ EXP_API int kvecc_exp_bytes_read_ip(int v, int per_cu, BYTES_PARAMS) {
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * per_cu);
   KVECC_LAUNCH(exp::kIpVariants[v].kern, dim3(grid), dim3(kTileBlock), 0, as_stream(stream), a);
   return check_launch("exp_bytes_read_ip");
+}
+
+// the workgroup-exchange interpolating read (fp16, statistics), full grid;
+// lds_pad bytes of dynamic LDS cap the workgroups per CU
+EXP_API int kvecc_exp_bytes_read_ipwg(int lds_pad, BYTES_PARAMS) {
+  using namespace kvecc;
+  const ShimTileArgs a = exp::bytes_args(1, k_cache, v_cache, k_scales, v_scales, table, tstride, batch, ctx, hkv,
+                                         d, block_size, k_out, v_out, stats, stream);
+  const unsigned grid = (unsigned)cdiv(a.units, kTileWaves);
+  // lds_pad bit 0: the flag form (pads are whole KiB)
+  if (lds_pad & 1)
+    KVECC_LAUNCH((exp::bytes_read_ipwg_kernel<__half, true, true>), dim3(grid), dim3(kTileBlock),
+                 (unsigned)(lds_pad & ~1), as_stream(stream), a);
+  else
+    KVECC_LAUNCH((exp::bytes_read_ipwg_kernel<__half, true>), dim3(grid), dim3(kTileBlock), (unsigned)lds_pad,
+                 as_stream(stream), a);
+  return check_launch("exp_bytes_read_ipwg");
 }

@@ -5,7 +5,7 @@ distributions (tools/exp/bytes_read_exp.hip kvecc_exp_bytes_read, runs
 (kvecc_shim_read_batch), interleaved: [B=8, L=4096, Hkv=32, D=128] K+V,
 block 16, BER 1e-3, fp16 out -- bench.py's fused_golay_decode.hamming84 workload.
 
-usage: python tools/exp/run_bytes_read_exp.py [interp:chunk:per_cu:pad_kib | name[:per_cu] ...]
+usage: python tools/exp/run_bytes_read_exp.py [interp:chunk:per_cu:pad_kib | name[:per_cu] | ipwg[:pad_kib] ...]
 """
 import ctypes
 import os
@@ -20,6 +20,7 @@ from kvecc import _lib, ops  # noqa: E402
 
 B, L, H, D, BS = 8, 4096, 32, 128, 16
 ROUNDS = int(os.environ.get("ROUNDS", "30"))
+BER = float(os.environ.get("BER", "1e-3"))
 DEFAULT = ["ip", "ip_tbl3", "ip_hbuf", "ip_tbl3_hbuf", "ip_d128", "ip_tbl3_d128", "ip_hm", "ip_tbl3_hm", "1:8:0:0"]
 
 
@@ -29,6 +30,7 @@ def main():
     vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
     lib.kvecc_exp_bytes_read.argtypes = [ci, ci, ci, ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
     lib.kvecc_exp_bytes_read_ip.argtypes = [ci, ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
+    lib.kvecc_exp_bytes_read_ipwg.argtypes = [ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
     lib.kvecc_exp_bytes_ip_name.restype = ctypes.c_char_p
     ipn = [lib.kvecc_exp_bytes_ip_name(i).decode() for i in range(lib.kvecc_exp_bytes_ip_count())]
     prod = lib.kvecc_shim_read_batch
@@ -43,7 +45,7 @@ def main():
     for side in range(2):
         x = torch.randint(0, 16, (nb * H * BS * D,), generator=gen, dtype=torch.uint8).to(dev)
         cw = ops.hamming84_encode(x)
-        ops.inject_into(cw, cw, 1e-3, 8, seed=42 + side)
+        ops.inject_into(cw, cw, BER, 8, seed=42 + side)
         caches.append(cw.view(nb, 1, H, BS * D))
         scales.append((torch.rand(nb, 1, H, BS, generator=gen) * 0.1 + 0.01).to(dev))
     table = torch.randperm(nb, generator=gen).to(torch.int32).view(B, nlb).to(dev)
@@ -63,6 +65,12 @@ def main():
                 rc = prod(caches[0].data_ptr(), caches[1].data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(),
                           table.data_ptr(), nlb, B, L, H, D, 1, BS, 0, 2, interp, out[0].data_ptr(),
                           out[1].data_ptr(), ops._DT[torch.float16], stats[r].data_ptr(), s)
+            elif r.startswith("ipwg"):  # ipwg[:pad_kib], ipwgf[:pad_kib] = the flag form
+                pad = int(r.partition(":")[2] or 0) * 1024 + (1 if r.startswith("ipwgf") else 0)
+                rc = lib.kvecc_exp_bytes_read_ipwg(pad, caches[0].data_ptr(), caches[1].data_ptr(),
+                                                   scales[0].data_ptr(), scales[1].data_ptr(), table.data_ptr(),
+                                                   nlb, B, L, H, D, BS, out[0].data_ptr(), out[1].data_ptr(),
+                                                   stats[r].data_ptr(), s)
             elif not r[0].isdigit():
                 name, _, pc = r.partition(":")
                 rc = lib.kvecc_exp_bytes_read_ip(ipn.index(name), int(pc or 2), caches[0].data_ptr(),
