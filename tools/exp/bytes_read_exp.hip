@@ -3,15 +3,16 @@
 // #includes shim.hip for its tile helpers; tools/exp/run_bytes_read_exp.py
 // times them against the product (kvecc_shim_read_batch) in one process.
 //
-// kvecc_exp_bytes_read: the product kernel at other work distributions (CHUNK
-// tiles per wave on a full grid, or the persistent grid at other per-CU
-// counts; `lds_pad` bytes of dynamic LDS cap the workgroups per CU).
+// (Round 4 also ran the product's tile kernel of the time at other work
+// distributions -- full grids of 1-8 tiles per wave, persistent grids of 2-3
+// workgroups per CU: profiles/r04/fused/bytes_read_grid_ab.log.)
 //
 // kvecc_exp_bytes_read_ipwg: the interpolating read on a full grid, neighbour
 // rows exchanged between the waves of a workgroup (bytes_read_ipwg_kernel).
 //
-// kvecc_exp_bytes_read_ip: the interpolating read (fp16 out, statistics on,
-// persistent grid + dynamic tail) rewritten with
+// kvecc_exp_bytes_read_ip: round 3's interpolating read (fp16 out, statistics
+// on, persistent grid + dynamic tail, each tile prefetching its two neighbour
+// rows from memory) -- "ip" is that product kernel -- rewritten with
 //   TBL3   the tile's block-table entry and its two neighbour rows' entries
 //          loaded together (one scalar round trip before the tile's loads
 //          issue; the product waits for the tile's entry, issues the tile,
@@ -25,14 +26,6 @@
 
 namespace kvecc {
 namespace exp {
-
-template <bool INTERP, int CHUNK>
-static void launch_bytes_exp(const ShimTileArgs &a, unsigned lds_pad, int per_cu, hipStream_t st) {
-  const unsigned grid = CHUNK ? (unsigned)cdiv(cdiv(a.units, CHUNK), kTileWaves)
-                              : (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * per_cu);
-  KVECC_LAUNCH((shim_read_bytes_tiles_kernel<__half, KVECC_CODEC_H84, INTERP, true, CHUNK>), dim3(grid),
-               dim3(kTileBlock), lds_pad, st, a);
-}
 
 template <bool TBL3, bool HBUF, int WPE, int DC = 0, int ORDER = 0>
 __global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void bytes_read_ip_kernel(
@@ -411,6 +404,178 @@ __global__ __launch_bounds__(kTileBlock) void bytes_read_ipwg_kernel(ShimTileArg
   }
 }
 
+// The ladder from the plain read to the workgroup-exchange interpolating read,
+// one feature per level (BER 0: every level computes the right values; above
+// it only level 6 interpolates correctly):
+//   0 the plain H(8,4) read (full grid, one tile per wave)
+//   1 + error types stored with the data and the double-error ballot
+//   2 + the tile staged one row down (rows 0 / rows + 1 kept for neighbours)
+//   3 + the interpolating phase-2 body, chosen per tile by the ballot
+//   4 + rows past the tile masked in phase 1 (statistics and LDS stores)
+//   5 + the start barrier and the per-wave "decoded" words (LDS, plain stores)
+//   6 + the neighbour-row exchange (the full kernel)
+template <int LV>
+__global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a) {
+  using TO = __half;
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ float scale_all[kTileWaves][kWave];
+  __shared__ uint32_t decoded[kTileWaves];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  if (LV >= 5) {
+    if (lane == 0) decoded[wave] = 0u;
+    __syncthreads();
+  }
+  uint8_t *stage = stage_all[wave];
+  const uint32_t cpr = a.d / 16;
+  const uint32_t items = a.tr * cpr;
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
+  uint32_t i2r[NI2], i2c[NI2];
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    ir[i] = f / cpr;
+    ic[i] = f - ir[i] * cpr;
+  }
+#pragma unroll
+  for (int i = 0; i < NI2; ++i) {
+    const uint32_t f = lane + kWave * i;
+    i2r[i] = f / (cpr * 16 / V);
+    i2c[i] = f - i2r[i] * (cpr * 16 / V);
+  }
+  uint32_t n1 = 0, n2 = 0;
+  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  if (LV < 5 && gw >= a.units) return;
+  const bool active = gw < a.units;
+  ShimTile t;
+  t.rows = 0;
+  t.row0 = -1;
+  t.pos0 = t.side = t.bh = 0;
+  bool tile_dbl = false;
+  const uint32_t off0 = LV >= 2 ? a.d : 0u;
+  if (active) {
+    t = shim_tile(a, gw);
+    const bool live = t.row0 >= 0;
+    const uint32_t side = uni(t.side);
+    const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + (live ? t.row0 : 0) * (int64_t)a.d);
+    const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + (live ? t.row0 : 0)));
+    const uint32_t nrows = uni(live ? t.rows : 0u);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.d), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ss =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+    const float scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
+    u32x4 w[kByteTileItems];
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
+    }
+    scale_all[wave][lane] = scale;
+    bool dbl_any = false;
+    auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
+      uint32_t q = cw, tt = 0, s1 = 0, s2 = 0;
+      h84_decode4(cw, q, tt, s1, s2);
+      if (count) {
+        n1 += s1;
+        n2 += s2;
+        dbl |= s2;
+      }
+      return LV >= 1 ? q | tt << 4 : q;
+    };
+#pragma unroll
+    for (int i = 0; i < kByteTileItems; ++i) {
+      if (i * kWave >= (int)items) break;
+      const bool real = LV >= 4 ? ir[i] < t.rows : true;
+      uint32_t dbl = 0;
+      const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
+                     dec(w[i].w, real, dbl)};
+      dbl_any |= dbl != 0;
+      if (LV >= 4 ? real : ir[i] < a.tr) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
+    }
+    if (LV >= 1) tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+  }
+  wave_lds_sync();
+  if (LV >= 5 && lane == 0) __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (!active || t.rows == 0) return;
+  if (LV >= 6 && tile_dbl) {
+    const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
+    const bool ext_a = !top_clamp && wave == 0, ext_b = !bot_clamp && wave == kTileWaves - 1;
+    if (!top_clamp && !ext_a)
+      while (__hip_atomic_load(&decoded[wave - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+    if (!bot_clamp && !ext_b)
+      while (__hip_atomic_load(&decoded[wave + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+    const bool below = lane >= cpr;
+    const uint32_t l = below ? lane - cpr : lane;
+    u32x4 hw{0u, 0u, 0u, 0u};
+    if (ext_a || ext_b) {
+      const uint32_t bh = uni(t.bh), b = bh / a.hkv, h = bh - b * a.hkv;
+      const uint32_t pos = uni(ext_a ? t.pos0 - 1 : t.pos0 + t.rows);
+      const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + pos / a.bs);
+      if (blk >= 0 && l < cpr && below == ext_b) {
+        const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - pos / a.bs * a.bs);
+        hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[uni(t.side)]) +
+                                                       row * a.d) + l);
+      }
+      uint32_t q, tt, s1, s2;
+      uint32_t *hv = reinterpret_cast<uint32_t *>(&hw);
+      for (int k = 0; k < 4; ++k) {
+        q = hv[k];
+        h84_decode4(hv[k], q, tt, s1, s2);
+        hv[k] = q | tt << 4;
+      }
+    }
+    if (lane < 2 * cpr) {
+      u32x4 v = hw;
+      if (below ? !ext_b : !ext_a) {
+        const uint8_t *src = below ? (bot_clamp ? stage + t.rows * a.d : stage_all[wave + 1] + off0)
+                                   : (top_clamp ? stage + off0 : stage_all[wave - 1] + a.tr * a.d);
+        v = reinterpret_cast<const u32x4 *>(src)[l];
+      }
+      *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;
+    }
+    wave_lds_sync();
+  }
+  const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+  const bool dead = t.row0 < 0;
+  auto phase2 = [&](auto interp_c) {
+    constexpr bool IP = decltype(interp_c)::value;
+#pragma unroll
+    for (int i = 0; i < NI2; ++i) {
+      if (i * kWave >= (int)(items * 16 / V)) break;
+      const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
+      const uint8_t *row = stage + off0 + r * a.d + V * c;
+      uint32_t q[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < V / 4; ++k) {
+        const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+        if (IP) {
+          const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+          const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+          q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+        } else {
+          q[k] = v & 0x0F0F0F0Fu;
+        }
+      }
+      tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+    }
+  };
+  if (LV >= 3 && tile_dbl)
+    phase2(std::integral_constant<bool, true>{});
+  else
+    phase2(std::integral_constant<bool, false>{});
+  n1 = wave_sum(n1);
+  n2 = wave_sum(n2);
+  if (lane == 0) {
+    uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+    if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
+  }
+}
+
 struct IpVariant {
   const char *name;
   void (*kern)(ShimTileArgs);
@@ -466,19 +631,6 @@ static ShimTileArgs bytes_args(int interp, const void *k_cache, const void *v_ca
       int64_t tstride, int64_t batch, int64_t ctx, int64_t hkv, int64_t d, int64_t block_size, void *k_out,       \
       void *v_out, uint64_t *stats, void *stream
 
-EXP_API int kvecc_exp_bytes_read(int interp, int chunk, int per_cu, int lds_pad, BYTES_PARAMS) {
-  using namespace kvecc;
-  const ShimTileArgs a = exp::bytes_args(interp, k_cache, v_cache, k_scales, v_scales, table, tstride, batch, ctx,
-                                         hkv, d, block_size, k_out, v_out, stats, stream);
-  hipStream_t st = as_stream(stream);
-  const unsigned pad = (unsigned)lds_pad;
-#define BX(I, C) \
-  if (interp == I && chunk == C) exp::launch_bytes_exp<I, C>(a, pad, per_cu, st);
-  BX(0, 0) BX(0, 1) BX(0, 2) BX(0, 4) BX(1, 0) BX(1, 1) BX(1, 2) BX(1, 4) BX(1, 8)
-#undef BX
-  return check_launch("exp_bytes_read");
-}
-
 EXP_API int kvecc_exp_bytes_ip_count(void) {
   return (int)(sizeof(kvecc::exp::kIpVariants) / sizeof(kvecc::exp::kIpVariants[0]));
 }
@@ -508,4 +660,21 @@ EXP_API int kvecc_exp_bytes_read_ipwg(int lds_pad, BYTES_PARAMS) {
     KVECC_LAUNCH((exp::bytes_read_ipwg_kernel<__half, true>), dim3(grid), dim3(kTileBlock), (unsigned)lds_pad,
                  as_stream(stream), a);
   return check_launch("exp_bytes_read_ipwg");
+}
+
+// the ladder (bytes_ladder_kernel<level>), full grid, 16 KiB dynamic LDS
+EXP_API int kvecc_exp_bytes_ladder(int level, BYTES_PARAMS) {
+  using namespace kvecc;
+  const ShimTileArgs a = exp::bytes_args(1, k_cache, v_cache, k_scales, v_scales, table, tstride, batch, ctx, hkv,
+                                         d, block_size, k_out, v_out, stats, stream);
+  const unsigned grid = (unsigned)cdiv(a.units, kTileWaves);
+  hipStream_t st = as_stream(stream);
+  switch (level) {
+#define LC(L) \
+  case L: KVECC_LAUNCH((exp::bytes_ladder_kernel<L>), dim3(grid), dim3(kTileBlock), 16384u, st, a); break;
+    LC(0) LC(1) LC(2) LC(3) LC(4) LC(5) LC(6)
+#undef LC
+    default: return set_error(KVECC_EINVAL, "ladder level");
+  }
+  return check_launch("exp_bytes_ladder");
 }

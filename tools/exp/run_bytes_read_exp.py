@@ -1,11 +1,10 @@
 """A/B of the fused Hamming(8,4) read (plain and interpolating) at other work
-distributions (tools/exp/bytes_read_exp.hip kvecc_exp_bytes_read, runs
-"interp:chunk:per_cu:pad_kib") and the interpolating-read variants
-(kvecc_exp_bytes_read_ip, runs "name[:per_cu]") against the product
-(kvecc_shim_read_batch), interleaved: [B=8, L=4096, Hkv=32, D=128] K+V,
+variants (tools/exp/bytes_read_exp.hip: kvecc_exp_bytes_read_ip, runs
+"name[:per_cu]"; kvecc_exp_bytes_read_ipwg, runs "ipwg[:pad_kib]" /
+"ipwgf[:pad_kib]") against the product (kvecc_shim_read_batch), interleaved: [B=8, L=4096, Hkv=32, D=128] K+V,
 block 16, BER 1e-3, fp16 out -- bench.py's fused_golay_decode.hamming84 workload.
 
-usage: python tools/exp/run_bytes_read_exp.py [interp:chunk:per_cu:pad_kib | name[:per_cu] | ipwg[:pad_kib] ...]
+usage: python tools/exp/run_bytes_read_exp.py [name[:per_cu] | ipwg[:pad_kib] | ipwgf[:pad_kib] | ladN ...]
 """
 import ctypes
 import os
@@ -21,16 +20,16 @@ from kvecc import _lib, ops  # noqa: E402
 B, L, H, D, BS = 8, 4096, 32, 128, 16
 ROUNDS = int(os.environ.get("ROUNDS", "30"))
 BER = float(os.environ.get("BER", "1e-3"))
-DEFAULT = ["ip", "ip_tbl3", "ip_hbuf", "ip_tbl3_hbuf", "ip_d128", "ip_tbl3_d128", "ip_hm", "ip_tbl3_hm", "1:8:0:0"]
+DEFAULT = ["ip", "ipwgf:16", "ipwgf:0", "ipwg:16", "plain"]
 
 
 def main():
     dev = torch.device("cuda:0")
     lib = ctypes.CDLL(os.path.join(REPO, "tools", "exp", "libbread.so"))
     vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
-    lib.kvecc_exp_bytes_read.argtypes = [ci, ci, ci, ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
     lib.kvecc_exp_bytes_read_ip.argtypes = [ci, ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
     lib.kvecc_exp_bytes_read_ipwg.argtypes = [ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
+    lib.kvecc_exp_bytes_ladder.argtypes = [ci] + [vp] * 5 + [i64] * 6 + [vp, vp, vp, vp]
     lib.kvecc_exp_bytes_ip_name.restype = ctypes.c_char_p
     ipn = [lib.kvecc_exp_bytes_ip_name(i).decode() for i in range(lib.kvecc_exp_bytes_ip_count())]
     prod = lib.kvecc_shim_read_batch
@@ -52,37 +51,34 @@ def main():
     out = (torch.empty(B, H, L, D, dtype=torch.float16, device=dev),
            torch.empty(B, H, L, D, dtype=torch.float16, device=dev))
     s = torch.cuda.current_stream().cuda_stream
-    for interp in (1, 0):
-        sel = ["product"] + [r for r in runs if (int(r.split(":")[0]) if r[0].isdigit() else 1) == interp]
-        if len(sel) == 1:
-            continue
+    for interp in (1,):  # "plain": the product without interpolation, for reference (same=False)
+        sel = ["product"] + runs
         stats = {r: ops.new_stats(dev) for r in sel}
 
         def call(r, ev=None):
             if ev is not None:
                 tn(ev[0].cuda_event, ev[1].cuda_event)
-            if r == "product":
+            if r in ("product", "plain"):
                 rc = prod(caches[0].data_ptr(), caches[1].data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(),
-                          table.data_ptr(), nlb, B, L, H, D, 1, BS, 0, 2, interp, out[0].data_ptr(),
+                          table.data_ptr(), nlb, B, L, H, D, 1, BS, 0, 2, int(r == "product"), out[0].data_ptr(),
                           out[1].data_ptr(), ops._DT[torch.float16], stats[r].data_ptr(), s)
+            elif r.startswith("lad"):  # ladN: bytes_ladder_kernel<N>
+                rc = lib.kvecc_exp_bytes_ladder(int(r[3:]), caches[0].data_ptr(), caches[1].data_ptr(),
+                                                scales[0].data_ptr(), scales[1].data_ptr(), table.data_ptr(),
+                                                nlb, B, L, H, D, BS, out[0].data_ptr(), out[1].data_ptr(),
+                                                stats[r].data_ptr(), s)
             elif r.startswith("ipwg"):  # ipwg[:pad_kib], ipwgf[:pad_kib] = the flag form
                 pad = int(r.partition(":")[2] or 0) * 1024 + (1 if r.startswith("ipwgf") else 0)
                 rc = lib.kvecc_exp_bytes_read_ipwg(pad, caches[0].data_ptr(), caches[1].data_ptr(),
                                                    scales[0].data_ptr(), scales[1].data_ptr(), table.data_ptr(),
                                                    nlb, B, L, H, D, BS, out[0].data_ptr(), out[1].data_ptr(),
                                                    stats[r].data_ptr(), s)
-            elif not r[0].isdigit():
+            else:
                 name, _, pc = r.partition(":")
                 rc = lib.kvecc_exp_bytes_read_ip(ipn.index(name), int(pc or 2), caches[0].data_ptr(),
                                                  caches[1].data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(),
                                                  table.data_ptr(), nlb, B, L, H, D, BS, out[0].data_ptr(),
                                                  out[1].data_ptr(), stats[r].data_ptr(), s)
-            else:
-                _, ch, pc, pad = (int(v) for v in r.split(":"))
-                rc = lib.kvecc_exp_bytes_read(interp, ch, pc, pad * 1024, caches[0].data_ptr(), caches[1].data_ptr(),
-                                              scales[0].data_ptr(), scales[1].data_ptr(), table.data_ptr(), nlb, B,
-                                              L, H, D, BS, out[0].data_ptr(), out[1].data_ptr(),
-                                              stats[r].data_ptr(), s)
             assert rc == 0, r
 
         for r in sel:
@@ -113,7 +109,7 @@ def main():
         for r in sel:
             us = [a.elapsed_time(b) * 1e3 for a, b in times[r]]
             med = statistics.median(us)
-            print(f"{'interp' if interp else 'plain '} {r:14s} median {med:6.1f} us  min {min(us):6.1f}  "
+            print(f"interp {r:14s} median {med:6.1f} us  min {min(us):6.1f}  "
                   f"{nbytes / med / 1e3:5.0f} GB/s  frac {nbytes / med / 1e3 / 8000:5.3f}  same={same[r]}", flush=True)
 
 
