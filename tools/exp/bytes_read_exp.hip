@@ -22,12 +22,13 @@
 //   WPE    amdgpu_waves_per_eu minimum (register budget; 1 = none)
 //   DC     the head size as a compile-time constant (0: runtime, the product)
 //   ORDER  1: tiles heads fastest (golay_read_exp.hip tile_at)
+//   MG     phase-2 (row, chunk) by a reciprocal multiply (bytes_ladder_kernel INC)
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/shim.hip"
 
 namespace kvecc {
 namespace exp {
 
-template <bool TBL3, bool HBUF, int WPE, int DC = 0, int ORDER = 0>
+template <bool TBL3, bool HBUF, int WPE, int DC = 0, int ORDER = 0, bool MG = false>
 __global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void bytes_read_ip_kernel(
     ShimTileArgs a) {
   using TO = __half;
@@ -55,6 +56,8 @@ __global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE)
     i2r[i] = f / (cpr * 16 / V);
     i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
+  const uint32_t per2 = cpr * 16 / V;
+  const uint32_t mg = uni((65536u + per2 - 1) / per2);
   uint32_t n1 = 0, n2 = 0;
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
   uint32_t u = gw;
@@ -191,7 +194,11 @@ __global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE)
 #pragma unroll
       for (int i = 0; i < NI2; ++i) {
         if (i * kWave >= (int)(items * 16 / V)) break;
-        const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
+        // MG: (row, chunk) by a reciprocal multiply (see bytes_ladder_kernel INC)
+        const uint32_t f = lane + kWave * i;
+        const uint32_t fq = __umul24(f, mg) >> 16;
+        const uint32_t rr = MG ? fq : i2r[i], c = MG ? f - fq * per2 : i2c[i];
+        const uint32_t r = min(rr, a.tr - 1);
         const uint8_t *row = stage + off0 + r * kd + V * c;
         uint32_t q[2] = {0u, 0u};
 #pragma unroll
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(kTileBlock) __attribute__((amdgpu_waves_per_eu(WPE)
             q[k] = v & 0x0F0F0F0Fu;
           }
         }
-        tile_store(os, (i2r[i] * kd + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+        tile_store(os, (rr * kd + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
       }
     };
     if (tile_dbl)
@@ -414,7 +421,12 @@ __global__ __launch_bounds__(kTileBlock) void bytes_read_ipwg_kernel(ShimTileArg
 //   4 + rows past the tile masked in phase 1 (statistics and LDS stores)
 //   5 + the start barrier and the per-wave "decoded" words (LDS, plain stores)
 //   6 + the neighbour-row exchange (the full kernel)
-template <int LV>
+//   INC: phase 2 derives each item's (row, chunk) by a reciprocal multiply
+//   (one 24-bit multiply and a shift) instead of holding a divided (row,
+//   chunk) per item -- which the compiler, short of registers once the
+//   interpolating body exists, re-derived by integer division after phase 1
+//   (~135 instructions on every wave's critical path)
+template <int LV, bool INC = false>
 __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a) {
   using TO = __half;
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
@@ -541,12 +553,19 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
   }
   const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
   const bool dead = t.row0 < 0;
+  const uint32_t per2 = cpr * 16 / V;  // V-value chunks per row (<= 64)
+  // f / per2 for f < 2^9 as (f * m) >> 16, m = ceil(2^16 / per2): exact, as
+  // f (m - 2^16 / per2) < 2^9 / 2^16 < 1 / per2
+  const uint32_t m = uni((65536u + per2 - 1) / per2);
   auto phase2 = [&](auto interp_c) {
     constexpr bool IP = decltype(interp_c)::value;
 #pragma unroll
     for (int i = 0; i < NI2; ++i) {
       if (i * kWave >= (int)(items * 16 / V)) break;
-      const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
+      const uint32_t f = lane + kWave * i;
+      const uint32_t fq = __umul24(f, m) >> 16;
+      const uint32_t rr = INC ? fq : i2r[i], c = INC ? f - fq * per2 : i2c[i];
+      const uint32_t r = min(rr, a.tr - 1);
       const uint8_t *row = stage + off0 + r * a.d + V * c;
       uint32_t q[2] = {0u, 0u};
 #pragma unroll
@@ -560,7 +579,7 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
           q[k] = v & 0x0F0F0F0Fu;
         }
       }
-      tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+      tile_store(os, (rr * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
     }
   };
   if (LV >= 3 && tile_dbl)
@@ -588,6 +607,8 @@ static const IpVariant kIpVariants[] = {
     {"ip_tbl3_d128", bytes_read_ip_kernel<true, false, 1, 128>},
     {"ip_tbl3_hbuf_d128", bytes_read_ip_kernel<true, true, 1, 128>},
     {"ip_tbl3_d128_w6", bytes_read_ip_kernel<true, false, 6, 128>},
+    {"ip_mg", bytes_read_ip_kernel<false, false, 1, 0, 0, true>},
+    {"ip_tbl3_mg", bytes_read_ip_kernel<true, false, 1, 0, 0, true>},
     {"ip_hm", bytes_read_ip_kernel<false, false, 1, 0, 1>},
     {"ip_tbl3_hm", bytes_read_ip_kernel<true, false, 1, 0, 1>},
 };
@@ -662,7 +683,7 @@ EXP_API int kvecc_exp_bytes_read_ipwg(int lds_pad, BYTES_PARAMS) {
   return check_launch("exp_bytes_read_ipwg");
 }
 
-// the ladder (bytes_ladder_kernel<level>), full grid, 16 KiB dynamic LDS
+// the ladder (bytes_ladder_kernel<level>; level + 10: INC), full grid, 16 KiB dynamic LDS
 EXP_API int kvecc_exp_bytes_ladder(int level, BYTES_PARAMS) {
   using namespace kvecc;
   const ShimTileArgs a = exp::bytes_args(1, k_cache, v_cache, k_scales, v_scales, table, tstride, batch, ctx, hkv,
@@ -671,7 +692,8 @@ EXP_API int kvecc_exp_bytes_ladder(int level, BYTES_PARAMS) {
   hipStream_t st = as_stream(stream);
   switch (level) {
 #define LC(L) \
-  case L: KVECC_LAUNCH((exp::bytes_ladder_kernel<L>), dim3(grid), dim3(kTileBlock), 16384u, st, a); break;
+  case L: KVECC_LAUNCH((exp::bytes_ladder_kernel<L>), dim3(grid), dim3(kTileBlock), 16384u, st, a); break;   \
+  case 10 + L: KVECC_LAUNCH((exp::bytes_ladder_kernel<L, true>), dim3(grid), dim3(kTileBlock), 16384u, st, a); break;
     LC(0) LC(1) LC(2) LC(3) LC(4) LC(5) LC(6)
 #undef LC
     default: return set_error(KVECC_EINVAL, "ladder level");

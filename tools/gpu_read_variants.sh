@@ -11,7 +11,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-export TMPDIR=/tmp ROUNDS=${ROUNDS:-10}
+export TMPDIR=/tmp ROUNDS=${ROUNDS:-20}
 LIB=$ROOT/quantized-kv-cache-ecc-protection_amd/kvecc/libkvecc.so
 for CASE in golay golay_packed hamming84 hamming84+interp; do
   D=$OUT/${CASE/+/_}

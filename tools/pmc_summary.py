@@ -77,7 +77,18 @@ def variants(src, dst):
         w = statistics.median(write[wk]) * 1024
         algo = per_row * 2 * (M // 43)
         ns = float(stats[name]["AverageNs"])
+        # the timed launches alone: the trace's last ROUNDS dispatches (the
+        # average above also counts the driver's warm-up calls)
+        trace = glob.glob(os.path.join(d, "prof", "*kernel_trace.csv"))[0]
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                for r in sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Dispatch_Id"]))
+                if kern in r["Kernel_Name"]]
+        rounds = int(os.environ.get("ROUNDS", "20"))
+        timed = durs[-rounds:]
+        med = statistics.median(timed)
         out["variants"][var] = {"kernel": name, "avg_ns": ns, "calls": int(stats[name]["Calls"]),
+                                "median_ns_timed": med, "timed_launches": len(timed),
+                                "frac_of_8tbs_timed": algo / med / 8e3,
                                 "algorithmic_bytes": algo, "fetch_bytes": f, "write_bytes": w,
                                 "hbm_bytes_per_launch": f + w, "traffic_over_algorithmic": (f + w) / algo,
                                 "achieved_tbs": algo / ns / 1e3, "frac_of_8tbs": algo / ns / 8e3}
