@@ -284,8 +284,8 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 //     166-168 / 153-155 / 164-166 at 85-90 (profiles/r03/fused/static_pct_ab1.log).
 constexpr int kTileBlock = 512;                    // 8 waves per workgroup
 constexpr int kTileWaves = kTileBlock / kWave;
-constexpr int kShimTilePerCu = 2;                  // Golay / interpolating reads: persistent grid
-constexpr int kShimBytesLdsPad = 16384;            // plain byte-codec read: caps 4 workgroups per CU
+constexpr int kShimTilePerCu = 2;                  // Golay read: persistent grid
+constexpr int kShimBytesLdsPad = 16384;            // byte-codec reads: caps 4 workgroups per CU
 constexpr uint32_t kShimReadStaticPct = 65;        // static share of the dynamic-tail schedule
 constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
 constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
@@ -559,36 +559,52 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
 
 // ---- byte codecs (raw INT4, H(7,4), H(8,4) [+ interpolation]) through wave tiles
 // The Golay tile scheme for one-byte codewords (d % 16 == 0): a wave owns the
-// `tr` rows of one (side, sequence, head, block).  Phase 1: each lane decodes
-// 16-byte chunks of codewords (16 values, SWAR through the v_perm tables) into
-// the wave's LDS tile as one byte per value, data | error type << 4; with
-// interpolation the tile also holds the decoded neighbour rows of positions
-// pos0 - 1 and pos0 + rows (clamped to the context, as the composed read
-// clamps), which live in other blocks.  Phase 2: each lane takes a 16-value
-// chunk of a row, interpolates double errors from the rows above and below
-// (decoded, not interpolated, neighbours), dequantizes and writes 16-byte
-// non-temporal stores.  A row in a missing block (table entry -1) reads as
-// zero codewords and outputs +0, as in the Golay kernel and the host twin.
+// `tr` rows of one (side, sequence, head, block), on a full grid -- one tile
+// per wave, workgroups retiring and being replaced, which evens out the waves'
+// uneven memory latency with no schedule (137-143 us against 147 for a
+// persistent grid).  Phase 1: each lane decodes 16-byte chunks
+// of codewords (16 values, SWAR through the v_perm tables) into the wave's LDS
+// tile, one byte per value.  Phase 2: each lane dequantizes a chunk of a row
+// and writes a 16-byte non-temporal store, 1 KiB contiguous per
+// wave-instruction.  A row in a missing block (table entry -1) reads as zero
+// codewords and outputs +0, as in the Golay kernel and the host twin.
 constexpr int kByteTileItems = 4;  // 16-value chunks per lane per phase (max)
-// Interpolation only changes a double error's value.  A tile whose decode saw
-// no double (a wave ballot in phase 1) dequantizes without the interpolation
-// arithmetic and the neighbour-row reads (at BER 1e-3 ~95 % of tiles).
-// [8,4096,32,128] K+V fp16, per launch: 204 -> 177 us at BER 0, 199 -> 176 us
-// at 1e-3, 201 -> 206 us at 1e-2 (profiles/r02/interp_read/).  Loading the
-// neighbour rows only when a double sits in a tile's first or last row ran 161
-// us at BER 0 but 188 / 221 us at 1e-3 / 1e-2, so every tile prefetches them.
-template <typename TO, int CODEC, bool INTERP, bool STATS, int CHUNK>
+
+// the tile's codewords (one 16-byte chunk per item: row ir, chunk ic) and its
+// rows' scales; rows past the tile and missing blocks load as 0 through the
+// buffer bounds (codeword 0 decodes clean)
+__device__ __forceinline__ float byte_tile_issue(const ShimTileArgs &a, const ShimTile &t, uint32_t lane,
+                                                 const uint32_t *ir, const uint32_t *ic, uint32_t items,
+                                                 u32x4 *w) {
+  const bool live = t.row0 >= 0;
+  const uint32_t side = uni(t.side);
+  const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + (live ? t.row0 : 0) * (int64_t)a.d);
+  const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + (live ? t.row0 : 0)));
+  const uint32_t nrows = uni(live ? t.rows : 0u);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.d), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ss =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+  const float scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    if (i * kWave >= (int)items) break;  // uniform
+    w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
+  }
+  return scale;
+}
+
+template <typename TO, int CODEC, bool STATS>
 __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
   __shared__ float scale_all[kTileWaves][kWave];  // row scales, staged like the rows
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
   uint8_t *stage = stage_all[wave];
-  const uint32_t nwaves = gridDim.x * kTileWaves;
   const uint32_t cpr = a.d / 16;       // 16-byte chunks per row
   const uint32_t items = a.tr * cpr;   // <= 64 * kByteTileItems (host check)
   uint32_t ir[kByteTileItems], ic[kByteTileItems];          // phase 1: row, 16-value chunk
-  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;  // phase 2: VPL-value chunks
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;  // phase 2: V-value chunks
   uint32_t i2r[NI2], i2c[NI2];                              // phase 2: row, chunk
 #pragma unroll
   for (int i = 0; i < kByteTileItems; ++i) {
@@ -602,72 +618,109 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     i2r[i] = f / (cpr * 16 / V);
     i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
-  uint32_t n1 = 0, n2 = 0;
-  // CHUNK > 0: wave w takes the CHUNK tiles [w CHUNK, w CHUNK + CHUNK) of a
-  // full grid; 0: the persistent grid with the dynamic tail
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
-  uint32_t u = CHUNK ? gw * CHUNK : gw;
-  const uint32_t uend = CHUNK ? min(a.units, u + CHUNK) : a.units;
-  if (u >= uend) return;
-  TileSchedule sched;
-  if (!CHUNK) sched.init(a.units, a.dyn, gw, nwaves, lane, kShimReadStaticPct);
-
-  ShimTile cur;
-  u32x4 w[kByteTileItems], hw = u32x4{0u, 0u, 0u, 0u};
-  float scale;
-  bool has_hw = false;  // hw holds the current tile's neighbour rows
-  // neighbour rows of tile c: lanes [0, cpr) row pos0 - 1 (pos0 itself at the
-  // context's start), [cpr, 2 cpr) row pos0 + rows (the last row at its end)
-  auto load_halo = [&](const ShimTile &c) -> u32x4 {
-    // both positions and their blocks are wave-uniform: scalar loads, so the
-    // halo does not wait behind the previous tile's stores
-    const uint32_t side = uni(c.side);
-    const bool below = lane >= cpr;
-    const uint32_t bh = uni(c.bh), b = bh / a.hkv, h = bh - b * a.hkv;
-    const uint32_t pa = uni(c.pos0 > 0 ? c.pos0 - 1 : 0u), pb = uni(min(c.pos0 + c.rows, a.ctx - 1));
-    const int32_t ba = ld_scalar(a.table + (int64_t)b * a.tstride + pa / a.bs);
-    const int32_t bb = ld_scalar(a.table + (int64_t)b * a.tstride + pb / a.bs);
-    const uint32_t pos = below ? pb : pa;
-    const uint32_t lb = pos / a.bs;
-    const int32_t blk = below ? bb : ba;
-    u32x4 r{0u, 0u, 0u, 0u};
-    if (lane < 2 * cpr && blk >= 0) {
-      const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - lb * a.bs);
-      r = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[side]) + row * a.d) +
-                    (below ? lane - cpr : lane));
-    }
-    return r;
-  };
-  auto fetch = [&](uint32_t uu) {
-    cur = shim_tile(a, uu);
-    const bool live = cur.row0 >= 0;
-    const uint32_t side = uni(cur.side);
-    const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + (live ? cur.row0 : 0) * (int64_t)a.d);
-    const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + (live ? cur.row0 : 0)));
-    const uint32_t nrows = uni(live ? cur.rows : 0u);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.d), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ss =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
-    scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
-#pragma unroll
-    for (int i = 0; i < kByteTileItems; ++i) {
-      if (i * kWave >= (int)items) break;  // uniform
-      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
-    }
-    has_hw = INTERP && cur.rows > 0;
-    if (has_hw) hw = load_halo(cur);
-  };
-  // 4 codewords -> data | type << 4 per byte (and the statistics); `dbl`
-  // collects the words' double errors
-  auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
-    uint32_t q = cw, t = 0, s1 = 0, s2 = 0;
+  if (gw >= a.units) return;
+  const ShimTile t = shim_tile(a, gw);
+  u32x4 w[kByteTileItems];
+  scale_all[wave][lane] = byte_tile_issue(a, t, lane, ir, ic, items, w);
+  uint32_t n1 = 0, n2 = 0;
+  auto dec = [&](uint32_t cw) -> uint32_t {  // 4 codewords -> data per byte (and the statistics)
+    uint32_t q = cw, tt = 0, s1 = 0, s2 = 0;
     if (CODEC == KVECC_CODEC_H84) {
-      h84_decode4(cw, q, t, s1, s2);
+      h84_decode4(cw, q, tt, s1, s2);
     } else if (CODEC == KVECC_CODEC_H74) {
-      h74_decode4(cw, q, t, s1);
-      t = 0;
+      h74_decode4(cw, q, tt, s1);
     }
+    if (STATS) {
+      n1 += s1;
+      n2 += s2;
+    }
+    return q;
+  };
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    if (i * kWave >= (int)items) break;  // uniform
+    const u32x4 d4{dec(w[i].x), dec(w[i].y), dec(w[i].z), dec(w[i].w)};
+    if (ir[i] < a.tr) *reinterpret_cast<u32x4 *>(stage + ir[i] * a.d + 16 * ic[i]) = d4;
+  }
+  wave_lds_sync();
+  // phase 2: rows past the tile fall outside its output descriptor (dropped);
+  // their LDS reads use row tr - 1
+  const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+  const bool dead = t.row0 < 0;
+#pragma unroll
+  for (int i = 0; i < NI2; ++i) {
+    if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
+    const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
+    const uint8_t *row = stage + r * a.d + V * c;
+    uint32_t q[2] = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < V / 4; ++k) {
+      const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+      q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
+    }
+    tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+  }
+  if (STATS) {
+    n1 = wave_sum(n1);
+    n2 = wave_sum(n2);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+      if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
+    }
+  }
+}
+
+// ---- H(8,4) with double-error interpolation (ecc_shim.py:1038-1059,
+// interpolation_triton.py:120-159) on the same full grid, neighbour rows from
+// the workgroup.
+// Interpolating row r needs the decoded rows r - 1 and r + 1; for a tile's
+// first and last rows those are the rows at positions pos0 - 1 and pos0 + rows
+// (the tile's own first / last row at the context's ends, as the composed read
+// clamps).  The 8 waves of a workgroup hold 8 consecutive tiles of the static
+// order -- adjacent blocks of one (side, sequence, head) -- so those rows are
+// the previous wave's last decoded row and the next wave's first, already in
+// LDS.  Interpolation only changes a double error's value, so only a tile whose
+// decode saw a double (a wave ballot; ~5 % of tiles at BER 1e-3) reads
+// neighbours: it waits for its neighbour waves' "decoded" words and copies
+// their edge rows into its stage rows 0 and rows + 1; wave 0's row above and
+// wave 7's row below come from memory (one synchronous row).  No barrier after
+// the decode: with one, every wave waited for the slowest load of its
+// workgroup.  Phase 2 derives each item's (row, chunk) by a reciprocal
+// multiply: with the interpolating body present the compiler re-derived
+// per-item divisions after phase 1, on every wave's critical path.
+// [8,4096,32,128] K+V fp16, BER 1e-3: 142.5-150.3 us against 151.8-158.8 for
+// round 3's persistent grid prefetching every tile's neighbour rows; at 1e-2
+// (every tile holds doubles) 202.7-207.0 against 187.6-199.0
+// (profiles/r04/fused/interp_ladder_inc*.log, tools/exp/bytes_read_exp.hip).
+template <typename TO, bool STATS>
+__global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ float scale_all[kTileWaves][kWave];
+  __shared__ uint32_t decoded[kTileWaves];  // wave w's tile is in its stage (1) or not yet (0)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  // LDS holds what the last workgroup on this CU left: clear the words before
+  // anyone looks (before any load, so the barrier waits for no memory)
+  if (lane == 0) __hip_atomic_store(&decoded[wave], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  uint8_t *stage = stage_all[wave];
+  const uint32_t cpr = a.d / 16;
+  const uint32_t items = a.tr * cpr;
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    ir[i] = f / cpr;
+    ic[i] = f - ir[i] * cpr;
+  }
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
+  uint32_t n1 = 0, n2 = 0;
+  // data | error type << 4 per byte; `dbl` collects the double errors
+  auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
+    uint32_t q = cw, tt = 0, s1 = 0, s2 = 0;
+    h84_decode4(cw, q, tt, s1, s2);
     if (count) {
       if (STATS) {
         n1 += s1;
@@ -675,81 +728,112 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
       }
       dbl |= s2;
     }
-    return INTERP ? q | t << 4 : q;  // phase 2 reads the type only to interpolate
+    return q | tt << 4;
   };
-  fetch(u);
-  for (;;) {
-    // ---- phase 1: decode into the LDS tile (row r at (r + INTERP) * d) --------
-    const uint32_t off0 = INTERP ? a.d : 0u;
-    scale_all[wave][lane] = scale;
-    bool dbl_any = false;  // this lane saw a double
+  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  const bool active = gw < a.units;  // every wave publishes its word
+  ShimTile t;
+  t.rows = 0;
+  t.row0 = -1;
+  t.pos0 = t.side = t.bh = 0;
+  bool tile_dbl = false;
+  const uint32_t off0 = a.d;  // tile row r at stage row r + 1; rows 0 and rows + 1: the neighbours
+  if (active) {
+    t = shim_tile(a, gw);
+    u32x4 w[kByteTileItems];
+    scale_all[wave][lane] = byte_tile_issue(a, t, lane, ir, ic, items, w);
+    bool dbl_any = false;
 #pragma unroll
     for (int i = 0; i < kByteTileItems; ++i) {
       if (i * kWave >= (int)items) break;  // uniform
-      // rows past the tile (and missing blocks) load as 0 through the buffer
-      // bounds, and codeword 0 decodes clean, so they add no statistics or
-      // doubles; the interpolating kernel still masks them (the same condition
-      // as its LDS store: without it the compiler took 131 VGPRs, past the 128
-      // that fit 2 workgroups per CU, and the kernel ran 20 % slower)
-      const bool real = !INTERP || ir[i] < cur.rows;
+      // rows past the tile: no statistics, no doubles, no LDS store (it would
+      // land on the row-below slot)
+      const bool real = ir[i] < t.rows;
       uint32_t dbl = 0;
       const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
                      dec(w[i].w, real, dbl)};
       dbl_any |= dbl != 0;
-      // (with interpolation, rows past the tile's end would overwrite the row below)
-      if (ir[i] < (INTERP ? cur.rows : a.tr)) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
+      if (real) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
     }
-    // wave-uniform: does this tile hold a double error at all
-    const bool tile_dbl = INTERP && __builtin_amdgcn_ballot_w64(dbl_any) != 0;
-    if (INTERP && has_hw && lane < 2 * cpr) {  // neighbours: row 0 above, row rows + 1 below
-      uint32_t none = 0;
-      const u32x4 d4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none),
-                     dec(hw.w, false, none)};
-      const uint32_t r = lane >= cpr ? cur.rows + 1 : 0u;
-      *reinterpret_cast<u32x4 *>(stage + r * a.d + 16 * (lane >= cpr ? lane - cpr : lane)) = d4;
-    }
-    wave_lds_sync();
-    const ShimTile t = cur;
-    u = CHUNK ? u + 1 : sched.next(u, lane);
-    const bool more = u < uend;
-    if (more) fetch(u);
-    // ---- phase 2: interpolate, dequantize; 16 output bytes per lane, so each
-    // wave-instruction stores 1 KiB contiguous (rows past the tile fall outside
-    // its output descriptor: dropped) -------------------------------------------
-    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
-    const bool dead = t.row0 < 0;
-    // one straight-line body per case (a branch per item serialised its LDS reads)
-    auto phase2 = [&](auto interp_c) {
-      constexpr bool IP = decltype(interp_c)::value;
-#pragma unroll
-      for (int i = 0; i < NI2; ++i) {
-        if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
-        // a lane's items past the tile store outside its output descriptor
-        // (dropped); their LDS reads use row tr - 1 (indices stay in the tile)
-        const uint32_t r = min(i2r[i], a.tr - 1), c = i2c[i];
-        const uint8_t *row = stage + off0 + r * a.d + V * c;
-        uint32_t q[2] = {0u, 0u};
-#pragma unroll
-        for (int k = 0; k < V / 4; ++k) {
-          const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
-          if (IP) {
-            const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
-            const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
-            q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
-          } else {
-            q[k] = CODEC == KVECC_CODEC_NONE ? v : v & 0x0F0F0F0Fu;  // raw bytes as stored, unmasked
-          }
-        }
-        tile_store(os, (i2r[i] * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+    tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+  }
+  wave_lds_sync();  // this wave's rows are in LDS before its word says so
+  if (lane == 0) __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (!active || t.rows == 0) return;
+  if (tile_dbl) {  // wave-uniform: the neighbour rows into stage rows 0 and rows + 1
+    const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
+    const bool ext_a = !top_clamp && wave == 0;               // row above: the previous workgroup's
+    const bool ext_b = !bot_clamp && wave == kTileWaves - 1;  // row below: the next workgroup's
+    // the neighbour tiles exist (same sequence, inside the grid) and belong to
+    // this workgroup, whose waves all publish: the waits end
+    if (!top_clamp && !ext_a)
+      while (__hip_atomic_load(&decoded[wave - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+    if (!bot_clamp && !ext_b)
+      while (__hip_atomic_load(&decoded[wave + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+    const bool below = lane >= cpr;
+    const uint32_t l = below ? lane - cpr : lane;
+    u32x4 hw{0u, 0u, 0u, 0u};
+    if (ext_a || ext_b) {  // one side at most (kTileWaves > 1)
+      const uint32_t bh = uni(t.bh), b = bh / a.hkv, h = bh - b * a.hkv;
+      const uint32_t pos = uni(ext_a ? t.pos0 - 1 : t.pos0 + t.rows);
+      const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + pos / a.bs);
+      if (blk >= 0 && l < cpr && below == ext_b) {
+        const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - pos / a.bs * a.bs);
+        hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[uni(t.side)]) +
+                                                       row * a.d) + l);
       }
-    };
-    if (INTERP && tile_dbl)
-      phase2(std::integral_constant<bool, true>{});
-    else
-      phase2(std::integral_constant<bool, false>{});
-    if (!more) break;
+      uint32_t none = 0;  // neighbours add no statistics
+      hw = u32x4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none), dec(hw.w, false, none)};
+    }
+    if (lane < 2 * cpr) {
+      u32x4 v = hw;
+      if (below ? !ext_b : !ext_a) {
+        const uint8_t *src = below ? (bot_clamp ? stage + t.rows * a.d : stage_all[wave + 1] + off0)
+                                   : (top_clamp ? stage + off0 : stage_all[wave - 1] + a.tr * a.d);
+        v = reinterpret_cast<const u32x4 *>(src)[l];
+      }
+      *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;
+    }
     wave_lds_sync();
   }
+  const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+  const bool dead = t.row0 < 0;
+  // item i: f = lane + 64 i, row f / per, chunk f % per; f / per as
+  // (f m) >> 16 with m = ceil(2^16 / per), exact since f (m - 2^16 / per) <
+  // 2^9 / 2^16 < 1 / per for f < 2^9, per <= 64
+  const uint32_t per = cpr * 16 / V;
+  const uint32_t m = uni((65536u + per - 1) / per);
+  // one straight-line body per case (a branch per item serialised its LDS reads)
+  auto phase2 = [&](auto interp_c) {
+    constexpr bool IP = decltype(interp_c)::value;
+#pragma unroll
+    for (int i = 0; i < NI2; ++i) {
+      if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
+      const uint32_t f = lane + kWave * i;
+      const uint32_t rr = __umul24(f, m) >> 16, c = f - rr * per;
+      const uint32_t r = min(rr, a.tr - 1);  // rows past the tile: stores dropped, reads in the tile
+      const uint8_t *row = stage + off0 + r * a.d + V * c;
+      uint32_t q[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < V / 4; ++k) {
+        const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+        if (IP) {
+          const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+          const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+          q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+        } else {
+          q[k] = v & 0x0F0F0F0Fu;
+        }
+      }
+      tile_store(os, (rr * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+    }
+  };
+  if (tile_dbl)
+    phase2(std::integral_constant<bool, true>{});
+  else
+    phase2(std::integral_constant<bool, false>{});
   if (STATS) {
     n1 = wave_sum(n1);
     n2 = wave_sum(n2);
@@ -820,16 +904,14 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
   }
 }
 
-// workgroups for `units` tiles: one pass over every tile in chunks, or the
-// persistent grid
-static unsigned tile_grid(uint32_t units, uint32_t chunk) {
-  if (chunk) return (unsigned)cdiv(cdiv(units, chunk), kTileWaves);
+// the Golay read's persistent grid: kShimTilePerCu workgroups per CU
+static unsigned tile_grid(uint32_t units) {
   return (unsigned)std::min<int64_t>(cdiv(units, kTileWaves), (int64_t)cu_count() * kShimTilePerCu);
 }
 
 template <typename TO>
 static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = tile_grid(a.units, 0);
+  const unsigned grid = tile_grid(a.units);
   constexpr unsigned pad = 0;
   if (a.stats && packed)
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), pad, st, a);
@@ -841,47 +923,34 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), pad, st, a);
 }
 
-// workgroups of `kern` resident per CU at `block` threads (registers, LDS),
-// at most `cap`: a persistent grid larger than what is resident runs its
-// excess after the first workgroups finish (the fp32-output interpolating read
-// takes 131 VGPRs: one 512-thread workgroup per CU, not kShimTilePerCu)
-static int resident_per_cu(const void *kern, int block, size_t lds, int cap) {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, block, lds) != hipSuccess || n < 1) return cap;
-  return std::min(n, cap);
-}
-
-template <typename TO, int CODEC, bool INTERP, bool STATS>
-static void launch_bytes_tiles_k(const ShimTileArgs &a, hipStream_t st) {
-  constexpr int kChunk = INTERP ? 0 : 1;  // interpolation: persistent; plain: full grid, one tile per wave
-  const auto kern = shim_read_bytes_tiles_kernel<TO, CODEC, INTERP, STATS, kChunk>;
-  const unsigned pad = kChunk ? kShimBytesLdsPad : 0u;  // caps the workgroups per CU
-  unsigned grid = tile_grid(a.units, kChunk);
-  if (!kChunk) {
-    static const int per_cu = resident_per_cu(reinterpret_cast<const void *>(kern), kTileBlock, pad, kShimTilePerCu);
-    grid = (unsigned)std::min<int64_t>(cdiv(a.units, kTileWaves), (int64_t)cu_count() * per_cu);
-  }
-  KVECC_LAUNCH(kern, dim3(grid), dim3(kTileBlock), pad, st, a);
-}
-
-template <typename TO, int CODEC, bool INTERP>
-static void launch_bytes_tiles_s(const ShimTileArgs &a, hipStream_t st) {
+// byte codecs: a full grid, one tile per wave; 16 KiB of dynamic LDS caps 4
+// workgroups per CU
+template <typename TO, int CODEC>
+static void launch_bytes_plain(const ShimTileArgs &a, hipStream_t st) {
+  const unsigned grid = (unsigned)cdiv(a.units, kTileWaves);
   if (a.stats)
-    launch_bytes_tiles_k<TO, CODEC, INTERP, true>(a, st);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, true>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad, st,
+                 a);
   else
-    launch_bytes_tiles_k<TO, CODEC, INTERP, false>(a, st);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, false>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad,
+                 st, a);
 }
 
 template <typename TO>
 static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
-  if (codec == KVECC_CODEC_H84 && interp)
-    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, true>(a, st);
-  else if (codec == KVECC_CODEC_H84)
-    launch_bytes_tiles_s<TO, KVECC_CODEC_H84, false>(a, st);
-  else if (codec == KVECC_CODEC_H74)
-    launch_bytes_tiles_s<TO, KVECC_CODEC_H74, false>(a, st);
-  else
-    launch_bytes_tiles_s<TO, KVECC_CODEC_NONE, false>(a, st);
+  if (codec == KVECC_CODEC_H84 && interp) {
+    const unsigned grid = (unsigned)cdiv(a.units, kTileWaves);
+    if (a.stats)
+      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad, st, a);
+    else
+      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad, st, a);
+  } else if (codec == KVECC_CODEC_H84) {
+    launch_bytes_plain<TO, KVECC_CODEC_H84>(a, st);
+  } else if (codec == KVECC_CODEC_H74) {
+    launch_bytes_plain<TO, KVECC_CODEC_H74>(a, st);
+  } else {
+    launch_bytes_plain<TO, KVECC_CODEC_NONE>(a, st);
+  }
 }
 
 }  // namespace kvecc
@@ -1075,8 +1144,7 @@ static int shim_read_impl(const void *k_cache, const void *v_cache, const float 
       a.tpb = (uint32_t)cdiv(block_size, a.tr);
       a.nlb = (uint32_t)cdiv(ctx, block_size);
       a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
-      a.dyn = shim_dyn_slot(stream);
-      if (!a.dyn) return KVECC_EHIP;
+      a.dyn = nullptr;  // full grids: no work counters
       switch (out_dtype) {
         case KVECC_F32: launch_bytes_tiles<float>(codec, interp, a, st); break;
         case KVECC_F16: launch_bytes_tiles<__half>(codec, interp, a, st); break;

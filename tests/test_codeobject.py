@@ -70,10 +70,10 @@ def test_no_spills_or_scratch(kernels):
 
 
 def test_fused_read_tiles_fit_two_workgroups_per_cu(kernels):
-    # shim_read_{bytes,golay}_tiles_kernel<__half | __hip_bfloat16, ...>
+    # shim_read_{bytes,golay}_tiles_kernel / shim_read_h84_interp_kernel <__half | __hip_bfloat16, ...>
     tiles = {k: v for k, v in kernels.items()
-             if re.search(r"shim_read_(bytes|golay)_tiles_kernelI(6__half|14__hip_bfloat16)", k)}
-    assert len(tiles) >= 20, sorted(tiles)
+             if re.search(r"shim_read_((bytes|golay)_tiles|h84_interp)_kernelI(6__half|14__hip_bfloat16)", k)}
+    assert len(tiles) >= 24, sorted(tiles)
     over = {k: v["vgpr"] for k, v in tiles.items() if v["vgpr"] + v["agpr"] > 128}
     assert not over, over
 
@@ -97,6 +97,8 @@ SHIPPED = [
     (r"shim_read_golay_tiles_kernelI6__half", 512, 32768 + 8 * (2304 + 256)),
     # fused byte-codec read: 512 threads, 8 x (2304 + 256) B (+16 KiB dynamic at launch)
     (r"shim_read_bytes_tiles_kernelI6__half", 512, 8 * (2304 + 256)),
+    # interpolating H(8,4) read: the same plus one "decoded" word per wave
+    (r"shim_read_h84_interp_kernelI6__half", 512, 8 * (2304 + 256 + 4)),
     # packed Golay decode wave tiles: 512 threads, 24 KiB tables + 8 x 3 KiB stage
     (r"golay_decode_packed_wave_kernel", 512, 24576 + 8 * 3072),
     # per-head rows register tiles: 512 threads

@@ -421,6 +421,10 @@ __global__ __launch_bounds__(kTileBlock) void bytes_read_ipwg_kernel(ShimTileArg
 //   4 + rows past the tile masked in phase 1 (statistics and LDS stores)
 //   5 + the start barrier and the per-wave "decoded" words (LDS, plain stores)
 //   6 + the neighbour-row exchange (the full kernel)
+//   7 levels 0-4, then a tile holding a double loads both neighbour rows from
+//     memory (synchronously; no barrier, no words, no exchange)
+//   8 levels 0-4, every tile's two neighbour rows issued with its own loads
+//     (asynchronous; decoded only by a tile holding a double)
 //   INC: phase 2 derives each item's (row, chunk) by a reciprocal multiply
 //   (one 24-bit multiply and a shift) instead of holding a divided (row,
 //   chunk) per item -- which the compiler, short of registers once the
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
   __shared__ uint32_t decoded[kTileWaves];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
-  if (LV >= 5) {
+  if (LV == 5 || LV == 6) {
     if (lane == 0) decoded[wave] = 0u;
     __syncthreads();
   }
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
   }
   uint32_t n1 = 0, n2 = 0;
   const uint32_t gw = blockIdx.x * kTileWaves + wave;
-  if (LV < 5 && gw >= a.units) return;
+  if ((LV < 5 || LV >= 7) && gw >= a.units) return;
   const bool active = gw < a.units;
   ShimTile t;
   t.rows = 0;
@@ -484,6 +488,25 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
       if (i * kWave >= (int)items) break;
       w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ir[i] * a.d + 16 * ic[i], 0, 2));
     }
+    // level 8: the two neighbour rows issued with the tile's loads (as round 3's
+    // persistent kernel prefetched them), decoded only if the tile needs them
+    u32x4 hw8{0u, 0u, 0u, 0u};
+    if (LV == 8 && t.rows > 0) {
+      const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
+      const bool below = lane >= cpr;
+      const uint32_t l = below ? lane - cpr : lane;
+      const uint32_t bh = uni(t.bh), b = bh / a.hkv, h = bh - b * a.hkv;
+      const uint32_t pa = uni(top_clamp ? 0u : t.pos0 - 1), pb = uni(bot_clamp ? 0u : t.pos0 + t.rows);
+      const int32_t ba = top_clamp ? -1 : ld_scalar(a.table + (int64_t)b * a.tstride + pa / a.bs);
+      const int32_t bb = bot_clamp ? -1 : ld_scalar(a.table + (int64_t)b * a.tstride + pb / a.bs);
+      const uint32_t pos = below ? pb : pa;
+      const int32_t blk = below ? bb : ba;
+      if (blk >= 0 && l < cpr && lane < 2 * cpr) {
+        const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - pos / a.bs * a.bs);
+        hw8 = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[side]) +
+                                                        row * a.d) + l);
+      }
+    }
     scale_all[wave][lane] = scale;
     bool dbl_any = false;
     auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
@@ -507,17 +530,36 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
       if (LV >= 4 ? real : ir[i] < a.tr) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
     }
     if (LV >= 1) tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+    if (LV == 8 && tile_dbl) {  // neighbours: decoded (clamped: the tile's own first / last row)
+      wave_lds_sync();
+      if (lane < 2 * cpr) {
+        const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
+        const bool below = lane >= cpr;
+        const uint32_t l = below ? lane - cpr : lane;
+        u32x4 v;
+        if (below ? bot_clamp : top_clamp) {
+          v = reinterpret_cast<const u32x4 *>(stage + off0 + (below ? t.rows - 1 : 0u) * a.d)[l];
+        } else {
+          uint32_t none = 0;
+          v = u32x4{dec(hw8.x, false, none), dec(hw8.y, false, none), dec(hw8.z, false, none),
+                    dec(hw8.w, false, none)};
+        }
+        *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;
+      }
+    }
   }
   wave_lds_sync();
-  if (LV >= 5 && lane == 0) __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if ((LV == 5 || LV == 6) && lane == 0)
+    __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (!active || t.rows == 0) return;
   if (LV >= 6 && tile_dbl) {
     const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
-    const bool ext_a = !top_clamp && wave == 0, ext_b = !bot_clamp && wave == kTileWaves - 1;
-    if (!top_clamp && !ext_a)
+    // level 7: both neighbour rows from memory, no exchange
+    const bool ext_a = !top_clamp && (LV == 7 || wave == 0), ext_b = !bot_clamp && (LV == 7 || wave == kTileWaves - 1);
+    if (LV == 6 && !top_clamp && !ext_a)
       while (__hip_atomic_load(&decoded[wave - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
-    if (!bot_clamp && !ext_b)
+    if (LV == 6 && !bot_clamp && !ext_b)
       while (__hip_atomic_load(&decoded[wave + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
     const bool below = lane >= cpr;
@@ -525,9 +567,12 @@ __global__ __launch_bounds__(kTileBlock) void bytes_ladder_kernel(ShimTileArgs a
     u32x4 hw{0u, 0u, 0u, 0u};
     if (ext_a || ext_b) {
       const uint32_t bh = uni(t.bh), b = bh / a.hkv, h = bh - b * a.hkv;
-      const uint32_t pos = uni(ext_a ? t.pos0 - 1 : t.pos0 + t.rows);
-      const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + pos / a.bs);
-      if (blk >= 0 && l < cpr && below == ext_b) {
+      const uint32_t pa = uni(ext_a ? t.pos0 - 1 : 0u), pb = uni(ext_b ? t.pos0 + t.rows : 0u);
+      const int32_t ba = ext_a ? ld_scalar(a.table + (int64_t)b * a.tstride + pa / a.bs) : -1;
+      const int32_t bb = ext_b ? ld_scalar(a.table + (int64_t)b * a.tstride + pb / a.bs) : -1;
+      const uint32_t pos = below ? pb : pa;
+      const int32_t blk = below ? bb : ba;
+      if (blk >= 0 && l < cpr && (below ? ext_b : ext_a)) {
         const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - pos / a.bs * a.bs);
         hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[uni(t.side)]) +
                                                        row * a.d) + l);
@@ -694,7 +739,7 @@ EXP_API int kvecc_exp_bytes_ladder(int level, BYTES_PARAMS) {
 #define LC(L) \
   case L: KVECC_LAUNCH((exp::bytes_ladder_kernel<L>), dim3(grid), dim3(kTileBlock), 16384u, st, a); break;   \
   case 10 + L: KVECC_LAUNCH((exp::bytes_ladder_kernel<L, true>), dim3(grid), dim3(kTileBlock), 16384u, st, a); break;
-    LC(0) LC(1) LC(2) LC(3) LC(4) LC(5) LC(6)
+    LC(0) LC(1) LC(2) LC(3) LC(4) LC(5) LC(6) LC(7) LC(8)
 #undef LC
     default: return set_error(KVECC_EINVAL, "ladder level");
   }
