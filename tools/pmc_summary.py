@@ -31,12 +31,11 @@ ALGO = {"golay_decode_kernel": 8 * M, "golay_encode_kernel": 7 * M,
         "shim_read_golay_tiles_kernel[int32]": 432 * 2 * (M // 43),
         "shim_read_golay_tiles_kernel[packed]": 389 * 2 * (M // 43),
         # fused shim read, Hamming(8,4) K+V token rows: 128 + 4 + 256 B
-        "shim_read_bytes_tiles_kernel[h84]": 388 * 2 * (M // 43),
-        "shim_read_bytes_tiles_kernel[h84+interp]": 388 * 2 * (M // 43)}
+        "shim_read_bytes_tiles_kernel": 388 * 2 * (M // 43),
+        "shim_read_h84_interp_kernel": 388 * 2 * (M // 43)}
 # kernels the bench launches in two configurations under one (truncated) name:
 # the first half of the launches is the first configuration
-SPLIT = {"shim_read_golay_tiles_kernel": ("[int32]", "[packed]"),
-         "shim_read_bytes_tiles_kernel": ("[h84]", "[h84+interp]")}
+SPLIT = {"shim_read_golay_tiles_kernel": ("[int32]", "[packed]")}
 
 
 def counters(path):
@@ -54,7 +53,7 @@ def counters(path):
 # fused-read variants traced one per run (tools/gpu_read_variants.sh): the
 # variant's algorithmic bytes per launch (K+V token rows of [8,4096,32,128])
 VARIANTS = {"golay": ("shim_read_golay_tiles_kernel", 432), "golay_packed": ("shim_read_golay_tiles_kernel", 389),
-            "hamming84": ("shim_read_bytes_tiles_kernel", 388), "hamming84_interp": ("shim_read_bytes_tiles_kernel", 388)}
+            "hamming84": ("shim_read_bytes_tiles_kernel", 388), "hamming84_interp": ("shim_read_h84_interp_kernel", 388)}
 
 
 def variants(src, dst):
