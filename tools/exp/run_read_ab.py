@@ -102,9 +102,8 @@ def main():
                     outs[i][0].data_ptr(), outs[i][1].data_ptr(), ops._DT[ODT], stats[i].data_ptr(), stream)
             assert rc == 0, (name, rc)
 
-        for i in range(len(handles)):  # WARMUP calls each: the clocks ramp for a few hundred ms
-            for _ in range(int(os.environ.get("WARMUP", "100"))):
-                call(i)
+        for i in range(len(handles)):
+            call(i)
         for s in stats:
             s.zero_()
         ok, ref = [], None
@@ -118,6 +117,12 @@ def main():
             ok.append(torch.equal(shared[0], ref[0]) and torch.equal(shared[1], ref[1])
                       and ops.read_stats(stats[i]) == ops.read_stats(stats[0]))
         del ref
+        # WARMUP back-to-back calls each right before the timed rounds: after any
+        # idle the clocks take ~40 launches (~6 ms) to settle for the full-grid
+        # H(8,4) reads (tools/exp/run_sustained.py, profiles/r04/fused/sustained.log)
+        for i in range(len(handles)):
+            for _ in range(int(os.environ.get("WARMUP", "100"))):
+                call(i)
         times = [[] for _ in handles]
         blk = int(os.environ.get("BLOCK", "1"))  # consecutive launches of one library before the next
         for r in range(0, ROUNDS, blk):
