@@ -130,8 +130,20 @@ def packed_vec(dev, pk):
             assert rc == 0
         return run
 
-    runs = [("product", prod), ("vec4_cu4", var(4, 4)), ("vec3_cu4", var(3, 4)), ("vec3_cu2", var(3, 2)),
-            ("vec3_u2_cu4", var(32, 4)), ("vec3_u3_cu4", var(33, 4)), ("vec3_u2_cu2", var(32, 2))]
+    runs = [("product", prod), ("vec3_cu4", var(3, 4)), ("vec3_cu2", var(3, 2))]
+    prev = os.environ.get("ATTN_PREV_LIB")  # the same kernels built from an earlier attention.hip
+    if prev:
+        pfn = ctypes.CDLL(os.path.abspath(prev)).kvecc_exp_paged_attention_packed
+        pfn.argtypes = pk.argtypes
+
+        def pvar(vec, per_cu):
+            def run():
+                rc = pfn(vec, per_cu, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), table.data_ptr(), lens.data_ptr(),
+                         ks.data_ptr(), vs.data_ptr(), out.data_ptr(), B, heads, kvh, D, blocks, BS, nb, CTX, sm,
+                         ws.data_ptr(), s)
+                assert rc == 0
+            return run
+        runs += [("prev_vec3_cu4", pvar(3, 4))]
     res = {}
     for _ in range(3):
         for lab, run in runs:
