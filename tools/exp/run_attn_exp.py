@@ -25,8 +25,8 @@ B, CTX, D, BS = 8, 4096, 128, 16
 # (label, G, per_cu, fused)
 VARIANTS = [("mfma_g1_cu4", 1, 4, 1), ("mfma_g1_cu2", 1, 2, 1), ("mfma_g1_cu8", 1, 8, 1),
             ("mfma_g1_cu4_nofuse", 1, 4, 0)]
-GQA_VARIANTS = [("mfma_g4_cu4", 4, 4, 0), ("mfma_g4_cu8", 4, 8, 0), ("mfma_g4_cu2", 4, 2, 0),
-                ("mfma_g2_cu4", 2, 4, 0)]
+GQA_VARIANTS = [("mfma_g4_cu4", 4, 4, 0), ("mfma_g4_cu4_fused", 4, 4, 1), ("mfma_g4_cu2_fused", 4, 2, 1),
+                ("mfma_g4_cu8_fused", 4, 8, 1)]
 
 
 def main():
