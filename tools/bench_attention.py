@@ -36,6 +36,11 @@ def main():
                     help="minimum warm-up time: the clocks take a few hundred ms to ramp on an idle GPU "
                          "(100 calls = 7 ms read 10-15 %% slow)")
     ap.add_argument("--passes", type=int, default=5, help="timed passes of --iters calls; the median is reported")
+    ap.add_argument("--data", choices=["random", "encoded"], default="random",
+                    help="cache contents: random bytes / int32 words (every codeword decodes through the full "
+                         "correction path: the decode tables' worst case), or encoded random INT4 values with "
+                         "bit errors at --ber (what a cache holds)")
+    ap.add_argument("--ber", type=float, default=None, help="encoded data: BER (default 1e-3 H84, 1e-2 Golay)")
     args = ap.parse_args()
     from kvecc import ops
     dev = torch.device("cuda:0")
@@ -48,8 +53,29 @@ def main():
     from kvecc.memory_layout import kv_cache_pair  # K/V as SimpleBlockManager lays them out
     kc, vc = kv_cache_pair((blocks, 1, args.kv_heads, args.bs * per),
                            torch.int32 if args.codec == "golay" else torch.uint8, dev)
-    kc.random_(0, 1 << 24 if args.codec == "golay" else 256, generator=g)
-    vc.copy_(kc.roll(1, 0))
+    if args.data == "random":
+        kc.random_(0, 1 << 24 if args.codec == "golay" else 256, generator=g)
+        vc.copy_(kc.roll(1, 0))
+    else:
+        ber = args.ber if args.ber is not None else (1e-3 if args.codec == "hamming84" else 1e-2)
+        for side, dst in enumerate((kc, vc)):
+            x = torch.randint(0, 16, (blocks, 1, args.kv_heads, args.bs, args.d), device=dev, generator=g,
+                              dtype=torch.uint8)
+            if args.codec == "hamming84":
+                cw = ops.hamming84_encode(x.view(-1))
+                ops.inject_into(cw, cw, ber, 8, seed=42 + side)
+                dst.view(-1).copy_(cw)
+            else:
+                gg = (args.d + 2) // 3
+                cw = ops.golay_encode_rows(x).view(-1)
+                ops.inject_into(cw, cw, ber, 24, seed=42 + side)
+                if args.codec == "golay":
+                    dst.view(-1).copy_(cw)
+                else:  # 3 bytes per codeword, rows padded to KVECC_GOLAY_PACKED_ROW
+                    b3 = torch.stack([(cw >> (8 * k)) & 0xFF for k in range(3)], -1).to(torch.uint8)
+                    dst.view(blocks, 1, args.kv_heads, args.bs, per)[..., :3 * gg].copy_(
+                        b3.view(blocks, 1, args.kv_heads, args.bs, 3 * gg))
+            del x
     ks = torch.rand(blocks, 1, args.kv_heads, args.bs, device=dev, generator=g)
     vs = torch.rand_like(ks)
     table = torch.randperm(blocks, device=dev, generator=g).to(torch.int32).view(args.batch, nb)
@@ -86,6 +112,7 @@ def main():
                       "ctx": args.ctx, "ms_per_call": ms, "bytes_per_call": bytes_,
                       "pass_ms": [round(x, 5) for x in passes],
                       "achieved_gbs": gbs, "hbm_frac": gbs / 8000.0,
+                      "data": args.data if args.data == "random" else f"encoded, BER {ber}",
                       "includes": "split kernel + combine kernel + workspace alloc"}))
 
 
