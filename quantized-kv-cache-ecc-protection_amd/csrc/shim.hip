@@ -790,8 +790,12 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTi
     if (lane < 2 * cpr) {
       u32x4 v = hw;
       if (below ? !ext_b : !ext_a) {
+        // the previous tile's last row: it holds tr rows, or, as the last
+        // chunk of the previous block (this tile starts a block), the block's
+        // remainder bs - (tpb - 1) tr
+        const uint32_t prev_rows = t.pos0 % a.bs ? a.tr : a.bs - (a.tpb - 1) * a.tr;
         const uint8_t *src = below ? (bot_clamp ? stage + t.rows * a.d : stage_all[wave + 1] + off0)
-                                   : (top_clamp ? stage + off0 : stage_all[wave - 1] + a.tr * a.d);
+                                   : (top_clamp ? stage + off0 : stage_all[wave - 1] + prev_rows * a.d);
         v = reinterpret_cast<const u32x4 *>(src)[l];
       }
       *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;

@@ -224,7 +224,10 @@ def test_hip_batch_read_vs_cpu(gpu, codec, batch, ctx, hkv, d, bs, dtype):
 
 
 INTERP_CASES = [(3, 70, 2, 64, 16), (2, 33, 2, 128, 16), (1, 1, 1, 16, 16), (2, 100, 3, 512, 4),
-                (2, 45, 2, 32, 7), (1, 17, 2, 128, 64), (2, 40, 2, 36, 8)]
+                (2, 45, 2, 32, 7), (1, 17, 2, 128, 64), (2, 40, 2, 36, 8),
+                # blocks that split into unequal tiles (the last chunk shorter): d 256 -> 7-row
+                # tiles of 16-row blocks (7, 7, 2); d 128 with 24-row blocks (16, 8)
+                (2, 100, 2, 256, 16), (2, 90, 2, 128, 24)]
 
 
 @pytest.mark.gpu
@@ -253,7 +256,8 @@ def test_hip_batch_read_interp_vs_cpu(gpu, batch, ctx, hkv, d, bs, dtype):
 # neighbours' rows; at 2e-2 every tile does, so every workgroup-boundary row
 # is read from memory and every inner one from a neighbour wave.
 MANY_TILE_CASES = [(4, 2001, 4, 32, 6, 2e-2), (3, 5000, 8, 128, 64, 2e-2), (2, 4099, 16, 64, 16, 1e-3),
-                   (3, 5000, 8, 128, 64, 1e-3), (4, 2001, 4, 32, 6, 3e-4), (2, 4099, 16, 128, 16, 0.0)]
+                   (3, 5000, 8, 128, 64, 1e-3), (4, 2001, 4, 32, 6, 3e-4), (2, 4099, 16, 128, 16, 0.0),
+                   (2, 3001, 4, 256, 16, 2e-2), (3, 2500, 4, 128, 24, 2e-2)]
 
 
 @pytest.mark.gpu
