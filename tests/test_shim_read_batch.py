@@ -278,6 +278,69 @@ def test_hip_batch_read_interp_many_tiles(gpu, batch, ctx, hkv, d, bs, ber):
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
 
 
+# random geometries (seeded): every head size the wave-tile kernels take
+# (d % 16 == 0, interpolation up to d = 512), block sizes that split into
+# equal and unequal tiles, partial last blocks, 1-3 layers, BER high enough
+# that most tiles hold doubles -- the byte reads, plain and interpolating,
+# against the host twin
+def _random_geometries(n, seed=2024):
+    import random
+    r = random.Random(seed)
+    out = []
+    for _ in range(n):
+        d = 16 * r.randint(1, 32)
+        bs = r.choice([1, 3, 4, 7, 8, 16, 24, 32, 40, 64])
+        ctx = r.randint(1, 12 * bs + 5)
+        out.append((r.randint(1, 3), ctx, r.randint(1, 3), d, bs, r.randint(1, 3), r.choice([True, False])))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,ctx,hkv,d,bs,layers,interp", _random_geometries(16))
+def test_hip_byte_read_random_geometry(gpu, batch, ctx, hkv, d, bs, layers, interp):
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache("hamming84", batch, ctx, hkv, d, bs, layers=layers, seed=ctx + d,
+                                       ber=3e-2)
+    layer = layers - 1
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, layer, "hamming84", torch.float16,
+                                     interp=interp, stats=st)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, layer, "hamming84", torch.float16,
+                               interp=interp, stats=gst)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
+def _random_golay_geometries(n, seed=4048):
+    import random
+    r = random.Random(seed)
+    out = []
+    for _ in range(n):
+        d = 8 * r.randint(1, 48)
+        bs = r.choice([1, 3, 4, 7, 8, 16, 24, 32, 40, 64])
+        ctx = r.randint(1, 12 * bs + 5)
+        out.append((r.choice(["golay", "golay_packed"]), r.randint(1, 3), ctx, r.randint(1, 3), d, bs,
+                    r.randint(1, 3)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,batch,ctx,hkv,d,bs,layers", _random_golay_geometries(12))
+def test_hip_golay_read_random_geometry(gpu, codec, batch, ctx, hkv, d, bs, layers):
+    """The Golay wave-tile read (d % 8 == 0) on random geometries against the host twin."""
+    from kvecc import cpu_ops, ops
+    kc, vc, ks, vs, table = make_cache(codec, batch, ctx, hkv, d, bs, layers=layers, seed=ctx + d)
+    layer = layers - 1
+    st, gst = cpu_ops.new_stats(), ops.new_stats(gpu)
+    ek, ev = cpu_ops.shim_read_batch(kc, vc, ks, vs, table, ctx, d, layer, codec, torch.float16, stats=st)
+    t = lambda x: x.to(gpu)  # noqa: E731
+    k, v = ops.shim_read_batch(t(kc), t(vc), t(ks), t(vs), t(table), ctx, d, layer, codec, torch.float16,
+                               stats=gst)
+    assert torch.equal(k.cpu(), ek) and torch.equal(v.cpu(), ev)
+    assert ops.read_stats(gst) == cpu_ops.read_stats(st)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("codec,interp,d", [("hamming84", False, 64), ("hamming84", True, 64),
                                             ("hamming74", False, 64), ("int4", False, 64),
