@@ -34,9 +34,18 @@ import torch  # noqa: E402
 PEAK = 8000.0  # GB/s
 
 
-def timed(fn, reps, warmup=100):
-    for _ in range(warmup):
+def timed(fn, reps, warmup=100, warmup_s=0.3):
+    # at least `warmup` calls and `warmup_s` seconds: after an idle set-up the
+    # clocks take a few hundred ms to ramp (100 calls of a 50-us kernel read
+    # 10-15 % slow; tools/bench_attention.py)
+    import time
+    t0 = time.perf_counter()
+    n = 0
+    while n < warmup or time.perf_counter() - t0 < warmup_s:
         fn()
+        n += 1
+        if n % 50 == 0:
+            torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     a.record()
