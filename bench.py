@@ -128,6 +128,20 @@ def cpu_baseline(budget_s, threads):
                       f"oracle/kvecc_oracle.c on {threads} host threads"}
 
 
+def _warm(fn, n, seconds=0.25):
+    """At least n calls of fn and `seconds` of them: after a set-up phase with
+    the GPU idle the clocks take a few hundred ms to ramp, and back-to-back
+    full-grid kernels run 10-30 % slow for their first ~40 launches
+    (profiles/r04/fused/sustained.log)."""
+    t0 = time.perf_counter()
+    k = 0
+    while k < n or time.perf_counter() - t0 < seconds:
+        fn()
+        k += 1
+        if k % 50 == 0:
+            torch.cuda.synchronize()
+
+
 def fused_decode_bench(dev, steps, warmup, packed=False):
     """The shim's fused Golay read (gather -> Golay decode -> dequantize -> fp16,
     ecc_shim.py:990-1071; kvecc_shim_read_batch's wave-tile kernel) over a paged
@@ -165,8 +179,7 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
         ops.shim_read_batch(caches[0], caches[1], scales[0], scales[1], table, L, D, 0, codec,
                             torch.float16, stats=st, out=outs)
 
-    for _ in range(warmup):
-        call()
+    _warm(call, warmup)
     evs = [ops.kernel_timer(dev) for _ in range(steps)]
     torch.cuda.synchronize()
     for k in range(steps):
@@ -186,7 +199,7 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
             "write_share": 2 * D / bytes_per_row,
             "ceiling_note": "write-heavy mix: non-temporal write-only streams peak at 4.8-5.3 TB/s and "
                             "read-only at 6.1-6.9 TB/s on MI355X (profiles/r02/hbm_ceiling.log)",
-            "timing": f"HIP events carried by the dispatch, mean of {steps} launches after {warmup} warm-up calls"}
+            "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} warm-up calls and >= 0.25 s"}
 
 
 def fused_h84_bench(dev, steps, warmup):
@@ -218,8 +231,7 @@ def fused_h84_bench(dev, steps, warmup):
         def call():
             ops.shim_read_batch(caches[0], caches[1], scales[0], scales[1], table, L, D, 0, "hamming84",
                                 torch.float16, stats=st, interp=interp, out=outs)
-        for _ in range(warmup):
-            call()
+        _warm(call, warmup)
         evs = [ops.kernel_timer(dev) for _ in range(steps)]
         torch.cuda.synchronize()
         for k in range(steps):
@@ -235,7 +247,7 @@ def fused_h84_bench(dev, steps, warmup):
     res.update({"workload": "shim_read_batch hamming84 -> fp16, [B=8,L=4096,Hkv=32,D=128] K+V, block_size 16, "
                             "BER 1e-3; plain and with double-error interpolation",
                 "kernel": "shim_read_bytes_tiles_kernel", "bytes_per_token_row": D + 4 + 2 * D,
-                "timing": f"HIP events carried by the dispatch, mean of {steps} launches after {warmup} warm-up calls"})
+                "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} warm-up calls and >= 0.25 s"})
     return res
 
 
@@ -250,9 +262,11 @@ def rows_bench(dev, x, noisy_rows, steps, warmup):
     nib = torch.empty(rows, D, dtype=torch.uint8, device=dev)
     st = ops.new_stats(dev)
     xr = x.view(rows, D)
-    for _ in range(warmup):
+    def pair():
         ops.golay_encode_rows_into(xr, cw)
         ops.golay_decode_rows_into(noisy_rows, nib, st)
+
+    _warm(pair, warmup)
     ev = [ops.kernel_timer(dev) + ops.kernel_timer(dev) for _ in range(steps)]
     torch.cuda.synchronize()
     for k in range(steps):
@@ -270,7 +284,7 @@ def rows_bench(dev, x, noisy_rows, steps, warmup):
             "hbm_gbs": {"encode": nbytes / (enc * 1e-3) / 1e9, "decode": nbytes / (dec * 1e-3) / 1e9},
             "frac": {"encode": nbytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "decode": nbytes / (dec * 1e-3) / 1e9 / HBM_PEAK_GBS},
-            "timing": f"HIP events carried by the dispatch, mean of {steps} launches after {warmup} warm-up calls"}
+            "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} warm-up calls and >= 0.25 s"}
 
 
 def cpu_quota():
@@ -554,9 +568,11 @@ def main():
         # HIP events carried by each kernel's own dispatch (as the other sections);
         # event markers between the launches read 2-4 us high
         pe = [ops.kernel_timer(dev) + ops.kernel_timer(dev) for _ in range(steps)]
-        for _ in range(side_warmup):
+        def pair():
             ops.golay_encode_packed_into(nib, cw3, m)
             ops.golay_decode_packed_into(noisy3, nib_out, flags, m, pst)
+
+        _warm(pair, side_warmup)
         torch.cuda.synchronize()
         for k in range(steps):
             ops.time_next_launch(pe[k][0], pe[k][1])
@@ -568,7 +584,7 @@ def main():
         p_dec = sum(e[2].elapsed_time(e[3]) for e in pe) / steps
         return {"layout": "3-byte codewords, INT4 nibbles two per byte (native, not the reference's)",
                 "timing": f"HIP events carried by the dispatches, mean of {steps} launches each after "
-                          f"{side_warmup} warm-up pairs",
+                          f">= {side_warmup} warm-up pairs and >= 0.25 s",
                 "codewords_per_s": m / ((p_enc + p_dec) * 1e-3),
                 "kernel_ms": {"encode": p_enc, "decode": p_dec},
                 "bytes_per_codeword": {"encode": 4.5, "decode": 4.625},
