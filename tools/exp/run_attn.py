@@ -1,4 +1,8 @@
-"""A/B: paged attention lane widths (tools/exp/libattn_v*.so built with other
+"""Historical (rounds 1-3): drives libattn_*.so builds of csrc/attention.hip with
+-DKVECC_ATTN_* switches, which round 4 removed (results: profiles/r01-r03/attention, attn).
+Round-4 attention experiments: tools/exp/attn_exp.hip + run_attn_exp.py.
+
+A/B: paged attention lane widths (tools/exp/libattn_v*.so built with other
 KVECC_ATTN_*_VEC) vs production libkvecc.so, interleaved, same inputs, both codecs.
 Build: make -C tools/exp libattn_v8.so libattn_v16.so libattn_u16.so   Run (GPU box): python tools/exp/run_attn.py"""
 import ctypes, math, os, statistics, sys

@@ -1,4 +1,7 @@
-"""GQA A/B for paged attention: the product library (workgroups share a cache
+"""Historical (round 3): drives libattn_<name>.so switch builds (removed in round 4;
+results in profiles/r03/attn). Round-4 experiments: tools/exp/attn_exp.hip + run_attn_exp.py.
+
+GQA A/B for paged attention: the product library (workgroups share a cache
 head across G query heads) against libattn_nogqa.so (KVECC_ATTN_GQA=0, one
 workgroup per query head), interleaved, on [B=8, ctx=4096, D=128] with 32
 query heads over 32 (MHA), 16 and 8 cache heads, every codec.  Times are

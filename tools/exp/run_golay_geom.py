@@ -1,4 +1,7 @@
-"""A/B: Golay encode/decode geometry variants (tools/exp/libgl_*.so) vs production, cold cache,
+"""Historical (round 1): drives libgl_*.so switch builds of csrc/golay.hip (removed in
+round 4; results in profiles/r01/golay).
+
+A/B: Golay encode/decode geometry variants (tools/exp/libgl_*.so) vs production, cold cache,
 interleaved.  Build: make -C tools/exp libgl_g1.so libgl_g1deep.so libgl_g2deep.so libgl_b256.so
 Env: LIBS (libgl_<name>.so list), WARM=1 (no cache flush between launches), ROUNDS."""
 import ctypes, os, statistics, sys

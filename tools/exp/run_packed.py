@@ -1,4 +1,7 @@
-"""A/B: packed Golay decode, production (LDS-staged) vs the direct 8-byte-load kernel
+"""Historical (round 1): drives libpk_direct.so, a switch build of csrc/packed.hip
+(removed in round 4). Round-4 experiments: tools/exp/packed_dec_exp.hip + run_packed_dec_exp.py.
+
+A/B: packed Golay decode, production (LDS-staged) vs the direct 8-byte-load kernel
 (libpk_direct.so), cold cache.
 Build: make -C tools/exp libpk_direct.so    Run (GPU box): python tools/exp/run_packed.py"""
 import ctypes, os, statistics, sys

@@ -1,4 +1,7 @@
-"""Per-wave start / exit times of the fused Golay read (a build with
+"""Historical (round 3): needs a -DKVECC_SHIM_WAVE_TIMES=1 build of csrc/shim.hip; round 4
+removed the switch (results in profiles/r03/fused/wave_times_*.log).
+
+Per-wave start / exit times of the fused Golay read (a build with
 -DKVECC_SHIM_WAVE_TIMES=1): how evenly the persistent grid's waves finish.
 usage: python tools/exp/run_wave_times.py libread_times.so"""
 import ctypes, os, sys
