@@ -435,6 +435,20 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   const int cs = live ? c : 0;
   const int64_t ws_stride = a.nsplit * (a.d + 2);  // per query head
   float *ws0 = a.ws + ((b * a.heads + h0) * a.nsplit + blockIdx.x) * (a.d + 2);
+  // this lane's query slice, issued before the block-table round trip (first
+  // used by the query sums after it)
+  float qv[G][E];
+  const float qscale = a.sm_scale * kAttnLogScale;
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int64_t di = (int64_t)c * E + e;
+      qv[j][e] = (live && di < a.d)
+                     ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h0 + j) * a.d + di]) * qscale
+                     : 0.0f;
+    }
+  }
 
   {  // block-table slice -> LDS (one load per logical block), then one 32-bit
      // division per token; none in the streaming loop
@@ -483,20 +497,12 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
     h84_decode4(threadIdx.x, q, t, n1, n2);
     lut[threadIdx.x] = (h84_lut_t)((int)(q & 0xFu) - 8);
   }
-  float qv[G][E];
-  const float qscale = a.sm_scale * kAttnLogScale;
   float qsum[G];  // sum of this lane's q (folds the decode's kOffset out of the K sums)
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     qsum[j] = 0.0f;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int64_t di = (int64_t)c * E + e;
-      qv[j][e] = (live && di < a.d)
-                     ? to_f32<T>(reinterpret_cast<const T *>(a.q)[(b * a.heads + h0 + j) * a.d + di]) * qscale
-                     : 0.0f;
-      qsum[j] += qv[j][e];
-    }
+    for (int e = 0; e < E; ++e) qsum[j] += qv[j][e];
   }
   __syncthreads();
 
@@ -762,6 +768,18 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
   const int64_t t0 = (int64_t)blockIdx.x * a.split;
   const int64_t t1 = min<int64_t>(t0 + a.split, ctx);
   const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
+  // Q^T operand (B): column n = head h0 + n, k-slot 8g + j of MFMA kk = d (D/4)g + 8kk + j.
+  // Issued first: it lands during the block-table round trip instead of
+  // after it (its first use, the query sum, precedes the first K/V loads)
+  f16x8 qop[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (n < G)
+      v = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const __half *>(a.q) +
+                                           (b * a.heads + h0 + n) * D + KB * g + 8 * kk);
+    qop[kk] = __builtin_bit_cast(f16x8, v);
+  }
   {  // block-table slice -> cache rows (-1: no block / past the split)
     const uint32_t bs = (uint32_t)a.bs;
     const uint32_t lb0 = (uint32_t)(t0 / a.bs);
@@ -790,16 +808,6 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_h84_mfma_kernel(AttnArgs
     uint32_t dq, dt, n1 = 0, n2 = 0;
     h84_decode4(threadIdx.x, dq, dt, n1, n2);  // kBlock == 256: one table entry per thread
     lut[threadIdx.x] = (uint8_t)(dq & 0xFu);
-  }
-  // Q^T operand (B): column n = head h0 + n, k-slot 8g + j of MFMA kk = d (D/4)g + 8kk + j
-  f16x8 qop[KK];
-#pragma unroll
-  for (int kk = 0; kk < KK; ++kk) {
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (n < G)
-      v = *reinterpret_cast<const u32x4 *>(reinterpret_cast<const __half *>(a.q) +
-                                           (b * a.heads + h0 + n) * D + KB * g + 8 * kk);
-    qop[kk] = __builtin_bit_cast(f16x8, v);
   }
   float qsum = 0.0f;  // sum of head n's query over all d (the offset fold)
 #pragma unroll
@@ -1012,6 +1020,22 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
   const int64_t t0 = (int64_t)blockIdx.x * a.split;
   const int64_t t1 = min<int64_t>(t0 + a.split, ctx);
   const int ntok = t1 > t0 ? (int)(t1 - t0) : 0;
+  // Q^T operand: k-slot v = 8kk + j of lane group g is d = KD g + v (v < KD, d < 128), else 0;
+  // issued before the block-table round trip, as in the H(8,4) kernel
+  f16x8 qop[KK];
+  {
+    const __half *qh = reinterpret_cast<const __half *>(a.q) + (b * a.heads + h0 + n) * D;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int v = 8 * kk + j, d = KD * g + v;
+        _Float16 x = 0;
+        if (n < G && v < KD && d < D) x = __builtin_bit_cast(_Float16, qh[d]);
+        qop[kk][j] = x;
+      }
+    }
+  }
   {  // block-table slice -> cache rows, as in the H(8,4) kernel
     const uint32_t bs = (uint32_t)a.bs;
     const uint32_t lb0 = (uint32_t)(t0 / a.bs);
@@ -1038,22 +1062,12 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
       rows[i] = row;
     }
   }
-  // Q^T operand: k-slot v = 8kk + j of lane group g is d = KD g + v (v < KD, d < 128), else 0
-  f16x8 qop[KK];
   float qsum = 0.0f;
   {
-    const __half *qh = reinterpret_cast<const __half *>(a.q) + (b * a.heads + h0 + n) * D;
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
+    for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int v = 8 * kk + j, d = KD * g + v;
-        _Float16 x = 0;
-        if (n < G && v < KD && d < D) x = __builtin_bit_cast(_Float16, qh[d]);
-        qop[kk][j] = x;
-        qsum += (float)x;
-      }
-    }
+      for (int j = 0; j < 8; ++j) qsum += (float)qop[kk][j];
     qsum += __shfl_xor(qsum, 16, kWave);
     qsum += __shfl_xor(qsum, 32, kWave);
   }
