@@ -65,10 +65,13 @@ constexpr uint32_t kRsrcWord3 = 0x00020000u;  // gfx9 raw buffer: 32-bit data fo
 // 4 codewords per lane (12 bytes, 3 aligned dwords, no realignment) left 5 of
 // 16 lanes idle: 68.0 vs 62.8 us per MHA call (profiles/r04/attn/packed_vec_ab.log)
 constexpr int kGolayPackedVec = 3;
-// Golay decodes through the spread tables (golay_attn_table_dev: 32-bit entries,
-// nibbles one per byte): per codeword 2 LDS reads + 9 VALU ops (address math,
-// one masked xor, three v_cvt_f32_ubyteN) instead of ~13 through the 16-bit
-// tables.  Hamming(8,4) decodes through a 256-entry LDS table of data(b) - 8
+// Golay decodes through the spread tables (golay_attn_x_table_dev: 32-bit
+// entries, nibbles one per byte, parity at the codeword's parity bits): per
+// codeword 2 LDS reads + 7 VALU ops (the first table's address, one masked xor
+// and a shift for the second's, one masked xor, three v_cvt_f32_ubyteN)
+// instead of ~13 through the 16-bit tables.  With the parity at bits 20-31
+// (golay_attn_table_dev, the shim's layout) the second address took 3 ops:
+// packed MHA main loop 393 -> 357 VALU per 4-row iteration.  Hamming(8,4) decodes through a 256-entry LDS table of data(b) - 8
 // as int8 (ds_read_i8 + v_cvt_f32_i32; the 256 bytes are 64 dwords over 32
 // banks, so random lookups conflict at most 2-way, where an fp32 table's 256
 // dwords conflict ~3.5-way: 60.6 vs 63.5 us per call on random caches).
@@ -96,7 +99,8 @@ struct AttnArgs {
   float sm_scale;
   float empty_value;          // output when a (b, h) has no valid token
   const uint16_t *par, *cor;  // Golay tables
-  const uint32_t *atab;       // Golay spread tables (golay_attn_table_dev)
+  const uint32_t *atab;       // Golay spread tables (golay_attn_table_dev): MFMA kernels
+  const uint32_t *atab_x;     // the split kernels' layout (golay_attn_x_table_dev)
   uint32_t *ctr;              // per-(batch, head group) split counters (attn_counter_slot), or
                               // null: a separate combine launch
 };
@@ -110,6 +114,8 @@ struct Chunk {
   // decode() returns (n - 8) + kOffset: the Golay path skips the subtraction
   // per element and the kernel folds -8 * kOffset into the sums instead
   static constexpr float kOffset = is_golay(CODEC) ? 8.0f : 0.0f;
+  // Golay: decode() returns value 3k + 2 of each codeword times 16
+  static constexpr bool kThird16 = is_golay(CODEC);
   uint32_t w[VEC];
   __device__ __forceinline__ void load_buf(const AttnArgs &a, __amdgpu_buffer_rsrc_t rs, int32_t row,
                                            int c) {
@@ -135,15 +141,17 @@ struct Chunk {
         const uint32_t off = (uint32_t)row * a.rowb + 12u * c;
         const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
         unpack3(v[0], v[1], v[2]);
-      } else {  // 9 bytes at 9c: the 3 dwords holding them, realigned
-        const uint32_t off = (uint32_t)row * a.rowb + 9u * c;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off & ~3u, 0, 0);
-        unpack9(v[0], v[1], v[2], off & 3u);
+      } else {  // 9 bytes at 9c: the 3 dwords holding them, realigned.  Rows
+                // are whole dwords (KVECC_GOLAY_PACKED_ROW), so the alignment
+                // is the lane's own constant, not recomputed per row
+        const uint32_t off = (uint32_t)row * a.rowb + ((9u * c) & ~3u);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+        unpack9(v[0], v[1], v[2], (9u * c) & 3u);
       }
     } else {
       const uint32_t off = ((uint32_t)row * (uint32_t)a.g + VEC * c) * 4u;
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0);
+      for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0) << 2;
     }
   }
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
@@ -174,23 +182,25 @@ struct Chunk {
     } else {
       const int32_t *p = reinterpret_cast<const int32_t *>(cache) + row * a.g;
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) w[k] = (uint32_t)p[min<int64_t>(VEC * c + k, a.g - 1)];
+      for (int k = 0; k < VEC; ++k) w[k] = (uint32_t)p[min<int64_t>(VEC * c + k, a.g - 1)] << 2;
     }
   }
-  // 4 little-endian 3-byte codewords from 3 dwords (golay_decode1 ignores bits 24-31)
+  // Golay words hold codeword << 2 (bits 0-1 and 26-31: neighbouring bytes,
+  // ignored by decode): the first table's byte offset is then one mask.
+  // 4 little-endian 3-byte codewords from 3 dwords
   __device__ __forceinline__ void unpack3(uint32_t d0, uint32_t d1, uint32_t d2) {
-    w[0] = d0;
-    w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbyte(d1, d0, 3);
-    w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbyte(d2, d1, 2);
-    w[3 < VEC ? 3 : 0] = d2 >> 8;
+    w[0] = d0 << 2;
+    w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbit(d1, d0, 22);
+    w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbit(d2, d1, 14);
+    w[3 < VEC ? 3 : 0] = d2 >> 6;
   }
   // 3 little-endian 3-byte codewords starting at byte `sh` (0-3) of 3 dwords
   __device__ __forceinline__ void unpack9(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t sh) {
     const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh), x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
     const uint32_t x2 = d2 >> (8 * sh);
-    w[0] = x0;
-    w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbyte(x1, x0, 3);
-    w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbyte(x2, x1, 2);
+    w[0] = x0 << 2;
+    w[1 < VEC ? 1 : 0] = __builtin_amdgcn_alignbit(x1, x0, 22);
+    w[2 < VEC ? 2 : 0] = __builtin_amdgcn_alignbit(x2, x1, 14);
   }
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
@@ -205,18 +215,23 @@ struct Chunk {
     } else {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
-        // P = spread(lo) | parity(lo) << 20; syndrome = (w >> 12) ^ parity,
-        // as a byte offset into the correction half: ((w >> 10) ^ (P >> 18)) & 0x3FFC
-        const uint32_t p = gtab[w[k] & 0xFFFu];
-        const uint32_t off = ((w[k] >> 10) ^ (p >> 18)) & 0x3FFCu;
+        // w = codeword << 2.  P = golay_attn_x_table_dev[lo] = nibbles 0, 1
+        // in bytes 0, 1, nibble 2 in bits 28-31, parity(lo) << 14 -- where w
+        // holds the received parity -- so the syndrome's byte offset into the
+        // correction half is ((w ^ P) & 0x3FFC000) >> 12: one v_bitop3
+        // (0x28 = (S0 ^ S1) & S2) and a shift
+        const uint32_t p = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab) + (w[k] & 0x3FFCu));
+        const uint32_t off = __builtin_amdgcn_bitop3_b32(w[k], p, 0x03FFC000u, 0x28) >> 12;
         const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab + 4096) + off);
-        // corrected nibbles, one per byte: (p ^ e) & 0x0F0F0F in one v_bitop3
-        // (0x28 = (S0 ^ S1) & S2); the conversions are written out because
-        // the compiler otherwise re-extracts each nibble with a shift and a mask
-        const uint32_t sp = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
+        // corrected nibbles: (p ^ e) & 0xF0000F0F; the conversions are written
+        // out because the compiler otherwise re-extracts each nibble with a
+        // shift and a mask.  The third value comes out as 16 n (byte 3 = n << 4):
+        // the kernel prescales its query slot by 1/16 and rescales its
+        // accumulator by 1/16 (kThirdScale; powers of two, so exact)
+        const uint32_t sp = __builtin_amdgcn_bitop3_b32(p, e, 0xF0000F0Fu, 0x28);
         asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(v[3 * k]) : "v"(sp));  // n, see kOffset
         asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(v[3 * k + 1]) : "v"(sp));
-        asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(v[3 * k + 2]) : "v"(sp));
+        asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(v[3 * k + 2]) : "v"(sp));  // 16 n
       }
     }
   }
@@ -479,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   }
   if (kSpread) {
     __syncthreads();  // blks (aliased) fully read
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab_x);
     u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
 #pragma unroll
     for (int i = threadIdx.x; i < 2048; i += kBlock) dst[i] = src[i];
@@ -503,6 +518,10 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
     qsum[j] = 0.0f;
 #pragma unroll
     for (int e = 0; e < E; ++e) qsum[j] += qv[j][e];
+    if (C::kThird16) {  // decode's 16 n in slots 3k + 2 (after the sum: it folds n - 8)
+#pragma unroll
+      for (int e = 2; e < E; e += 3) qv[j][e] *= 0.0625f;
+    }
   }
   __syncthreads();
 
@@ -639,8 +658,10 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
     if (j > 0) __syncthreads();  // the previous head's merge fully read red / gml / gw
     if (live) {
 #pragma unroll
-      for (int e = 0; e < E; ++e)
-        red[(grp * W + c) * E + e] = C::kOffset != 0.0f ? acc[j][e] - C::kOffset * psum[j] : acc[j][e];
+      for (int e = 0; e < E; ++e) {
+        const float ae = C::kThird16 && e % 3 == 2 ? acc[j][e] * 0.0625f : acc[j][e];  // 16 n slots
+        red[(grp * W + c) * E + e] = C::kOffset != 0.0f ? ae - C::kOffset * psum[j] : ae;
+      }
     }
     if (c == 0) {
       gml[0][grp] = m[j];
@@ -1073,7 +1094,10 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
   }
   __syncthreads();
 
-  // codeword -> data nibbles one per byte (bytes 0..2), uncorrectable words keep their data
+  // codeword -> data nibbles one per byte (bytes 0..2), uncorrectable words keep
+  // their data.  (The split kernels' table, parity at the codeword's parity
+  // bits and the nibbles in bytes 0, 1, 3, measured 1 % slower here:
+  // profiles/r04/attn/xtab_ab.log.)
   auto sp_of = [&](uint32_t c) -> uint32_t {
     const uint32_t p = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gt) + ((c << 2) & 0x3FFCu));
     const uint32_t off = ((c >> 10) ^ (p >> 18)) & 0x3FFCu;
@@ -1552,7 +1576,7 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
   if (a.nsplit > kMaxSplits)
     return set_error(KVECC_EINVAL, "paged_attention: context %lld too long", (long long)max_context_len);
   a.par = a.cor = nullptr;
-  a.atab = nullptr;
+  a.atab = a.atab_x = nullptr;
   a.ctr = nullptr;
   // fused combine for one query head per workgroup only (MHA 59.7 -> 58.9 us).
   // With G heads the tail after the last split -- the sc1 stores' acknowledgement,
@@ -1569,7 +1593,8 @@ KVECC_API int kvecc_paged_attention(const void *query, int q_dtype, const void *
     a.par = golay_parity_table_dev();
     a.cor = golay_correct_table_dev();
     a.atab = golay_attn_table_dev();
-    if (!a.par || !a.cor || !a.atab) return KVECC_EHIP;
+    a.atab_x = golay_attn_x_table_dev();
+    if (!a.par || !a.cor || !a.atab || !a.atab_x) return KVECC_EHIP;
   }
   hipStream_t st = as_stream(stream);
   if (gm) {

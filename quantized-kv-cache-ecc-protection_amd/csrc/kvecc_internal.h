@@ -38,6 +38,11 @@ const uint16_t *golay_correct_table_dev();
 //   [4096, 8192) spread(data error of syndrome s) | ((count(s) & 3) | unc << 6) << 24
 //                (count 0-3 bits corrected; uncorrectable: spread part 0, byte 3 = 0x40)
 const uint32_t *golay_attn_table_dev();
+// the attention split kernels' layout, for words holding codeword << 2: data
+// nibbles at bits 0-3, 8-11, 28-31 and parity(d) << 14 (where such a word holds
+// the received parity); correction half without the count byte (syndrome
+// offset = ((w ^ P) & 0x3FFC000) >> 12)
+const uint32_t *golay_attn_x_table_dev();
 // packed decode tables, 24 KiB: uint16 [4096] parity(lo) << 2, then uint32
 // [4096] error data | (bits corrected & 3) << 24 | uncorrectable << 31
 const uint8_t *golay_pk_table_dev();

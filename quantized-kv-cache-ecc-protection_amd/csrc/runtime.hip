@@ -43,6 +43,7 @@ static int g_cu[kMaxDev];
 static std::atomic<uint16_t *> g_parity[kMaxDev];
 static std::atomic<uint16_t *> g_correct[kMaxDev];
 static std::atomic<uint32_t *> g_attn[kMaxDev];
+static std::atomic<uint32_t *> g_attn_x[kMaxDev];
 static std::atomic<uint8_t *> g_pk[kMaxDev];
 
 int current_device() {
@@ -119,11 +120,13 @@ void build_golay_correct_table(uint16_t *out) {
 }
 
 static uint32_t spread12(uint32_t x) { return (x & 0xFu) | (x >> 4 & 0xFu) << 8 | (x >> 8 & 0xFu) << 16; }
+static uint32_t spread12x(uint32_t x) { return (x & 0xFu) | (x >> 4 & 0xFu) << 8 | (x >> 8 & 0xFu) << 28; }
 
 // All Golay device tables of a device in one allocation, built together the
 // first time any of them is needed (kvecc_init_device builds them eagerly, so
 // no upload ever happens inside a HIP-graph capture): parity[4096] and
-// correct[4096] as uint16, then the attention spread tables (uint32[8192]).
+// correct[4096] as uint16, then the attention spread tables (uint32[8192], two
+// layouts).
 // The pointers are published through atomics after the upload completes.
 static int ensure_tables(int d) {
   if (d < 0 || d >= kMaxDev) return set_error(KVECC_EINVAL, "device %d out of range", d);
@@ -132,6 +135,7 @@ static int ensure_tables(int d) {
   struct Host {
     uint16_t par[4096], cor[4096];
     uint32_t attn[8192];
+    uint32_t attn_x[8192];  // attention-only variant: parity at the codeword's parity bits
     uint16_t pk0[4096];  // packed decode: parity(lo) << 2 (byte offset of the syndrome's entry)
     uint32_t pk1[4096];  // packed decode: error data | (bits & 3) << 24 | uncorrectable << 31
   };
@@ -146,6 +150,12 @@ static int ensure_tables(int d) {
     // so a sum of byte 3 over up to 21 codewords keeps both fields apart
     const uint32_t n = host.cor[i] >> 12;  // 0-3 bits corrected, 4 = uncorrectable
     host.attn[4096 + i] = spread12(host.cor[i] & 0xFFFu) | ((n & 3u) | (n >> 2) << 6) << 24;
+    // the attention split kernels' variant, for words holding codeword << 2:
+    // data nibbles at bits 0-3, 8-11 and 28-31, parity(lo) at bits 14-25 --
+    // where such a word holds the received parity -- so the syndrome's byte
+    // offset is one masked XOR and a shift
+    host.attn_x[i] = spread12x(i) | (uint32_t)host.par[i] << 14;
+    host.attn_x[4096 + i] = spread12x(host.cor[i] & 0xFFFu);
     host.pk0[i] = (uint16_t)(host.par[i] << 2);
     host.pk1[i] = (host.cor[i] & 0xFFFu) | (n & 3u) << 24 | (n >> 2) << 31;
   }
@@ -161,6 +171,7 @@ static int ensure_tables(int d) {
   g_parity[d].store(buf->par, std::memory_order_release);
   g_correct[d].store(buf->cor, std::memory_order_release);
   g_pk[d].store(reinterpret_cast<uint8_t *>(buf->pk0), std::memory_order_release);
+  g_attn_x[d].store(buf->attn_x, std::memory_order_release);
   g_attn[d].store(buf->attn, std::memory_order_release);  // last: the "built" flag
   return KVECC_OK;
 }
@@ -176,6 +187,7 @@ static const P *table_dev(std::atomic<P *> *tabs) {
 const uint16_t *golay_parity_table_dev() { return table_dev(g_parity); }
 const uint16_t *golay_correct_table_dev() { return table_dev(g_correct); }
 const uint32_t *golay_attn_table_dev() { return table_dev(g_attn); }
+const uint32_t *golay_attn_x_table_dev() { return table_dev(g_attn_x); }
 const uint8_t *golay_pk_table_dev() { return table_dev(g_pk); }
 
 // ---- counter slots of the dynamically scheduled kernels -------------------------

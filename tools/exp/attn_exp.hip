@@ -75,6 +75,7 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_mfma(
   a.par = golay_parity_table_dev();
   a.cor = golay_correct_table_dev();
   a.atab = golay_attn_table_dev();
+  a.atab_x = golay_attn_x_table_dev();
   hipStream_t st = as_stream(stream);
   switch (G) {
     case 1: exp::launch_mfma_g<1>(codec, a, batch, st); break;
@@ -121,6 +122,7 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_packed(
   a.par = golay_parity_table_dev();
   a.cor = golay_correct_table_dev();
   a.atab = golay_attn_table_dev();
+  a.atab_x = golay_attn_x_table_dev();
   const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * heads));
   hipStream_t st = as_stream(stream);
   if (vec == 3)
