@@ -364,6 +364,40 @@ __global__ __launch_bounds__(kBlock) void paged_attn_combine_kernel(AttnArgs a) 
   combine_bh<T>(a, blockIdx.x, wt, bred);
 }
 
+// The combine for <= kCombineWaveSplits splits and head_dim <= 128: one
+// workgroup of two waves per (b, h), thread d owns output d.  Every wave folds
+// the splits' (m, l) itself -- lane s holds split s, the maximum and the
+// weighted sum by cross-lane reductions, the weights broadcast by readlane --
+// so the kernel has no LDS and no barrier between its one memory round trip
+// and its store.
+constexpr int kCombineWaveSplits = 16;
+template <typename T>
+__global__ __launch_bounds__(2 * kWave) void paged_attn_combine_wave_kernel(AttnArgs a) {
+  const int64_t bh = blockIdx.x, stride = a.d + 2;
+  const float *ws = a.ws + bh * a.nsplit * stride;
+  const int t = threadIdx.x, lane = t % kWave, ns = (int)a.nsplit;
+  float ov[kCombineWaveSplits];
+#pragma unroll
+  for (int s = 0; s < kCombineWaveSplits; ++s) ov[s] = t < a.d && s < ns ? ws[s * stride + 2 + t] : 0.0f;
+  const float ms = lane < ns ? ws[lane * stride] : -INFINITY;
+  const float ls = lane < ns ? ws[lane * stride + 1] : 0.0f;
+  float mx = ms;
+#pragma unroll
+  for (int off = kCombineWaveSplits / 2; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, kWave));
+  const float w = ms == -INFINITY ? 0.0f : attn_exp(ms - mx);
+  float L = w * ls;
+#pragma unroll
+  for (int off = kCombineWaveSplits / 2; off > 0; off >>= 1) L += __shfl_xor(L, off, kWave);
+  L = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, L)));
+  if (t < a.d) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int s = 0; s < kCombineWaveSplits; ++s)
+      acc += ov[s] * __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, w), s));
+    reinterpret_cast<T *>(a.out)[bh * a.d + t] = from_f32<T>(L > 0.0f ? acc / L : a.empty_value);
+  }
+}
+
 // Fused combine: the workgroup that finishes the last split of its (batch, head
 // group) -- counted on a.ctr[blockIdx.y] -- combines the group's G query heads
 // and resets the counter, saving the combine launch (the launcher uses it for
@@ -1300,7 +1334,10 @@ __global__ __launch_bounds__(kBlock, 2) void paged_attn_golay_mfma_kernel(AttnAr
 
 template <typename T>
 static void launch_combine(const AttnArgs &a, int64_t batch, hipStream_t st) {
-  KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
+  if (a.nsplit <= kCombineWaveSplits && a.d <= 2 * kWave)
+    KVECC_LAUNCH(paged_attn_combine_wave_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(2 * kWave), 0, st, a);
+  else
+    KVECC_LAUNCH(paged_attn_combine_kernel<T>, dim3((unsigned)(batch * a.heads)), dim3(kBlock), 0, st, a);
 }
 
 static int pow2_at_least(int64_t x) {
