@@ -85,8 +85,21 @@ def parse():
     ap.add_argument("--dist", action="store_true",
                     help="create the RCCL process group even at world size 1 (exercises the "
                          "barrier and the stats/timing all-reduces on one GPU)")
+    ap.add_argument("--no-interp", action="store_true", help="skip the interpolation roofline section")
+    ap.add_argument("--no-quant", action="store_true",
+                    help="skip the fused quantize+encode / decode+dequantize roofline section")
+    ap.add_argument("--no-pipeline", action="store_true", help="skip the encode+inject+decode pipeline")
+    ap.add_argument("--no-sections", action="store_true",
+                    help="headline only: skip every optional section and the CPU baselines")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
-    return ap.parse_args()
+    ap.add_argument("--inject-pmc-json", default=os.path.join(REPO, "profiles", "inject_valu.json"),
+                    help="VALU instructions per Philox (rocprofv3 SQ_INSTS_VALU pass) for the inject roofline")
+    a = ap.parse_args()
+    if a.no_sections:
+        for k in ("no_cpu_baseline", "no_inject", "no_packed", "no_fused", "no_rows", "no_interp",
+                  "no_quant", "no_pipeline"):
+            setattr(a, k, True)
+    return a
 
 
 def cpu_baseline(budget_s, threads):
@@ -140,6 +153,89 @@ def _warm(fn, n, seconds=0.25):
         k += 1
         if k % 50 == 0:
             torch.cuda.synchronize()
+
+
+def kernel_ms(dev, call, steps, warmup):
+    """Mean duration of the first kvecc kernel each call() launches, from HIP
+    events carried by that kernel's own dispatch (kvecc_time_next_launch), over
+    `steps` launches after the time-based warm-up."""
+    from kvecc import ops
+    _warm(call, warmup)
+    evs = [ops.kernel_timer(dev) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for k in range(steps):
+        ops.time_next_launch(*evs[k])
+        call()
+    torch.cuda.synchronize()
+    return sum(e[0].elapsed_time(e[1]) for e in evs) / steps
+
+
+def hbm_roofline(kernel, nbytes, ms, unit_note):
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": kernel, "kernel_ms": ms, "bytes_per_launch": nbytes,
+            "bytes_per_unit": unit_note, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS}
+
+
+def interp_bench(dev, steps, warmup):
+    """Double-error interpolation along L (interpolation_triton.py:120-265) of the
+    H(8,4) decode of [8,4096,32,128] at BER 1e-3 -- the tensor the config-5
+    hamming84_interp trial interpolates (each (b, h, d) column a sequence).
+    3 B per element (q and err in, out); the kernel alone, and the API call
+    (kvecc_interpolate_auto: the same pass records the no-double fast path)."""
+    from kvecc import ops
+    n = B * L * H * D
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(0, 16, (n,), generator=g, dtype=torch.uint8).to(dev)
+    cw = ops.hamming84_encode(x)
+    ops.inject_into(cw, cw, 1e-3, 8, seed=SEED)
+    q = torch.empty_like(x)
+    et = torch.empty_like(x)
+    ops.hamming84_decode_into(cw, q, et)
+    del cw, x
+    out = torch.empty_like(q)
+    ms = kernel_ms(dev, lambda: ops.interpolate_into(q, et, out, B, L, H * D), steps, warmup)
+    ms_api = kernel_ms(dev, lambda: ops.interpolate_auto_into(q, et, out, B, L, H * D), steps, warmup)
+    r = hbm_roofline("interp_vec_kernel<false>", 3 * n, ms, "3 B/element (q, err in; out)")
+    r.update({"workload": "interpolate_double_errors along L of the H(8,4) decode of [8,4096,32,128], BER 1e-3",
+              "doubles": int((et == 2).sum()),
+              "api": hbm_roofline("interp_vec_kernel<true> (kvecc_interpolate_auto)", 3 * n, ms_api,
+                                  "3 B/element"),
+              "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} "
+                        "warm-up calls and >= 0.25 s"})
+    return r
+
+
+def quant_bench(dev, steps, warmup):
+    """Fused quantize + Hamming(8,4) encode (fused_kernels.py:18-160) of fp16 rows
+    [8*4096*32, 128] (D*3+4 B/row: 2 B in and 1 B out per value, fp32 scale out),
+    and the fused H(8,4) decode + dequantize (fused_kernels.py:272-437) of those
+    codewords at BER 1e-3 back to fp16 (D*3+4 B/row) and fp32 (D*5+4 B/row)."""
+    from kvecc import _lib, ops
+    rows = B * L * H
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(rows, D, generator=g, dtype=torch.float32).to(dev).to(torch.float16)
+    cw = torch.empty(rows, D, dtype=torch.uint8, device=dev)
+    sc = torch.empty(rows, dtype=torch.float32, device=dev)
+    ms_q = kernel_ms(dev, lambda: ops.quantize_encode_rows_into(x, _lib.CODEC_H84, cw, sc), steps, warmup)
+    del x
+    ops.inject_into(cw.view(-1), cw.view(-1), 1e-3, 8, seed=SEED)
+    st = ops.new_stats(dev)
+    res = {"quantize_encode": hbm_roofline("quant_encode_kernel (fp16 -> H84)", rows * (3 * D + 4), ms_q,
+                                           "D*3+4 B/row (fp16 in, codeword + fp32 scale out)")}
+    for name, dt, per in (("decode_dequant", torch.float16, 3 * D + 4),
+                          ("decode_dequant_fp32", torch.float32, 5 * D + 4)):
+        out = torch.empty(rows, D, dtype=dt, device=dev)
+        ms = kernel_ms(dev, lambda: ops.decode_dequant_h84_into(cw, sc, out, True, st), steps, warmup)
+        res[name] = hbm_roofline(f"decode_dequant_h84_kernel (-> {str(dt)[6:]})", rows * per, ms,
+                                 f"{'D*3+4' if per == 3 * D + 4 else 'D*5+4'} B/row (codeword + scale in, "
+                                 f"{str(dt)[6:]} out)")
+        del out
+    res.update({"workload": f"fp16 rows [{rows}, {D}] = [8,4096,32,128] K, row absmax INT4, Hamming(8,4), "
+                            "BER 1e-3 between encode and decode",
+                "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} "
+                          "warm-up calls and >= 0.25 s"})
+    return res
 
 
 def fused_decode_bench(dev, steps, warmup, packed=False):
@@ -364,11 +460,18 @@ def cpu_backend_baseline(budget_s, threads):
 
 def main():
     args = parse()
+    # --gpus N > 1 without a launcher: start the N ranks as child processes
+    # (before anything here touches the GPU) and exit with their status
+    from kvecc import launch
+    rc = launch.launch_if_needed(os.path.abspath(__file__), sys.argv[1:], args.gpus, args.backend)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     # one GPU per rank; --backend gloo lets several ranks share one device to
     # rehearse the multi-rank path on a 1-GPU box (RCCL refuses that)
     ngpu = torch.cuda.device_count()
@@ -387,6 +490,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        launch.check_world(dist, args.gpus)
 
     import kvecc
     from kvecc import ops
@@ -473,11 +577,17 @@ def main():
         dec_ms = sum(e[1].elapsed_time(e[2]) for e in timed) / len(timed)
     tt = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
     st = ops.stats_totals(stats)
+    per_rank = [tt.tolist()]
+    world_info = {"backend": None, "world_size": 1}
     if dist is not None:
         if args.backend == "gloo":  # gloo reduces host tensors
             tt, st = tt.cpu(), st.cpu()
+        gathered = [torch.empty_like(tt) for _ in range(world)]
+        dist.all_gather(gathered, tt)                 # per-rank times, reported
+        per_rank = [g.tolist() for g in gathered]
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(st, op=dist.ReduceOp.SUM)     # the single stats all-reduce
+        world_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
     elapsed, enc_ms, dec_ms = tt.tolist()
     bits, unc = st.tolist()
 
@@ -507,18 +617,29 @@ def main():
 
     # ---- injection throughput (VALU-bound, Philox4x32-10 per bit) ------------
     def inject_section():
-        reps = 3
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ops.inject_into(cw, noisy, BER, 24, seed=SEED, global_n=m * world, offset0=rank * m)
-        e0.record()
-        for _ in range(reps):
-            ops.inject_into(cw, noisy, BER, 24, seed=SEED, global_n=m * world, offset0=rank * m)
-        e1.record()
-        torch.cuda.synchronize()
-        inj_ms = e0.elapsed_time(e1) / reps
-        return {"ms": round(inj_ms, 4), "codewords_per_s": m / (inj_ms * 1e-3),
-                "philox_per_s": m * 24 / (inj_ms * 1e-3), "flips": ops.read_stats(inj_stats)[0],
-                "bound": "valu"}
+        scratch = ops.new_stats(dev)
+        inj_ms = kernel_ms(dev, lambda: ops.inject_into(cw, noisy, BER, 24, seed=SEED, stats=scratch,
+                                                        global_n=m * world, offset0=rank * m), 10, 3)
+        philox = m * 24  # one Philox4x32-10 per bit (fault_injection_triton.py:303-334)
+        res = {"kernel": "inject_kernel<int32, 24> (with stats)", "ms": inj_ms,
+               "codewords_per_s": m / (inj_ms * 1e-3), "philox_per_s": philox / (inj_ms * 1e-3),
+               "flips": ops.read_stats(inj_stats)[0], "bound": "valu",
+               "timing": "HIP events carried by the dispatch, mean of 10 launches after >= 3 warm-up calls"}
+        # VALU roofline: wave-level VALU instructions per Philox from the committed
+        # SQ_INSTS_VALU pass (rocprofv3 cannot run inside this process) x the live
+        # Philox rate, against the full-rate issue peak (a wave64 VALU instruction
+        # takes 2 cycles of a SIMD-32: 256 CUs x 4 SIMDs x 2.4 GHz / 2)
+        peak = 256 * 4 * 2.4e9 / 2
+        if os.path.exists(args.inject_pmc_json):
+            with open(args.inject_pmc_json) as f:
+                pmc = json.load(f)
+            ipp = pmc["valu_insts_per_philox"]
+            achieved = philox / (inj_ms * 1e-3) * ipp
+            res["roofline"] = {"bound": "valu", "achieved": achieved, "peak": peak,
+                               "unit": "wave VALU instructions/s", "frac": achieved / peak,
+                               "valu_insts_per_philox": ipp, "source": pmc.get("source"),
+                               "valu_busy": pmc.get("valu_busy")}
+        return res
 
     inject = None if args.no_inject else optional("inject", inject_section)
 
@@ -549,7 +670,7 @@ def main():
                 "note": "the headline value excludes injection (done once, before timing); this is the "
                         "rate a Monte-Carlo trial sees"}
 
-    pipeline = optional("end_to_end_pipeline", pipeline_section)
+    pipeline = None if args.no_pipeline else optional("end_to_end_pipeline", pipeline_section)
 
     # ---- native packed layout (3-byte codewords, nibbles two per byte) -------
     # Same codewords, its own bytes/unit (4.5 B encode, 4.625 B decode); never
@@ -600,6 +721,10 @@ def main():
         return rows_bench(dev, xr, noisy_rows, max(args.steps, 10), side_warmup)
 
     rows = None if args.no_rows else optional("golay_rows", rows_section)
+    interp = None if args.no_interp else optional(
+        "interp", lambda: interp_bench(dev, max(args.steps, 10), side_warmup))
+    quant = None if args.no_quant else optional(
+        "fused_quant", lambda: quant_bench(dev, max(args.steps, 10), side_warmup))
 
     fused = None
     if not args.no_fused:
@@ -653,7 +778,13 @@ def main():
         "data": "synthetic: torch.randint(0,16) INT4 nibbles, seed=rank; BER 1e-2 Philox corruption",
         "config": {"workload": "golay24 per-head encode+decode, [B=8,L=4096,H=32,D=128] per GPU",
                    "codewords_per_gpu": m, "ber": BER, "seed": SEED, "parallelism": f"dp{world}",
-                   "global_batch": B * world, "seq_len": L},
+                   "global_batch": B * world, "seq_len": L,
+                   "process_group": world_info,
+                   "launcher": ("self (bench.py spawned its ranks)" if os.environ.get(launch.ENV_LAUNCHED) == "1"
+                                else "external (torchrun)" if world > 1 else "single process"),
+                   "per_rank": [{"rank": r, "elapsed_s": v[0], "encode_ms": v[1], "decode_ms": v[2],
+                                 "codewords_per_s": m * args.steps / v[0]}
+                                for r, v in enumerate(per_rank)]},
         "hbm_gbs": {"decode": dec_gbs, "encode": enc_gbs,
                     "round_trip": (DECODE_BYTES_PER_CW + ENCODE_BYTES_PER_CW) * m
                     / ((enc_ms + dec_ms) * 1e-3) / 1e9},
@@ -673,6 +804,8 @@ def main():
         "end_to_end_pipeline": pipeline,
         "fused_golay_decode": fused,
         "golay_rows": rows,
+        "interp": interp,
+        "fused_quant": quant,
         "packed": packed,
         "cpu_baseline": cpu,
         "cpu_backend": host,

@@ -87,14 +87,19 @@ KVECC_API int kvecc_init_device(int device);
  * combine).  No reference counterpart: the reference launches one program per
  * row and schedules nothing.  Each kernel needs its counters zero and to itself
  * while it runs, and leaves them zero.  The library gives eager launches one
- * counter slot per stream (per thread for hipStreamPerThread), and launches
- * captured into a graph a slot of their own per (capture, stream), so launches
- * that can overlap never share counters.  The first launch on a new stream
- * takes a slot from a pool that grows outside captures only;
- * kvecc_reserve_counter_slots(device, n) makes n slots available for the
- * captures to come (kvecc_init_device keeps a reserve of 32).  A graph keeps
- * its slots for every replay: replay one graph on one stream at a time (two
- * overlapping replays of the same graph would share counters). */
+ * counter slot per stream (per thread for hipStreamPerThread; keyed by the
+ * stream's address -- a stream created at a destroyed stream's address inherits
+ * its slot, safe because hipStreamDestroy drains the queue first), and
+ * launches captured into a graph a slot of their own per (capture, stream), so
+ * launches that can overlap never share counters.  Slots (48 KiB each) come
+ * from a pool that grows outside captures only: every eager launch of such a
+ * kernel tops the free list back up to 32 slots, so 32 captures can follow any
+ * eager launch; kvecc_reserve_counter_slots(device, n) makes n more available
+ * ahead of a longer run of captures.  A captured slot is tied to its graph by
+ * a HIP user object and returns to the pool when the graph and all its
+ * executable instances are destroyed.  A graph keeps its slots for every
+ * replay: replay one graph on one stream at a time (two overlapping replays of
+ * the same graph would share counters). */
 KVECC_API int kvecc_reserve_counter_slots(int device, int n);
 /* Diagnostic (synchronises the device): slots handed out, and how many counter
  * words of all slots are non-zero -- 0 whenever no launch is in flight. */

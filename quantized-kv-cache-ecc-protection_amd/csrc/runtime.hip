@@ -197,38 +197,89 @@ const uint8_t *golay_pk_table_dev() { return table_dev(g_pk); }
 // resets it).  Both hold by stream order if a slot is never shared between
 // launches that can overlap:
 //   - eager launches: one slot per stream (per thread for hipStreamPerThread),
-//     so consecutive users of a slot are ordered by their stream;
-//   - launches captured into a graph: a slot of their own per (capture, stream),
-//     never handed out again, so replays never share with eager work or with
-//     other graphs (replaying ONE graph concurrently with itself would race on
-//     its outputs anyway).
-// Slots come zeroed from a pool that grows outside captures only (a reserve of
-// kSlotReserve free slots is kept for them).
+//     so consecutive users of a slot are ordered by their stream.  A slot is
+//     keyed by the stream's address: a new stream created at a destroyed
+//     stream's address inherits its slot, which is safe because
+//     hipStreamDestroy drains the stream's queue before it returns (the old
+//     stream's launches are done).  (hipStreamGetId would tell the two apart,
+//     but it is a HIP 7.1 symbol and torch's HIP runtime here is 7.0);
+//   - launches captured into a graph: a slot of their own per (capture, stream).
+//     The slot is tied to the graph by a HIP user object: when the graph and
+//     every executable instance of it are gone (and their launches done) the
+//     runtime drops the last reference and the slot returns to the pool, zero
+//     (every launch left it so).  Replays never share with eager work or other
+//     graphs (replaying ONE graph concurrently with itself would race on its
+//     outputs anyway).
+// Slots come zeroed from a pool that grows outside captures only: every eager
+// call tops the free list back up to kSlotReserve slots, so up to that many
+// graphs can be captured between two eager launches (kvecc_reserve_counter_slots
+// for more).  Growth zeroes a new chunk on a private stream (no device-wide sync).
 struct SlotPool {
   std::mutex mu;
   std::vector<uint32_t *> free;                        // zeroed, never handed out
   std::unordered_map<uint64_t, uint32_t *> eager;      // stream key -> slot
   std::map<std::pair<uint64_t, unsigned long long>, uint32_t *> captured;  // (stream, capture id) -> slot
   std::vector<uint32_t *> chunks;
+  hipStream_t side = nullptr;                          // zeroes new chunks
+  // slots released by graph user objects: the runtime's destructor callback
+  // only appends here (its own lock, no HIP call under it); counter_slot moves
+  // them back to `free` under `mu`
+  std::mutex ret_mu;
+  std::vector<uint32_t *> returned;
 };
 static SlotPool g_pool[kMaxDev];
 constexpr int kSlotChunk = 64;    // slots per allocation (3 MiB)
 constexpr int kSlotReserve = 32;  // free slots kept for graph captures
 
 static int grow_pool(int d, SlotPool &p) {  // p.mu held; not during a capture
-  uint32_t *mem = nullptr;
-  const size_t bytes = sizeof(uint32_t) * (size_t)kSlotChunk * kSlotWords;
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
   if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
-  hipError_t e = hipMalloc(&mem, bytes);
-  if (e == hipSuccess) e = hipMemset(mem, 0, bytes);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
+  hipError_t e = hipSuccess;
+  {
+    uint32_t *mem = nullptr;
+    const size_t bytes = sizeof(uint32_t) * (size_t)kSlotChunk * kSlotWords;
+    if (!p.side) e = hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&mem, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(mem, 0, bytes, p.side);
+    if (e == hipSuccess) e = hipStreamSynchronize(p.side);
+    if (e == hipSuccess) {
+      p.chunks.push_back(mem);
+      for (int i = kSlotChunk - 1; i >= 0; --i) p.free.push_back(mem + (size_t)i * kSlotWords);
+    }
+  }
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return set_error(KVECC_EHIP, "counter slots: %s", hipGetErrorString(e));
-  p.chunks.push_back(mem);
-  for (int i = kSlotChunk - 1; i >= 0; --i) p.free.push_back(mem + (size_t)i * kSlotWords);
   return KVECC_OK;
+}
+
+// slots whose graphs are gone: back to the free list (p.mu held)
+static void drain_returned(SlotPool &p) {
+  std::vector<uint32_t *> back;
+  {
+    std::lock_guard<std::mutex> lk(p.ret_mu);
+    back.swap(p.returned);
+  }
+  for (uint32_t *s : back) {
+    for (auto it = p.captured.begin(); it != p.captured.end();)
+      it = it->second == s ? p.captured.erase(it) : std::next(it);
+    p.free.push_back(s);
+  }
+}
+
+struct SlotRelease {
+  int dev;
+  uint32_t *slot;
+};
+
+static void release_captured_slot(void *arg) {  // HIP user-object destructor
+  SlotRelease *r = static_cast<SlotRelease *>(arg);
+  SlotPool &p = g_pool[r->dev];
+  {
+    std::lock_guard<std::mutex> lk(p.ret_mu);
+    p.returned.push_back(r->slot);
+  }
+  delete r;
 }
 
 static int ensure_pool(int d) {
@@ -247,21 +298,28 @@ uint32_t *counter_slot(void *stream) {
   hipStream_t st = as_stream(stream);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long cid = 0;
-  if (hipStreamGetCaptureInfo(st, &cs, &cid) != hipSuccess) cs = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  if (hipStreamGetCaptureInfo_v2(st, &cs, &cid, &graph, nullptr, nullptr) != hipSuccess)
+    cs = hipStreamCaptureStatusNone;
   uint64_t key = reinterpret_cast<uint64_t>(stream);
   if (st == hipStreamPerThread)  // one handle, a different stream in every thread
     key = (uint64_t)std::hash<std::thread::id>{}(std::this_thread::get_id()) | (1ull << 63);
   SlotPool &p = g_pool[d];
   std::lock_guard<std::mutex> lk(p.mu);
+  drain_returned(p);
   const bool capturing = cs == hipStreamCaptureStatusActive;
   if (!capturing) {
+    // keep the reserve for captures topped up (allocation is illegal during one)
+    if (p.free.size() <= (size_t)kSlotReserve && grow_pool(d, p) != KVECC_OK) return nullptr;
     auto it = p.eager.find(key);
     if (it != p.eager.end()) return it->second;
-  } else {
-    auto it = p.captured.find({key, cid});
-    if (it != p.captured.end()) return it->second;
+    uint32_t *s = p.free.back();
+    p.free.pop_back();
+    p.eager.emplace(key, s);
+    return s;
   }
-  if (!capturing && p.free.size() <= (size_t)kSlotReserve && grow_pool(d, p) != KVECC_OK) return nullptr;
+  auto it = p.captured.find({key, cid});
+  if (it != p.captured.end()) return it->second;
   if (p.free.empty()) {
     set_error(KVECC_EHIP,
               "no free counter slot during graph capture (call kvecc_reserve_counter_slots before capturing)");
@@ -269,13 +327,20 @@ uint32_t *counter_slot(void *stream) {
   }
   uint32_t *s = p.free.back();
   p.free.pop_back();
-  if (!capturing) {
-    p.eager.emplace(key, s);
-  } else {
-    // a stream is in one capture at a time: its earlier captures' entries are done
-    for (auto it = p.captured.begin(); it != p.captured.end();)
-      it = it->first.first == key ? p.captured.erase(it) : std::next(it);
-    p.captured.emplace(std::make_pair(key, cid), s);
+  // a stream is in one capture at a time: its earlier captures' entries are done
+  for (auto jt = p.captured.begin(); jt != p.captured.end();)
+    jt = jt->first.first == key ? p.captured.erase(jt) : std::next(jt);
+  p.captured.emplace(std::make_pair(key, cid), s);
+  // tie the slot to the graph; without a graph handle or user objects it stays
+  // allocated for the process (the pre-round-5 behaviour)
+  if (graph) {
+    SlotRelease *r = new SlotRelease{d, s};
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, r, release_captured_slot, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+      delete r;
+    } else if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+      (void)hipUserObjectRelease(obj, 1);  // runs the destructor: the slot goes back
+    }
   }
   return s;
 }
@@ -317,6 +382,7 @@ KVECC_API int kvecc_reserve_counter_slots(int device, int n) {
     return set_error(KVECC_EINVAL, "reserve_counter_slots: bad device %d or count %d", device, n);
   SlotPool &p = g_pool[device];
   std::lock_guard<std::mutex> lk(p.mu);
+  drain_returned(p);
   while (p.free.size() < (size_t)n + kSlotReserve) {
     const int rc = grow_pool(device, p);
     if (rc != KVECC_OK) return rc;
@@ -331,6 +397,7 @@ KVECC_API int kvecc_counter_slots_check(int device, int64_t *slots_in_use, int64
     return set_error(KVECC_EINVAL, "counter_slots_check: bad argument");
   SlotPool &p = g_pool[device];
   std::lock_guard<std::mutex> lk(p.mu);
+  drain_returned(p);
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
     return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", device);

@@ -758,7 +758,10 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTi
     tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
   }
   wave_lds_sync();  // this wave's rows are in LDS before its word says so
-  if (lane == 0) __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // release / acquire at workgroup scope: the waiting wave's stage reads are
+  // ordered after the flag it spins on (in the memory model, not by accident of
+  // LDS ordering); both cost a waitcnt
+  if (lane == 0) __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (!active || t.rows == 0) return;
   if (tile_dbl) {  // wave-uniform: the neighbour rows into stage rows 0 and rows + 1
     const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
@@ -767,10 +770,10 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTi
     // the neighbour tiles exist (same sequence, inside the grid) and belong to
     // this workgroup, whose waves all publish: the waits end
     if (!top_clamp && !ext_a)
-      while (__hip_atomic_load(&decoded[wave - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      while (__hip_atomic_load(&decoded[wave - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
     if (!bot_clamp && !ext_b)
-      while (__hip_atomic_load(&decoded[wave + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+      while (__hip_atomic_load(&decoded[wave + 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
         __builtin_amdgcn_s_sleep(1);
     const bool below = lane >= cpr;
     const uint32_t l = below ? lane - cpr : lane;

@@ -21,6 +21,7 @@ from .ops import (fused_decode_dequantize_hamming84, fused_quantize_encode_hammi
                   inject_bit_errors_triton_vectorized, interpolate_double_errors,
                   interpolate_double_errors_1d, interpolate_double_errors_autotuned,
                   paged_attention_ecc)
+from . import torch_ops  # noqa: F401  -- registers torch.ops.kvecc.* (CPU + HIP kernels, fake kernels)
 
 __version__ = "0.1.0"
 

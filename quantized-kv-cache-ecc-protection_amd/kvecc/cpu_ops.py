@@ -482,30 +482,39 @@ SHIM_CODECS = {"int4": _lib.CODEC_NONE, "hamming74": _lib.CODEC_H74, "hamming84"
 
 def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0,
                scale_rule=None):
+    shim_write_tensors(k, v, manager.k_cache, manager.v_cache, manager.k_scales, manager.v_scales,
+                       manager.block_table[seq_id], manager.num_layers, manager.block_size,
+                       manager.num_kv_heads, manager.head_dim, layer, codec, n_bits, inject, ber, seed0,
+                       scale_rule)
+
+
+def shim_write_tensors(k, v, k_cache, v_cache, k_scales, v_scales, table, num_layers, block_size, hkv, d,
+                       layer, codec, n_bits, inject, ber, seed0, scale_rule=None):
     batch, seq = k.shape[0], k.shape[1]
     if k.dtype not in _DT or v.dtype != k.dtype:
         raise TypeError(f"unsupported K/V dtype {k.dtype}/{v.dtype}")
     _check_cpu(k)
     k, v = k.reshape(batch, seq, -1).contiguous(), v.reshape(batch, seq, -1).contiguous()
-    table = manager.block_table[seq_id]
-    _lib.call("kvecc_cpu_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq,
-              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec],
-              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), int(n_bits),
-              int(bool(inject)), float(ber), int(seed0), _ptr(manager.k_cache),
-              _ptr(manager.v_cache), _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table),
-              manager.num_layers, manager.block_size, int(layer), NUM_THREADS)
+    _lib.call("kvecc_cpu_shim_write", _ptr(k), _ptr(v), _DT[k.dtype], batch, seq, int(hkv), int(d),
+              SHIM_CODECS[codec], _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), int(n_bits),
+              int(bool(inject)), float(ber), int(seed0), _ptr(k_cache), _ptr(v_cache), _ptr(k_scales),
+              _ptr(v_scales), _ptr(table), int(num_layers), int(block_size), int(layer), NUM_THREADS)
 
 
 def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=0):
-    shape = (manager.num_kv_heads, ctx, manager.head_dim)
+    return shim_read_tensors(manager.k_cache, manager.v_cache, manager.k_scales, manager.v_scales,
+                             manager.block_table[seq_id], ctx, manager.num_kv_heads, manager.head_dim,
+                             manager.num_layers, manager.block_size, layer, codec, interp, out_dtype, stats)
+
+
+def shim_read_tensors(k_cache, v_cache, k_scales, v_scales, table, ctx, hkv, d, num_layers, block_size,
+                      layer, codec, interp, out_dtype, stats=None):
+    shape = (hkv, ctx, d)
     k_out = torch.empty(shape, dtype=out_dtype)
     v_out = torch.empty(shape, dtype=out_dtype)
-    table = manager.block_table[seq_id]
-    _lib.call("kvecc_cpu_shim_read", _ptr(manager.k_cache), _ptr(manager.v_cache),
-              _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table), int(ctx),
-              manager.num_kv_heads, manager.head_dim, manager.num_layers, manager.block_size,
-              int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
-              _DT[out_dtype], _ptr(stats), NUM_THREADS)
+    _lib.call("kvecc_cpu_shim_read", _ptr(k_cache), _ptr(v_cache), _ptr(k_scales), _ptr(v_scales), _ptr(table),
+              int(ctx), int(hkv), int(d), int(num_layers), int(block_size), int(layer), SHIM_CODECS[codec],
+              int(bool(interp)), _ptr(k_out), _ptr(v_out), _DT[out_dtype], _ptr(stats), NUM_THREADS)
     return k_out, v_out
 
 

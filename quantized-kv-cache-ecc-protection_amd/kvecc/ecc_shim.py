@@ -294,8 +294,14 @@ class ECCBackend:
         inject = cfg.inject_errors and cfg.ber > 0
         seed0 = cfg.seed + self._injection_count
         if self._fused_ok(k) and k.dtype == v.dtype:
-            self.codec_backend.shim_write(k, v, mgr, layer_idx, mgr.shim_codec, _N_BITS[cfg.codec],
-                                          inject, cfg.ber, seed0, seq_id, cfg.scale_rule)
+            if self._traced():  # torch.compile: the dispatcher operator (no graph break)
+                torch.ops.kvecc.shim_write(k, v, mgr.k_cache, mgr.v_cache, mgr.k_scales, mgr.v_scales,
+                                           mgr.block_table[seq_id], mgr.num_layers, mgr.block_size,
+                                           mgr.num_kv_heads, mgr.head_dim, layer_idx, mgr.shim_codec,
+                                           _N_BITS[cfg.codec], inject, cfg.ber, seed0, cfg.scale_rule)
+            else:
+                self.codec_backend.shim_write(k, v, mgr, layer_idx, mgr.shim_codec, _N_BITS[cfg.codec],
+                                              inject, cfg.ber, seed0, seq_id, cfg.scale_rule)
             if inject:
                 self._injection_count += rows
             return
@@ -335,6 +341,12 @@ class ECCBackend:
             mgr.view5(cache)[blk, layer_idx, :, slot, :] = enc[-1].to(cache.dtype)
         if inject:
             self._injection_count += rows
+
+    def _traced(self):
+        """True while torch.compile traces this backend and it is one whose
+        kernels are registered as torch.ops.kvecc operators (hip, cpu): calls
+        then go through the dispatcher, eager calls straight to the C ABI."""
+        return torch.compiler.is_compiling() and self.codec_backend.__name__ in ("kvecc.ops", "kvecc.cpu_ops")
 
     def _fused_ok(self, x=None):
         if not self.fused or self.config.codec not in self.FUSED_CODECS:
@@ -388,9 +400,15 @@ class ECCBackend:
         if self._fused_ok():
             # the reference's seq_len==1 Triton path (ecc_shim.py:791-800) keeps no statistics
             interp = cfg.use_interpolation and cfg.codec == "hamming84"
-            k_t, v_t = self.codec_backend.shim_read(
-                mgr, layer_idx, ctx, mgr.shim_codec, interp, torch.float32 if fast else q.dtype,
-                None if fast else self._stats, seq_id)
+            out_dtype, stats = (torch.float32, None) if fast else (q.dtype, self._stats)
+            if self._traced():
+                k_t, v_t = torch.ops.kvecc.shim_read(
+                    mgr.k_cache, mgr.v_cache, mgr.k_scales, mgr.v_scales, mgr.block_table[seq_id], ctx,
+                    mgr.num_kv_heads, mgr.head_dim, mgr.num_layers, mgr.block_size, layer_idx, mgr.shim_codec,
+                    interp, out_dtype, stats)
+            else:
+                k_t, v_t = self.codec_backend.shim_read(mgr, layer_idx, ctx, mgr.shim_codec, interp,
+                                                        out_dtype, stats, seq_id)
             if fast:
                 return self._decode_step_attention(q, k_t, v_t)
             return self._run_attention_hd(q, k_t, v_t)
@@ -423,6 +441,11 @@ class ECCBackend:
         q1 = q[:, :, 0, :].contiguous()
         table = mgr.block_table[seq_id].unsqueeze(0).expand(b, -1).contiguous()
         lens = torch.full((b,), ctx, dtype=torch.int32, device=q.device)
+        if self._traced():
+            out = torch.ops.kvecc.paged_attention(q1, mgr.k_cache, mgr.v_cache, table, lens, mgr.k_scales,
+                                                  mgr.v_scales, layer_idx, mgr.block_size, 1.0 / math.sqrt(d),
+                                                  "hamming84", ctx)
+            return out.unsqueeze(2)
         out = torch.empty_like(q1)
         self.codec_backend.paged_attention_into(
             q1, mgr.k_cache, mgr.v_cache, table, lens, mgr.k_scales, mgr.v_scales, out,

@@ -26,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 
@@ -359,16 +360,35 @@ def main(argv=None):
     ap.add_argument("--bers", type=float, nargs="*", default=[1e-4, 1e-3, 1e-2])
     ap.add_argument("--seeds", type=int, nargs="*", default=[42, 101, 997])
     ap.add_argument("--output", default=None)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without torchrun the sweep starts them itself")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process-group backend (nccl = RCCL; gloo lets ranks share one GPU)")
     args = ap.parse_args(argv)
+    from . import launch
+    gpus = args.gpus if args.gpus is not None else int(os.environ.get("WORLD_SIZE", "1"))
+    rc = launch.launch_if_needed(os.path.abspath(sys.argv[0]), list(sys.argv[1:] if argv is None else argv),
+                                 gpus, args.backend)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if world != gpus:
+        print(f"sweep: --gpus {gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    ngpu = torch.cuda.device_count()
+    local_dev = local % ngpu if args.backend == "gloo" and ngpu else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        launch.check_world(dist, gpus)
     cfg = MonteCarloConfig(shape=tuple(args.shape), codecs=tuple(args.codecs),
                            bers=tuple(args.bers), seeds=tuple(args.seeds), output=args.output)
     shard = HipShard(cfg, rank, world, dev)
@@ -376,7 +396,8 @@ def main(argv=None):
     if rank == 0:
         for r in rows:
             print(json.dumps(r))
-        print(json.dumps({"trials": len(rows), "seconds": elapsed, "world": world}))
+        print(json.dumps({"trials": len(rows), "seconds": elapsed, "world": world,
+                          "backend": dist.get_backend() if dist is not None else None}))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -635,20 +635,27 @@ def shim_write(k, v, manager, layer, codec, n_bits, inject, ber, seed0, seq_id=0
     hkv*d] or [batch, seq, hkv, d] -> quantize, encode, per-row inject, scatter
     into manager's caches.  Strided views whose head rows are contiguous are read
     in place (kvecc_shim_write_strided), anything else is made contiguous."""
+    shim_write_tensors(k, v, manager.k_cache, manager.v_cache, manager.k_scales, manager.v_scales,
+                       manager.block_table[seq_id], manager.num_layers, manager.block_size,
+                       manager.num_kv_heads, manager.head_dim, layer, codec, n_bits, inject, ber, seed0,
+                       scale_rule)
+
+
+def shim_write_tensors(k, v, k_cache, v_cache, k_scales, v_scales, table, num_layers, block_size, hkv, d,
+                       layer, codec, n_bits, inject, ber, seed0, scale_rule=None):
+    """shim_write on the cache tensors themselves (the torch.ops.kvecc.shim_write
+    kernel): table = the sequence's block-table row, int32 [max_blocks]."""
     batch, seq = k.shape[0], k.shape[1]
     if k.dtype not in _DT or v.dtype != k.dtype:
         raise TypeError(f"unsupported K/V dtype {k.dtype}/{v.dtype}")
-    hkv, d = manager.num_kv_heads, manager.head_dim
     k4 = _head_rows(k, batch, seq, hkv, d)
     v4 = _head_rows(v, batch, seq, hkv, d)
-    table = manager.block_table[seq_id]
     _lib.call("kvecc_shim_write_strided", _ptr(k4), _ptr(v4), k4.stride(0), k4.stride(1),
               k4.stride(2), v4.stride(0), v4.stride(1), v4.stride(2), _DT[k.dtype], batch, seq,
-              manager.num_kv_heads, manager.head_dim, SHIM_CODECS[codec],
-              _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE), int(n_bits),
-              int(bool(inject)), float(ber), int(seed0), _ptr(manager.k_cache),
-              _ptr(manager.v_cache), _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table),
-              manager.num_layers, manager.block_size, int(layer), _stream(k.device))
+              hkv, d, SHIM_CODECS[codec], _lib.scale_rule_code(scale_rule, DEFAULT_SCALE_RULE),
+              int(n_bits), int(bool(inject)), float(ber), int(seed0), _ptr(k_cache), _ptr(v_cache),
+              _ptr(k_scales), _ptr(v_scales), _ptr(table), int(num_layers), int(block_size), int(layer),
+              _stream(k.device))
 
 
 def _head_rows(x, batch, seq, hkv, d):
@@ -666,16 +673,21 @@ def _head_rows(x, batch, seq, hkv, d):
 def shim_read(manager, layer, ctx, codec, interp, out_dtype, stats=None, seq_id=0):
     """ECCBackend.attend decode side (ecc_shim.py:990-1071) -> K, V [hkv, ctx, d]
     in out_dtype (decode, optional H84 interpolation along ctx, dequantize)."""
-    dev = manager.k_cache.device
-    shape = (manager.num_kv_heads, ctx, manager.head_dim)
+    return shim_read_tensors(manager.k_cache, manager.v_cache, manager.k_scales, manager.v_scales,
+                             manager.block_table[seq_id], ctx, manager.num_kv_heads, manager.head_dim,
+                             manager.num_layers, manager.block_size, layer, codec, interp, out_dtype, stats)
+
+
+def shim_read_tensors(k_cache, v_cache, k_scales, v_scales, table, ctx, hkv, d, num_layers, block_size,
+                      layer, codec, interp, out_dtype, stats=None):
+    """shim_read on the cache tensors themselves (the torch.ops.kvecc.shim_read kernel)."""
+    dev = k_cache.device
+    shape = (hkv, ctx, d)
     k_out = torch.empty(shape, dtype=out_dtype, device=dev)
     v_out = torch.empty(shape, dtype=out_dtype, device=dev)
-    table = manager.block_table[seq_id]
-    _lib.call("kvecc_shim_read", _ptr(manager.k_cache), _ptr(manager.v_cache),
-              _ptr(manager.k_scales), _ptr(manager.v_scales), _ptr(table), int(ctx),
-              manager.num_kv_heads, manager.head_dim, manager.num_layers, manager.block_size,
-              int(layer), SHIM_CODECS[codec], int(bool(interp)), _ptr(k_out), _ptr(v_out),
-              _DT[out_dtype], _sptr(stats, dev), _stream(dev))
+    _lib.call("kvecc_shim_read", _ptr(k_cache), _ptr(v_cache), _ptr(k_scales), _ptr(v_scales), _ptr(table),
+              int(ctx), int(hkv), int(d), int(num_layers), int(block_size), int(layer), SHIM_CODECS[codec],
+              int(bool(interp)), _ptr(k_out), _ptr(v_out), _DT[out_dtype], _sptr(stats, dev), _stream(dev))
     return k_out, v_out
 
 

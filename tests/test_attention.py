@@ -91,8 +91,8 @@ CASES = [("hamming84", 2, 4, 4, 64, 300, 0.01), ("hamming84", 1, 12, 12, 64, 102
          # queries: the matrix-core kernel; fp32: the VALU kernels)
          ("hamming84", 2, 16, 2, 64, 257, 0.01), ("hamming84", 1, 32, 2, 128, 1000, 0.01),
          ("hamming84", 2, 8, 4, 32, 100, 0.0),
-         # MHA at head_dim 128 (fp16 queries: the matrix-core kernel at one head per workgroup)
-         ("hamming84", 2, 8, 8, 128, 700, 0.01)]
+         # MHA at head_dim 128 / 32 (fp16 queries: the matrix-core kernel at one head per workgroup)
+         ("hamming84", 2, 8, 8, 128, 700, 0.01), ("hamming84", 2, 4, 4, 32, 300, 0.01)]
 
 
 @pytest.mark.parametrize("codec,batch,heads,kvh,d,ctx,ber", CASES)

@@ -1,0 +1,82 @@
+"""bench.py / tools/sweep.py start their own ranks on a GPU box (kvecc.launch).
+
+On a one-GPU box two ranks share cuda:0 over gloo (RCCL refuses two ranks on
+one device); the JSON line must report the world the process group itself
+reports.  Asking for more GPUs than the box has fails before any rank starts.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    from kvecc import launch
+    return {k: v for k, v in os.environ.items()
+            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", launch.ENV_LAUNCHED)}
+
+
+def _json_line(stdout):
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_spawns_two_gloo_ranks(gpu):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--steps", "10", "--warmup", "2", "--no-cpu-baseline", "--no-inject", "--no-packed",
+                        "--no-fused", "--no-rows", "--roofline-samples", "2", "--no-sections"],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 2
+    assert line["config"]["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert line["config"]["launcher"].startswith("self")
+    ranks = line["config"]["per_rank"]
+    assert [p["rank"] for p in ranks] == [0, 1]
+    assert all(p["decode_ms"] > 0 and p["encode_ms"] > 0 for p in ranks)
+    # value = every rank's codewords over the slowest rank's time
+    m = line["config"]["codewords_per_gpu"]
+    slowest = max(p["elapsed_s"] for p in ranks)
+    assert line["value"] == pytest.approx(2 * m * line["steps"] / slowest, rel=1e-6)
+    # the decode statistics are the all-reduced sum of both shards
+    assert line["decode_stats"]["bits_corrected"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_more_gpus_than_the_box_fails(gpu):
+    import torch
+    n = torch.cuda.device_count() + 1
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=_env())
+    assert r.returncode != 0
+    assert f"needs {n} GPUs" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_sweep_spawns_two_gloo_ranks_equal_to_one(gpu, tmp_path):
+    """tools/sweep.py --gpus 2 (spawned, gloo, sharing cuda:0) gives the single-rank table."""
+    args = ["--shape", "4", "64", "4", "32", "--codecs", "hamming84_interp", "golay",
+            "--bers", "1e-2", "--seeds", "42"]
+    one = subprocess.run([sys.executable, os.path.join(REPO, "tools", "sweep.py"), *args],
+                         capture_output=True, text=True, timeout=180, env=_env())
+    assert one.returncode == 0, one.stderr[-3000:]
+    two = subprocess.run([sys.executable, os.path.join(REPO, "tools", "sweep.py"), "--gpus", "2",
+                          "--backend", "gloo", *args], capture_output=True, text=True, timeout=180, env=_env())
+    assert two.returncode == 0, two.stderr[-3000:]
+
+    def rows(out):
+        rs = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+        return [r for r in rs if "key" in r], rs[-1]
+
+    r1, s1 = rows(one.stdout)
+    r2, s2 = rows(two.stdout)
+    assert s1["world"] == 1 and s2["world"] == 2 and s2["backend"] == "gloo"
+    assert r1 == r2 and len(r1) == 2

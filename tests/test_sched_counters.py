@@ -145,3 +145,57 @@ def test_counter_slots_check_api(gpu):
     used, nonzero = ops.counter_slots_check(gpu)
     assert used >= 0 and nonzero == 0
     ops.reserve_counter_slots(4, gpu)
+
+
+def test_many_captures_on_one_stream_and_slot_release(gpu):
+    """A serving loop's pattern: warm up eagerly, capture, repeat -- 80 graphs on
+    one stream, all alive at once, with no kvecc_reserve_counter_slots call (the
+    eager launches keep the capture reserve topped up).  Every graph's slot is
+    its own while the graph lives, every replay is exact, and the slots return
+    to the pool when the graphs are destroyed (HIP user objects)."""
+    import gc
+    import time
+
+    from kvecc import ops
+    dev = gpu
+    work = _workloads(dev)
+    run, mk, _ = work["golay_rows"]
+    base, st = mk(), ops.new_stats(dev)
+    run(base, st)
+    torch.cuda.synchronize()
+    base_st = ops.read_stats(st)
+    s = torch.cuda.Stream(dev)
+    out = mk()
+    used0, _ = ops.counter_slots_check(dev)
+    graphs, gstats = [], []
+    for i in range(80):
+        with torch.cuda.stream(s):
+            run(out, ops.new_stats(dev))  # eager warm-up on the capture stream
+        g, gs = torch.cuda.CUDAGraph(), ops.new_stats(dev)
+        with torch.cuda.graph(g, stream=s):
+            run(out, gs)
+        graphs.append(g)
+        gstats.append(gs)
+    torch.cuda.synchronize()
+    used1, nz = ops.counter_slots_check(dev)
+    assert nz == 0 and used1 >= used0 + 80, (used0, used1)
+    for g, gs in zip(graphs, gstats):
+        gs.zero_()
+        for t in out:
+            t.zero_()
+        with torch.cuda.stream(s):
+            g.replay()
+        torch.cuda.synchronize()
+        assert _same(out, base) and ops.read_stats(gs) == base_st
+    del graphs, g
+    gc.collect()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    used2 = used1
+    while time.time() - t0 < 5:
+        used2, nz = ops.counter_slots_check(dev)
+        if used2 <= used0 + 1:
+            break
+        time.sleep(0.1)
+    assert nz == 0
+    assert used2 <= used0 + 1, f"captured slots not returned: {used0} before, {used1} alive, {used2} after"

@@ -1,0 +1,154 @@
+"""torch.ops.kvecc: the codec path registered with the torch dispatcher
+(kvecc/torch_ops.py).  Each operator has a HIP (CUDA dispatch key) and a CPU
+kernel plus a fake kernel; torch.compile(fullgraph=True) must trace
+encode -> inject -> decode and a patched GPT-2 attention forward with no graph
+break and give the eager bits.  CPU cases run here; the `gpu` cases run the
+HIP kernels on the GPU box."""
+
+import pytest
+import torch
+
+import kvecc  # noqa: F401  -- registers the operators
+from kvecc import torch_ops
+
+OPS = torch.ops.kvecc
+
+
+def test_every_operator_registered():
+    for name in torch_ops.OPS:
+        op = getattr(OPS, name).default
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "CPU"), name
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(op.name(), "CUDA"), name
+
+
+def _pipeline(x):
+    """H(8,4) and Golay encode -> inject -> decode, and interpolation, all operators."""
+    cw = OPS.hamming84_encode(x)
+    noisy, ist = OPS.inject_bit_errors(cw, 1e-2, 8, 42)
+    d, et, st = OPS.hamming84_decode(noisy)
+    r = OPS.interpolate_double_errors(d, et, 1)
+    rows = OPS.golay_encode_rows(x)
+    gn, gst = OPS.inject_bit_errors(rows, 1e-2, 24, 7)
+    dr, drs = OPS.golay_decode_rows(gn, x.shape[-1])
+    trip = x.reshape(-1, 2)[:, :1].expand(-1, 3).contiguous()
+    g = OPS.golay_encode(trip)
+    gn2, _ = OPS.inject_bit_errors(g, 5e-2, 24, 3)
+    t, c, gs = OPS.golay_decode(gn2)
+    return d, et, st, r, ist, dr, drs, gst, t, c, gs
+
+
+def _check_pipeline(device):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 16, (2, 48, 3, 20), generator=g, dtype=torch.uint8).to(device)
+    eager = _pipeline(x)
+    torch._dynamo.reset()
+    comp = torch.compile(_pipeline, fullgraph=True, backend="aot_eager")(x)
+    for a, b in zip(eager, comp):
+        assert a.dtype == b.dtype and a.shape == b.shape and torch.equal(a, b)
+    # the operators agree with the reference-named API of the same backend
+    be = kvecc.get_codec_backend("hip" if device.type == "cuda" else "cpu")
+    cw = be.inject_bit_errors_triton(be.hamming84_encode(x), 1e-2, 8, 42)
+    d, et, (corr, det) = be.hamming84_decode(cw, return_error_types=True)
+    assert torch.equal(d, eager[0]) and torch.equal(et, eager[1]) and eager[2].tolist() == [corr, det]
+    assert eager[2].tolist()[0] > 0 and eager[4].tolist()[0] > 0 and eager[10].tolist()[0] > 0
+
+
+def test_pipeline_compiles_cpu():
+    _check_pipeline(torch.device("cpu"))
+
+
+@pytest.mark.gpu
+def test_pipeline_compiles_hip(gpu):
+    _check_pipeline(gpu)
+
+
+def test_fake_shapes():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    with FakeTensorMode():
+        cw = torch.empty(10, dtype=torch.int32)
+        t, c, s = OPS.golay_decode(cw)
+        assert (t.shape, t.dtype, c.shape, c.dtype, s.shape) == ((10, 3), torch.uint8, (10,), torch.uint8, (2,))
+        assert OPS.golay_encode(torch.empty(7, 3, dtype=torch.uint8)).shape == (7,)
+        assert OPS.golay_encode_rows(torch.empty(2, 5, 128, dtype=torch.uint8)).shape == (2, 5, 43)
+        x = torch.empty(4, 64, dtype=torch.float16)
+        q, sc = OPS.fused_quantize_encode(x, "hamming84", None)
+        assert q.dtype == torch.uint8 and q.shape == (4, 64) and sc.shape == (4,) and sc.dtype == torch.float32
+        o, n = OPS.fused_decode_dequantize_hamming84(q, sc, torch.float16)
+        assert o.dtype == torch.float16 and o.shape == (4, 64) and n.shape == (1,)
+        d, et, st = OPS.hamming84_decode(torch.empty(3, 5, dtype=torch.uint8))
+        assert d.shape == et.shape == (3, 5) and st.shape == (2,)
+
+
+def test_opcheck_cpu():
+    """torch.library.opcheck: schema, fake kernel and dispatch consistency."""
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 16, (64,), generator=g, dtype=torch.uint8)
+    cw = OPS.hamming84_encode(x)
+    checks = ("test_schema", "test_faketensor")
+    torch.library.opcheck(OPS.hamming84_encode.default, (x,), test_utils=checks)
+    torch.library.opcheck(OPS.hamming84_decode.default, (cw,), test_utils=checks)
+    torch.library.opcheck(OPS.inject_bit_errors.default, (cw, 0.05, 8, 1), test_utils=checks)
+    torch.library.opcheck(OPS.inject_bit_errors_.default, (cw.clone(), 0.05, 8, 1), test_utils=checks)
+    trip = torch.randint(0, 16, (32, 3), generator=g, dtype=torch.uint8)
+    torch.library.opcheck(OPS.golay_encode.default, (trip,), test_utils=checks)
+    torch.library.opcheck(OPS.golay_decode.default, (OPS.golay_encode(trip),), test_utils=checks)
+    xf = torch.randn(6, 32, generator=g)
+    torch.library.opcheck(OPS.fused_quantize_encode.default, (xf, "hamming84", "div7"), test_utils=checks)
+
+
+def test_inplace_inject_matches_copy():
+    g = torch.Generator().manual_seed(2)
+    x = torch.randint(0, 1 << 24, (1000,), generator=g, dtype=torch.int32)
+    out, st = OPS.inject_bit_errors(x, 0.02, 24, 5)
+    y = x.clone()
+    st2 = OPS.inject_bit_errors_(y, 0.02, 24, 5)
+    assert torch.equal(y, out) and torch.equal(st, st2)
+    # sharded in place: the two halves draw the unsharded stream
+    z = x.clone()
+    OPS.inject_bit_errors_(z[:500], 0.02, 24, 5, 1000, 0)
+    OPS.inject_bit_errors_(z[500:], 0.02, 24, 5, 1000, 500)
+    assert torch.equal(z, out)
+
+
+def _gpt2_attention(device, codec, interp, seq):
+    from transformers import GPT2Config, GPT2LMHeadModel
+    from kvecc.ecc_shim import ECCShimConfig, patch_model_with_ecc_attention, reset_ecc_cache
+    torch.manual_seed(0)
+    model = GPT2LMHeadModel(GPT2Config(n_layer=2, n_head=4, n_embd=128, n_positions=128,
+                                       vocab_size=100)).eval().to(device)
+    cfg = ECCShimConfig(codec=codec, ber=1e-2, inject_errors=True, seed=42, block_size=16,
+                        use_interpolation=interp, backend="hip" if device.type == "cuda" else "cpu")
+    h = torch.randn(1, seq, 128, generator=torch.Generator().manual_seed(1)).to(device)
+    outs = []
+    for compiled in (False, True):
+        with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=16):
+            reset_ecc_cache(model)
+            attn = model.transformer.h[0].attn
+            fwd = attn.forward
+            if compiled:
+                torch._dynamo.reset()
+                fwd = torch.compile(attn.forward, fullgraph=True, backend="aot_eager")
+            out = fwd(h)[0]
+            be = model._ecc_backend
+            mgr = model._ecc_block_manager
+            outs.append((out.clone(), mgr.k_cache.clone(), mgr.v_cache.clone(), mgr.k_scales.clone(),
+                         be._stats.clone(), be._injection_count))
+    (o0, k0, v0, s0, st0, n0), (o1, k1, v1, s1, st1, n1) = outs
+    assert torch.equal(k0, k1) and torch.equal(v0, v1) and torch.equal(s0, s1)
+    assert torch.equal(st0, st1) and n0 == n1 == seq * 4
+    assert torch.equal(o0, o1)
+
+
+# seq 1 with plain Hamming(8,4) takes the decode-step paged attention (kvecc::paged_attention)
+CASES = [("hamming84", True, 24), ("golay", False, 24), ("hamming84", False, 24), ("hamming84", False, 1)]
+
+
+@pytest.mark.parametrize("codec,interp,seq", CASES)
+def test_patched_gpt2_attention_compiles_cpu(codec, interp, seq):
+    _gpt2_attention(torch.device("cpu"), codec, interp, seq)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("codec,interp,seq", CASES)
+def test_patched_gpt2_attention_compiles_hip(gpu, codec, interp, seq):
+    _gpt2_attention(gpu, codec, interp, seq)

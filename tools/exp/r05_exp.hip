@@ -1,0 +1,229 @@
+// r05_exp.hip -- round-5 geometry probes for the two standalone kernels the
+// round-4 verdict names (interpolation, H(8,4) decode + dequantize), against
+// the production kernels (included).  Not shipped; make -C tools/exp libr05.so,
+// run with tools/exp/run_r05.py on the GPU box.
+//
+// Interpolation, workgroup tiles with an LDS halo: a workgroup owns 64 column
+// chunks (1 KiB) x W*R rows; wave w owns rows [w*R, w*R+R) and loads them once,
+// publishes its first and last q row in LDS, and takes its neighbours' edge rows
+// from there after one barrier, so only the tile's two outer halo rows come from
+// HBM (2 / (W*R) of q instead of 2 / R).
+//
+// Decode + dequantize, wave tiles: a wave owns T*64 consecutive 16-byte output
+// vectors; load u and store u of every lane cover one contiguous span (512 B of
+// codewords, 1 KiB of fp16), and the grid is full (no grid stride), so each
+// wave writes T KiB and retires.
+#include "../../quantized-kv-cache-ecc-protection_amd/csrc/quant.hip"
+#include "../../quantized-kv-cache-ecc-protection_amd/csrc/interp.hip"
+
+namespace kvecc {
+
+template <int R, int W>
+__global__ __launch_bounds__(64 * W) void interp_tile_kernel(const u32x4 *__restrict__ q,
+                                                             const u32x4 *__restrict__ err,
+                                                             u32x4 *__restrict__ out, int64_t len,
+                                                             int64_t chunks) {
+  __shared__ u32x4 edge[2][W][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t cgroups = chunks / 64;
+  const int64_t rtiles = len / (R * W);
+  const int64_t t = blockIdx.x;
+  const int64_t cg = t % cgroups;
+  const int64_t rt = (t / cgroups) % rtiles;
+  const int64_t o = t / (cgroups * rtiles);
+  const int64_t l0 = rt * (R * W) + w * R;
+  const int64_t base = o * len * chunks + cg * 64 + lane;
+  u32x4 qr[R + 2], er[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
+  if (w == 0) qr[0] = ld_stream(q + base + (l0 > 0 ? l0 - 1 : 0) * chunks);
+  if (w == W - 1) qr[R + 1] = ld_stream(q + base + (l0 + R < len ? l0 + R : len - 1) * chunks);
+#pragma unroll
+  for (int k = 0; k < R; ++k) er[k] = ld_stream(err + base + (l0 + k) * chunks);
+  edge[0][w][lane] = qr[1];
+  edge[1][w][lane] = qr[R];
+  __syncthreads();
+  if (w > 0) qr[0] = edge[1][w - 1][lane];
+  if (w < W - 1) qr[R + 1] = edge[0][w + 1][lane];
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    st_stream(out + base + (l0 + k) * chunks, interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
+}
+
+// the production item kernel (interp.hip) with its work split into a full grid
+// of one item per lane, and a workgroup-size variant
+template <int R, int BS>
+__global__ __launch_bounds__(BS) void interp_items_kernel(const u32x4 *__restrict__ q,
+                                                          const u32x4 *__restrict__ err,
+                                                          u32x4 *__restrict__ out, int64_t len,
+                                                          int64_t chunks) {
+  const int64_t it = (int64_t)blockIdx.x * BS + threadIdx.x;
+  const int64_t c = it % chunks;
+  const int64_t t = it / chunks;
+  const int64_t rblocks = len / R;
+  const int64_t rb = t % rblocks;
+  const int64_t o = t / rblocks;
+  const int64_t l0 = rb * R;
+  const int64_t base = o * len * chunks + c;
+  u32x4 qr[R + 2], er[R];
+  qr[0] = ld_stream(q + base + (l0 > 0 ? l0 - 1 : 0) * chunks);
+#pragma unroll
+  for (int k = 0; k < R; ++k) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
+  qr[R + 1] = ld_stream(q + base + (l0 + R < len ? l0 + R : len - 1) * chunks);
+#pragma unroll
+  for (int k = 0; k < R; ++k) er[k] = ld_stream(err + base + (l0 + k) * chunks);
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    st_stream(out + base + (l0 + k) * chunks, interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
+}
+
+// decode + dequantize to fp16, wave tiles of T x 64 output vectors, full grid
+template <int T, int BS>
+__global__ __launch_bounds__(BS) void dd_tile_kernel(const u32x2 *__restrict__ cw,
+                                                     const float *__restrict__ scales,
+                                                     u32x4 *__restrict__ out, uint32_t total,
+                                                     int shift, uint64_t *__restrict__ stats) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * BS + threadIdx.x) >> 6;
+  const uint32_t base = wave * (64 * T) + lane;
+  uint32_t n1 = 0, n2 = 0;
+  u32x2 w[T];
+  float s[T];
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    const uint32_t i = base + u * 64;
+    w[u] = i < total ? ld_stream(cw + i) : u32x2{0, 0};
+    s[u] = i < total ? scales[i >> shift] : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    const uint32_t i = base + u * 64;
+    uint32_t nb[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint32_t q, t;
+      h84_decode4(w[u][k], q, t, n1, n2);
+      const uint32_t dbl = (t >> 1) & ~t & 0x01010101u;
+      q &= ~(dbl * 0xFFu);
+      nb[k] = q;
+    }
+    // dq16 reads nb[0..1]
+    const u32x4 o = dq16<__half>(nb, s[u], false);
+    if (i < total) st_stream(out + i, o);
+  }
+  flush_stats2<BS>(stats, n1, n2);
+}
+
+// the recording pass of kvecc_interpolate_auto (full row blocks): MODE 0 =
+// production (__syncthreads_or, one store per workgroup), 1 = per-wave ballot,
+// store only when the flag word does not already hold the epoch, 2 = no flag
+// writes (the bound)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void interp_rec_kernel(const u32x4 *__restrict__ q,
+                                                            const u32x4 *__restrict__ err,
+                                                            u32x4 *__restrict__ out, int64_t len,
+                                                            int64_t chunks, int32_t *__restrict__ flags,
+                                                            int32_t epoch) {
+  constexpr int R = kRows;
+  const int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t c = it % chunks;
+  const int64_t t = it / chunks;
+  const int64_t rblocks = len / R;
+  const int64_t rb = t % rblocks;
+  const int64_t o = t / rblocks;
+  const int64_t l0 = rb * R;
+  const int64_t base = o * len * chunks + c;
+  u32x4 qr[R + 2], er[R];
+  qr[0] = ld_stream(q + base + (l0 > 0 ? l0 - 1 : 0) * chunks);
+#pragma unroll
+  for (int k = 0; k < R; ++k) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
+  qr[R + 1] = ld_stream(q + base + (l0 + R < len ? l0 + R : len - 1) * chunks);
+#pragma unroll
+  for (int k = 0; k < R; ++k) er[k] = ld_stream(err + base + (l0 + k) * chunks);
+  uint32_t dbl = 0, over = 0;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    st_stream(out + base + (l0 + k) * chunks, interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
+    dbl |= seen_double(er[k]);
+    over |= seen_over15(qr[k + 1]);
+  }
+  if (MODE == 0) {
+    const bool d = __syncthreads_or(dbl != 0), ov = __syncthreads_or(over != 0);
+    if (threadIdx.x == 0) {
+      if (d) flags[0] = epoch;
+      if (ov) flags[1] = epoch;
+    }
+  } else if (MODE == 1) {
+    const bool d = __any(dbl != 0), ov = __any(over != 0);
+    if ((threadIdx.x & 63) == 0) {
+      if (d && __builtin_nontemporal_load(flags) != epoch) flags[0] = epoch;
+      if (ov && __builtin_nontemporal_load(flags + 1) != epoch) flags[1] = epoch;
+    }
+  } else {
+    asm volatile("" ::"v"(dbl), "v"(over));
+  }
+}
+
+}  // namespace kvecc
+
+using namespace kvecc;
+
+extern "C" KVECC_API int r05_interp_rec(int mode, const void *q, const void *e, void *o, int64_t outer,
+                                        int64_t len, int64_t chunks, int32_t *flags, int32_t epoch,
+                                        void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 g(outer * (len / kRows) * chunks / kBlock);
+  const u32x4 *qq = (const u32x4 *)q, *ee = (const u32x4 *)e;
+  u32x4 *oo = (u32x4 *)o;
+  if (mode == 0) hipLaunchKernelGGL(interp_rec_kernel<0>, g, dim3(kBlock), 0, s, qq, ee, oo, len, chunks, flags, epoch);
+  else if (mode == 1) hipLaunchKernelGGL(interp_rec_kernel<1>, g, dim3(kBlock), 0, s, qq, ee, oo, len, chunks, flags, epoch);
+  else hipLaunchKernelGGL(interp_rec_kernel<2>, g, dim3(kBlock), 0, s, qq, ee, oo, len, chunks, flags, epoch);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" KVECC_API int r05_interp(int v, const void *q, const void *e, void *o, int64_t outer, int64_t len,
+                          int64_t chunks, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const u32x4 *qq = (const u32x4 *)q, *ee = (const u32x4 *)e;
+  u32x4 *oo = (u32x4 *)o;
+  const int64_t cg = chunks / 64;
+  switch (v) {
+#define TILE(V, R, W)                                                                              \
+  case V:                                                                                          \
+    hipLaunchKernelGGL((interp_tile_kernel<R, W>), dim3(outer * (len / (R * W)) * cg), dim3(64 * W), 0, s, \
+                       qq, ee, oo, len, chunks);                                                   \
+    break;
+    TILE(0, 8, 4) TILE(1, 8, 8) TILE(2, 4, 8) TILE(3, 4, 16) TILE(4, 16, 4) TILE(5, 2, 16)
+#undef TILE
+#define ITEMS(V, R, BS)                                                                            \
+  case V:                                                                                          \
+    hipLaunchKernelGGL((interp_items_kernel<R, BS>), dim3(outer * (len / R) * chunks / BS), dim3(BS), 0, s, \
+                       qq, ee, oo, len, chunks);                                                   \
+    break;
+    ITEMS(10, 8, 256) ITEMS(11, 8, 512) ITEMS(12, 4, 256) ITEMS(13, 16, 256) ITEMS(14, 8, 1024)
+#undef ITEMS
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" KVECC_API int r05_dd(int v, const void *cw, const float *sc, void *out, int64_t rows, int64_t d,
+                      uint64_t *stats, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nchunk = (uint32_t)(d / 8), total = (uint32_t)(rows * nchunk);
+  const int shift = __builtin_ctz(nchunk);
+  switch (v) {
+#define DD(V, T, BS)                                                                              \
+  case V:                                                                                         \
+    hipLaunchKernelGGL((dd_tile_kernel<T, BS>), dim3((total + 64 * T * (BS / 64) - 1) / (64 * T * (BS / 64))), \
+                       dim3(BS), 0, s, (const u32x2 *)cw, sc, (u32x4 *)out, total, shift, stats); \
+    break;
+    DD(0, 1, 256) DD(1, 2, 256) DD(2, 4, 256) DD(3, 8, 256) DD(4, 4, 512) DD(5, 2, 512) DD(6, 4, 128)
+    DD(7, 8, 128)
+#undef DD
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -1,0 +1,54 @@
+#!/bin/bash
+# Round-5 GPU session steps (each with its own time limit; a fault, abort or
+# timeout stops the script).  usage: tools/gpu_r05.sh <tag> [steps...]
+#   launch  tests/test_gpu_launch.py (bench.py / tools/sweep.py spawn their ranks)
+#   test    the whole -m gpu suite          bench  bench.py (all sections)
+#   exp     tools/exp/run_r05.py            injpmc rocprofv3 VALU passes of the injection
+#   prof    rocprofv3 kernel trace of bench.py       smoke  __graft_entry__.smoke()
+set -u
+TAG=${1:-r05}
+shift || true
+STEPS=${@:-launch bench}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export TMPDIR=/tmp
+
+run() {  # name seconds cmd...
+  local name=$1 to=$2
+  shift 2
+  local t0=$(date +%s)
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/status.txt"
+  tail -3 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "stopping: $name ended with rc=$rc" | tee -a "$OUT/status.txt"
+    exit $rc
+  fi
+  return 0
+}
+
+for s in $STEPS; do
+  case $s in
+    launch) run pytest_launch 600 python -u -m pytest tests/test_gpu_launch.py -x -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
+    test)   run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench 600 python bench.py ;;
+    exp)    run exp_r05 600 python tools/exp/run_r05.py all ;;
+    injpmc)
+      run inj_trace 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/inj_trace" -o t -- \
+        python "$ROOT/tools/inject_pmc.py"
+      run inj_pmc1 120 timeout -s KILL 110 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_SALU \
+        --kernel-trace -T --output-format csv -d "$OUT/inj_pmc1" -o p -- python "$ROOT/tools/inject_pmc.py"
+      run inj_pmc2 120 timeout -s KILL 110 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+        --kernel-trace -T --output-format csv -d "$OUT/inj_pmc2" -o p -- python "$ROOT/tools/inject_pmc.py" ;;
+    prof)   run prof_trace 600 rocprofv3 --kernel-trace --stats -T --output-format csv \
+              -d "$OUT/prof" -o trace -- python "$ROOT/bench.py" --steps 20 --no-cpu-baseline ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+echo "done" | tee -a "$OUT/status.txt"

@@ -1,4 +1,8 @@
-"""Launcher for the sharded Monte-Carlo sweep (kvecc.montecarlo); torchrun-able:
+"""Launcher for the sharded Monte-Carlo sweep (kvecc.montecarlo).
+
+    python tools/sweep.py --gpus 8 --output sweep.jsonl      # spawns its 8 ranks
+
+or under torchrun (WORLD_SIZE set, nothing spawned):
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29501 tools/sweep.py --output sweep.jsonl
