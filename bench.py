@@ -89,6 +89,7 @@ def parse():
     ap.add_argument("--no-quant", action="store_true",
                     help="skip the fused quantize+encode / decode+dequantize roofline section")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the encode+inject+decode pipeline")
+    ap.add_argument("--no-montecarlo", action="store_true", help="skip the config-5 sweep section")
     ap.add_argument("--no-sections", action="store_true",
                     help="headline only: skip every optional section and the CPU baselines")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -97,7 +98,7 @@ def parse():
     a = ap.parse_args()
     if a.no_sections:
         for k in ("no_cpu_baseline", "no_inject", "no_packed", "no_fused", "no_rows", "no_interp",
-                  "no_quant", "no_pipeline"):
+                  "no_quant", "no_pipeline", "no_montecarlo"):
             setattr(a, k, True)
     return a
 
@@ -236,6 +237,24 @@ def quant_bench(dev, steps, warmup):
                 "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} "
                           "warm-up calls and >= 0.25 s"})
     return res
+
+
+def montecarlo_bench(dev):
+    """BASELINE config 5 on this GPU: the 36-trial codec sweep (4 codecs x BER
+    {1e-4,1e-3,1e-2} x seeds {42,101,997}) at [8,4096,32,128] through
+    kvecc.montecarlo.run_sweep, one fused launch per trial (kvecc_mc_trial),
+    one statistics fold at the end; a warm-up sweep first, the second timed."""
+    from kvecc import montecarlo as mc
+    cfg = mc.MonteCarloConfig()
+    shard = mc.HipShard(cfg, 0, 1, dev)
+    mc.run_sweep(cfg, shard)
+    rows, sec = mc.run_sweep(cfg, shard)
+    return {"workload": "config 5: 36 trials, 4 codecs x BER {1e-4,1e-3,1e-2} x seeds {42,101,997}, "
+                        "[8,4096,32,128], one GPU", "trials": len(rows), "ms": sec * 1e3,
+            "ms_per_trial": sec * 1e3 / len(rows), "fused": shard.fused,
+            "values_per_s": len(rows) * B * L * H * D / sec,
+            "bound": "valu (Philox per bit; the trial reads the ground truth once)",
+            "timing": "wall clock of run_sweep (device-synchronised), second of two sweeps"}
 
 
 def fused_decode_bench(dev, steps, warmup, packed=False):
@@ -627,18 +646,25 @@ def main():
                "timing": "HIP events carried by the dispatch, mean of 10 launches after >= 3 warm-up calls"}
         # VALU roofline: wave-level VALU instructions per Philox from the committed
         # SQ_INSTS_VALU pass (rocprofv3 cannot run inside this process) x the live
-        # Philox rate, against the full-rate issue peak (a wave64 VALU instruction
-        # takes 2 cycles of a SIMD-32: 256 CUs x 4 SIMDs x 2.4 GHz / 2)
-        peak = 256 * 4 * 2.4e9 / 2
+        # Philox rate.  Peak = what the SIMDs issue for this kernel's opcode mix:
+        # each opcode's share (its gfx950 disassembly) at its measured issue cost
+        # (profiles/r05/valu_rate.json: 32-bit multiplies, shifts and add3 take
+        # 4.15 cycles per wave64 instruction, v_bitop3 3.7, v_add_u32 2.4).  The
+        # nominal 2-cycle rate of 256 CUs x 4 SIMD-32 x 2.4 GHz is reported beside it.
+        nominal = 256 * 4 * 2.4e9 / 2
         if os.path.exists(args.inject_pmc_json):
             with open(args.inject_pmc_json) as f:
                 pmc = json.load(f)
-            ipp = pmc["valu_insts_per_philox"]
-            achieved = philox / (inj_ms * 1e-3) * ipp
+            ipp = pmc["valu_insts_per_philox"]  # lane-instructions per Philox (SQ_INSTS_VALU x 64 / Philox)
+            achieved = philox / (inj_ms * 1e-3) * ipp / 64  # wave-instructions per second
+            peak = pmc.get("mix_peak_wave_instr_per_s", nominal)
             res["roofline"] = {"bound": "valu", "achieved": achieved, "peak": peak,
                                "unit": "wave VALU instructions/s", "frac": achieved / peak,
-                               "valu_insts_per_philox": ipp, "source": pmc.get("source"),
-                               "valu_busy": pmc.get("valu_busy")}
+                               "peak_basis": "opcode mix of inject_kernel<int,24> at measured per-opcode issue cost",
+                               "nominal_peak": nominal, "frac_of_nominal": achieved / nominal,
+                               "valu_insts_per_philox": ipp, "mix_cycles_per_wave_instr":
+                               pmc.get("mix_cycles_per_wave_instr"),
+                               "valu_busy_pmc": pmc.get("valu_busy"), "source": pmc.get("source")}
         return res
 
     inject = None if args.no_inject else optional("inject", inject_section)
@@ -725,6 +751,7 @@ def main():
         "interp", lambda: interp_bench(dev, max(args.steps, 10), side_warmup))
     quant = None if args.no_quant else optional(
         "fused_quant", lambda: quant_bench(dev, max(args.steps, 10), side_warmup))
+    montecarlo = None if args.no_montecarlo or world > 1 else optional("montecarlo", lambda: montecarlo_bench(dev))
 
     fused = None
     if not args.no_fused:
@@ -806,6 +833,7 @@ def main():
         "golay_rows": rows,
         "interp": interp,
         "fused_quant": quant,
+        "montecarlo": montecarlo,
         "packed": packed,
         "cpu_baseline": cpu,
         "cpu_backend": host,

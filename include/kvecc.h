@@ -204,6 +204,38 @@ KVECC_API int kvecc_any_equal_u8(const uint8_t *x, int64_t n, uint8_t value, int
 KVECC_API int kvecc_count_ne_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint64_t *stats,
                                 void *stream);
 
+/* ---- Monte-Carlo trial (BASELINE config 5) ---------------------------------- */
+/* One trial of the codec-level fault-injection sweep in one launch: for every
+ * value of the ground-truth INT4 tensor x [outer, len, heads, head_dim] (uint8
+ * nibbles, contiguous), encode -> Bernoulli flips (the reference's per-bit
+ * Philox stream of fault_injection_triton.py:228-334 over the shard's global
+ * indices: global_n elements, this shard starting at offset0) -> decode
+ * (-> double-error interpolation along `len`) -> compare with x, keeping only
+ * the statistics; the codewords and decoded values never reach HBM.  The
+ * counterpart of the reference's encode / inject_bit_errors_triton / decode
+ * trial (evaluation/experiments/quantization_ecc_comparison.py:164-203,
+ * evaluation/sweep.py:352-626) and exactly the counters of that pipeline run
+ * kernel by kernel:
+ *   stats[0] flips, stats[1] elements with >= 1 flip,
+ *   stats[2] corrected (H74: syndrome != 0; H84: single errors; Golay: bits),
+ *   stats[3] detected (H74: 0; H84: double errors; Golay: uncorrectable words),
+ *   stats[4] decoded (interpolated) values != x.
+ * Hamming codecs draw n_bits 7 / 8 per value (global_n, offset0 in values);
+ * Golay packs each head row into ceil(head_dim/3) codewords (the shim's
+ * per-head padding, ecc_shim.py:623-682) and draws 24 bits per codeword
+ * (global_n, offset0 in codewords).  KVECC_MC_H84_INTERP needs heads*head_dim
+ * % 4 == 0. */
+enum { KVECC_MC_H74 = 1, KVECC_MC_H84 = 2, KVECC_MC_H84_INTERP = 3, KVECC_MC_GOLAY = 4 };
+KVECC_API int kvecc_mc_trial(const uint8_t *x, int64_t outer, int64_t len, int64_t heads,
+                             int64_t head_dim, int codec, float ber, int64_t seed, int64_t global_n,
+                             int64_t offset0, uint64_t *stats, void *stream);
+/* dst[b * dst_stride + w] += stats word w summed over the KVECC_STATS_SLOTS
+ * slots of buffer b (buffers KVECC_STATS_WORDS apart), for b < nbuf and
+ * w < nwords <= KVECC_STATS_STRIDE; the buffers are zeroed afterwards.  One
+ * launch folds every trial's counters into the sweep's table. */
+KVECC_API int kvecc_stats_fold(uint64_t *stats, int64_t nbuf, int nwords, int64_t *dst,
+                               int64_t dst_stride, void *stream);
+
 /* ---- Fused quantize / encode and decode / dequantize ----------------------- */
 /* fused_kernels.py:18-160 (H84), :163-269 (H74), and the shim's torch path
  * ecc_shim.py:572-580: per row of d values (dtype x_dtype), scale = absmax/7

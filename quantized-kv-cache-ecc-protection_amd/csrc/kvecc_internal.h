@@ -293,6 +293,26 @@ __device__ __forceinline__ void flush_stats2(uint64_t *stats, uint32_t a, uint32
   }
 }
 
+// N per-lane counters into words 0..N-1 of the sharded statistics buffer (as
+// flush_stats2; one atomic per non-zero statistic per workgroup)
+template <int N, int BS = kBlock>
+__device__ __forceinline__ void flush_stats_n(uint64_t *stats, const uint32_t (&v)[N]) {
+  __shared__ uint32_t red[N][BS / kWave];
+  const int wave = threadIdx.x / kWave;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    const uint32_t s = wave_sum(v[k]);
+    if ((threadIdx.x & (kWave - 1)) == 0) red[k][wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < N) {
+    unsigned long long sum = 0;
+    for (int w = 0; w < BS / kWave; ++w) sum += red[threadIdx.x][w];
+    uint64_t *slot = stats + (size_t)(blockIdx.x % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (sum) atomicAdd(reinterpret_cast<unsigned long long *>(slot + threadIdx.x), sum);
+  }
+}
+
 // The dynamic tile schedule of one wave (the fused reads in shim.hip, the
 // per-head rows in golay.hip, the packed Golay decode): its first tile is gw,
 // next() gives the following ones (>= units: none left).  A wave takes the first

@@ -49,6 +49,8 @@ SIGNATURES = {
     "kvecc_interpolate": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "kvecc_any_equal_u8": [_vp, _i64, _u8, _vp, _vp],
     "kvecc_count_ne_u8": [_vp, _vp, _i64, _vp, _vp],
+    "kvecc_mc_trial": [_vp, _i64, _i64, _i64, _i64, _int, _f32, _i64, _i64, _i64, _vp, _vp],
+    "kvecc_stats_fold": [_vp, _i64, _int, _vp, _i64, _vp],
     "kvecc_interpolate_auto": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp],
     "kvecc_quantize_encode_rows": [_vp, _int, _int, _int, _vp, _vp, _i64, _i64, _vp],
     "kvecc_decode_dequant_h84_rows": [_vp, _vp, _vp, _int, _i64, _i64, _int, _vp, _vp],
@@ -105,6 +107,8 @@ _RESTYPE = {
 F32, F16, BF16 = 0, 1, 2
 CODEC_NONE, CODEC_H74, CODEC_H84, CODEC_GOLAY = 0, 1, 2, 3
 CODEC_GOLAY_PACKED = 4  # shim caches only: 3-byte Golay codewords (kvecc.h)
+# kvecc_mc_trial codecs (kvecc.h KVECC_MC_*)
+MC_CODECS = {"hamming74": 1, "hamming84": 2, "hamming84_interp": 3, "golay": 4}
 
 
 def golay_packed_row_bytes(g: int) -> int:

@@ -114,16 +114,25 @@ class _TrialBuffers:
 class HipShard:
     """One rank's shard of the sweep on an MI355X (kvecc HIP kernels).
 
-    Trials are pipelined over two HIP streams: trial k's encode + injection
-    (VALU-bound Philox, ~1.65 ms at [8,4096,32,128]) runs on one stream while
-    trial k-1's decode, interpolation and residual count (HBM-bound) run on the
-    other, in two alternating buffer sets ordered by events.  The counters are
-    the same as a serial run's; finish() drains the pipeline."""
+    fused=True (default): a trial is ONE launch, kvecc_mc_trial, which encodes,
+    flips, decodes (and interpolates) in registers and keeps only the five
+    counters -- the trial is VALU-bound on its Philox draws and touches HBM
+    only to read the ground truth.  Every trial gets its own statistics buffer;
+    finish() folds them all into the sweep's table in one launch
+    (kvecc_stats_fold).
 
-    def __init__(self, cfg: MonteCarloConfig, rank: int, world: int, device):
+    fused=False: the kernel-by-kernel pipeline (encode, inject, decode,
+    interpolate, count as separate launches), pipelined over two HIP streams:
+    trial k's encode + injection runs on one stream while trial k-1's decode,
+    interpolation and residual count run on the other, in two alternating
+    buffer sets ordered by events.  Kept as the check of the fused trial
+    (same counters) and for A/B timing.  finish() drains the pipeline."""
+
+    def __init__(self, cfg: MonteCarloConfig, rank: int, world: int, device, fused: bool = True):
         from . import ops
         self.ops = ops
         self.cfg = cfg
+        self.fused = fused
         self.dev = torch.device(device)
         b, l, h, d = cfg.shape
         self.b0, self.b1 = shard_bounds(b, rank, world)
@@ -140,18 +149,39 @@ class HipShard:
         if self.sb:
             ops.inject_into(self.x.view(-1), self.x.view(-1), 0.5, 4, cfg.data_seed,
                             global_n=self.n_total, offset0=self.off)
+        self.k = 0
+        self.pending = None
+        self._stat_chunks, self._queued = [], []  # fused: statistics buffers, (buffer, row) per trial
+        # the fused interpolating trial reads 4-value column chunks
+        self.fused = fused = fused and (h * d) % 4 == 0
+        if fused:
+            return
         with torch.cuda.device(self.dev):
             self.bufs = [_TrialBuffers(ops, shape, self.g, self.dev) for _ in range(2)]
             self.s_inj = torch.cuda.Stream(self.dev)
             self.s_dec = torch.cuda.Stream(self.dev)
-        self.k = 0
-        self.pending = None
+
+    _CHUNK = 64  # statistics buffers allocated at once (fused)
+
+    def _stats_buffer(self):
+        i = len(self._queued)
+        if i // self._CHUNK >= len(self._stat_chunks):
+            self._stat_chunks.append(torch.zeros(self._CHUNK, self.ops.STATS_SLOTS * self.ops.STATS_STRIDE,
+                                                 dtype=torch.int64, device=self.dev))
+        return self._stat_chunks[i // self._CHUNK][i % self._CHUNK]
 
     def run_trial(self, codec, ber, seed, row):
         """Queue one trial; its 5 counters land in `row` (device int64[5]) once
-        the pipeline has run it (finish() or the next trial)."""
+        the shard has run it (finish(), or the next trial for fused=False)."""
         ops = self.ops
         if self.sb == 0:
+            return row
+        if self.fused:
+            st = self._stats_buffer()
+            golay = codec == "golay"
+            ops.mc_trial_into(self.x, codec, ber, seed, self.m_total if golay else self.n_total,
+                              self.m_off if golay else self.off, st)
+            self._queued.append(row)
             return row
         caller = torch.cuda.current_stream(self.dev)
         buf = self.bufs[self.k % 2]
@@ -212,11 +242,31 @@ class HipShard:
             buf.free.record(self.s_dec)
 
     def finish(self):
-        """Drain the pipeline; the caller's stream then waits for every queued trial."""
+        """Fold the fused trials' statistics into their rows, or drain the
+        pipeline; the caller's stream then holds every queued trial's counters."""
+        if self.fused:
+            self._fold()
+            return
         self._drain()
         caller = torch.cuda.current_stream(self.dev)
         caller.wait_stream(self.s_inj)
         caller.wait_stream(self.s_dec)
+
+    def _fold(self):
+        rows, self._queued = self._queued, []
+        for c, chunk in enumerate(self._stat_chunks):
+            part = rows[c * self._CHUNK:(c + 1) * self._CHUNK]
+            if not part:
+                break
+            r0 = part[0]
+            step = r0.element_size() * len(STAT_NAMES)
+            if all(r.data_ptr() == r0.data_ptr() + k * step and r.is_contiguous() for k, r in enumerate(part)):
+                # consecutive rows of one table (run_sweep's): one launch for the chunk
+                dst = torch.as_strided(r0, (len(part), len(STAT_NAMES)), (len(STAT_NAMES), 1))
+                self.ops.stats_fold_into(chunk, len(part), len(STAT_NAMES), dst)
+            else:
+                for k, r in enumerate(part):
+                    self.ops.stats_fold_into(chunk[k], 1, len(STAT_NAMES), r.view(1, -1))
 
 
 class HostShard:

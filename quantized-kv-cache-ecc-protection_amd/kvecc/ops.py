@@ -453,6 +453,37 @@ def count_ne_into(a, b, stats):
     return stats
 
 
+def mc_trial_into(x, codec, ber, seed, global_n, offset0, stats):
+    """One Monte-Carlo trial in one launch (kvecc_mc_trial): x uint8 [outer, len,
+    heads, head_dim] ground-truth nibbles -> encode -> Philox flips -> decode
+    (-> interpolation along len) -> compare; stats words 0..4 += (flips,
+    affected, corrected, detected, mismatches).  No host sync."""
+    _check_gpu(x)
+    if x.dim() != 4 or x.dtype != torch.uint8 or not x.is_contiguous():
+        raise ValueError("mc_trial_into: x must be a contiguous uint8 [outer, len, heads, head_dim] tensor")
+    if codec not in _lib.MC_CODECS:
+        raise ValueError(f"mc_trial_into: codec {codec!r} not in {sorted(_lib.MC_CODECS)}")
+    _ensure_device(x.device)
+    outer, length, heads, d = x.shape
+    _lib.call("kvecc_mc_trial", _ptr(x), outer, length, heads, d, _lib.MC_CODECS[codec], float(ber), int(seed),
+              int(global_n), int(offset0), _sptr(stats, x.device), _stream(x.device))
+    return stats
+
+
+def stats_fold_into(stats, nbuf, nwords, dst):
+    """dst[b, w] += statistic w of buffer b (nbuf buffers of KVECC_STATS_WORDS
+    words back to back), then zero the buffers (kvecc_stats_fold); one launch."""
+    if stats.dtype != torch.int64 or not stats.is_contiguous() or stats.numel() < nbuf * STATS_SLOTS * STATS_STRIDE:
+        raise ValueError("stats_fold_into: stats must hold nbuf contiguous int64 statistics buffers")
+    if dst.dtype != torch.int64 or dst.dim() != 2 or dst.shape[0] < nbuf or dst.shape[1] < nwords or dst.stride(1) != 1:
+        raise ValueError("stats_fold_into: dst must be int64 [>= nbuf, >= nwords] with unit column stride")
+    if dst.device != stats.device:
+        raise ValueError("stats_fold_into: stats and dst on different devices")
+    _lib.call("kvecc_stats_fold", _ptr(stats), int(nbuf), int(nwords), _ptr(dst), dst.stride(0),
+              _stream(stats.device))
+    return dst
+
+
 def any_equal(x, value, flag=None):
     """Device int32 flag = any(x == value), no host sync."""
     if flag is None:

@@ -149,10 +149,13 @@ def test_sweep_resume(tmp_path):
 
 
 @pytest.mark.gpu
-def test_hip_shard_matches_oracle_shard(gpu):
+@pytest.mark.parametrize("fused", [True, False])
+def test_hip_shard_matches_oracle_shard(gpu, fused):
+    """The fused one-launch trial (kvecc_mc_trial) and the kernel-by-kernel
+    pipeline both give the oracle shard's counters."""
     cfg = mc.MonteCarloConfig(shape=(4, 64, 3, 128), bers=(1e-3, 0.03), seeds=(42,))
     for world, rank in ((1, 0), (3, 1)):
-        hip = mc.HipShard(cfg, rank, world, gpu)
+        hip = mc.HipShard(cfg, rank, world, gpu, fused=fused)
         ora = OracleShard(cfg, rank, world)
         assert np.array_equal(hip.x.cpu().numpy(), ora.x)
         for codec, ber, seed in cfg.trials():
@@ -165,12 +168,14 @@ def test_hip_shard_matches_oracle_shard(gpu):
 
 
 @pytest.mark.gpu
-def test_hip_shard_pipeline_equals_oracle(gpu):
-    """Trials queued back to back (encode + injection of trial k on one stream,
-    decode + count of trial k-1 on the other, two alternating buffer sets)
-    give every trial the oracle's counters."""
+@pytest.mark.parametrize("fused", [True, False])
+def test_hip_shard_pipeline_equals_oracle(gpu, fused):
+    """Trials queued back to back give every trial the oracle's counters: fused
+    (one launch per trial, one statistics fold at the end) and unfused
+    (encode + injection of trial k on one stream, decode + count of trial k-1
+    on the other, two alternating buffer sets)."""
     cfg = mc.MonteCarloConfig(shape=(2, 96, 4, 128), bers=(1e-3, 0.03), seeds=(42, 7))
-    hip = mc.HipShard(cfg, 0, 1, gpu)
+    hip = mc.HipShard(cfg, 0, 1, gpu, fused=fused)
     ora = OracleShard(cfg, 0, 1)
     trials = cfg.trials()
     rows = torch.zeros(len(trials), 5, dtype=torch.int64, device=gpu)
@@ -265,6 +270,35 @@ def test_hip_sweep_gloo_world2_on_one_gpu_equals_single(gpu, tmp_path):
     res = _launch_ranks("gloo", 2, str(tmp_path / "gloo2.json"))
     assert res["backend"] == "gloo" and res["world"] == 2
     assert res["rows"] == _single_hip_rows(gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(3, 41, 2, 20), (2, 7, 3, 5), (1, 5, 1, 4), (2, 130, 1, 129), (3, 9, 4, 1)])
+def test_fused_trial_odd_geometry_equals_oracle(gpu, shape):
+    """kvecc_mc_trial at geometries off the sweep's: head_dim not a multiple of
+    3 (Golay padding) or 4, sequence lengths that end mid row-block (the
+    interpolating trial's edge rows), value counts not a multiple of 4, and
+    shards whose offset starts mid-tensor; every counter equals the oracle's."""
+    cfg = mc.MonteCarloConfig(shape=shape, bers=(0.03, 0.15), seeds=(42,))
+    for world, rank in ((1, 0), (2, 1)):
+        if shard_empty(shape, world, rank):
+            continue
+        hip = mc.HipShard(cfg, rank, world, gpu, fused=True)
+        ora = OracleShard(cfg, rank, world)
+        for codec, ber, seed in cfg.trials():
+            if codec == "hamming84_interp" and (shape[2] * shape[3]) % 4:
+                continue  # the fused interpolating trial needs heads*head_dim % 4 == 0
+            a = torch.zeros(5, dtype=torch.int64, device=gpu)
+            b = torch.zeros(5, dtype=torch.int64)
+            hip.run_trial(codec, ber, seed, a)
+            hip.finish()
+            ora.run_trial(codec, ber, seed, b)
+            assert a.cpu().tolist() == b.tolist(), (shape, codec, ber, world, rank)
+
+
+def shard_empty(shape, world, rank):
+    b0, b1 = mc.shard_bounds(shape[0], rank, world)
+    return b1 == b0
 
 
 @pytest.mark.parametrize("world,rank", [(1, 0), (2, 1), (3, 2)])

@@ -39,15 +39,25 @@ for s in $STEPS; do
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench 600 python bench.py ;;
     exp)    run exp_r05 600 python tools/exp/run_r05.py all ;;
+    valu)   run valu_rate 300 python tools/exp/run_valu_rate.py ;;
+    mc)     run mc_time 300 python tools/mc_time.py ;;
+    mcprof) run mc_trace 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/mc_trace" -o t -- \
+              python "$ROOT/tools/mc_time.py" --only fused ;;
     injpmc)
-      run inj_trace 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/inj_trace" -o t -- \
+      run inj_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/inj_trace" -o t -- \
         python "$ROOT/tools/inject_pmc.py"
       run inj_pmc1 120 timeout -s KILL 110 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_SALU \
-        --kernel-trace -T --output-format csv -d "$OUT/inj_pmc1" -o p -- python "$ROOT/tools/inject_pmc.py"
+        --kernel-trace --output-format csv -d "$OUT/inj_pmc1" -o p -- python "$ROOT/tools/inject_pmc.py"
       run inj_pmc2 120 timeout -s KILL 110 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-        --kernel-trace -T --output-format csv -d "$OUT/inj_pmc2" -o p -- python "$ROOT/tools/inject_pmc.py" ;;
-    prof)   run prof_trace 600 rocprofv3 --kernel-trace --stats -T --output-format csv \
+        --kernel-trace --output-format csv -d "$OUT/inj_pmc2" -o p -- python "$ROOT/tools/inject_pmc.py" ;;
+    prof)   run prof_trace 600 rocprofv3 --kernel-trace --stats --output-format csv \
               -d "$OUT/prof" -o trace -- python "$ROOT/bench.py" --steps 20 --no-cpu-baseline ;;
+    pmc)    run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
+              -d "$OUT/pmc_fetch" -o fetch -- python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline \
+              --no-inject --side-warmup 5
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv \
+              -d "$OUT/pmc_write" -o write -- python "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline \
+              --no-inject --side-warmup 5 ;;
     *) echo "unknown step $s" ;;
   esac
 done
