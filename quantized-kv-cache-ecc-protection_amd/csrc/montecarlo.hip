@@ -18,15 +18,16 @@
 // individual kernels and the host twin use.
 //
 // Interpolation (hamming84 + interp) needs the decoded values of the sequence
-// neighbours: a lane owns a 4-value column chunk of kMcRows consecutive
-// positions, so interior neighbours are in its registers; an edge row's outer
-// neighbour is recomputed (its 4 values encoded, flipped and decoded again)
-// only when that row holds a double error, which at the sweep's BERs is rare.
+// neighbours: a lane walks a 4-value column chunk down a strip of kMcStrip
+// consecutive positions with the previous, current and next decoded rows in
+// registers; a strip edge's outer neighbour is recomputed (its 4 values
+// encoded, flipped and decoded again) only when the edge row holds a double
+// error, which at the sweep's BERs is rare.
 #include "kvecc_internal.h"
 
 namespace kvecc {
 
-constexpr int kMcRows = 4;     // positions per lane (interpolating trial)
+constexpr int kMcStrip = 32;   // positions per lane (interpolating trial)
 constexpr int kMcPerCu = 16;   // workgroups per CU (grid-strided, as the injection)
 
 struct McArgs {
@@ -119,33 +120,40 @@ __device__ __forceinline__ uint32_t mc_h84_row(const McArgs &a, int64_t o, int64
 __global__ __launch_bounds__(kBlock) void mc_h84_interp_kernel(McArgs a) {
   uint32_t c[5] = {0, 0, 0, 0, 0};
   const int64_t chunks = a.inner / 4;
-  const int64_t rblocks = (a.len + kMcRows - 1) / kMcRows;
-  const int64_t items = a.outer * rblocks * chunks;
+  const int64_t strips = (a.len + kMcStrip - 1) / kMcStrip;
+  const int64_t items = a.outer * strips * chunks;
   for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < items;
        it += (int64_t)gridDim.x * kBlock) {
     const int64_t c4 = it % chunks;
     const int64_t t = it / chunks;
-    const int64_t rb = t % rblocks;
-    const int64_t o = t / rblocks;
-    const int64_t l0 = rb * kMcRows;
-    const int nrow = (int)min<int64_t>(kMcRows, a.len - l0);
-    uint32_t q[kMcRows], e[kMcRows], xw[kMcRows];
-#pragma unroll
-    for (int k = 0; k < kMcRows; ++k)
-      if (k < nrow) q[k] = mc_h84_row<true>(a, o, l0 + k, c4, e[k], xw[k], c);
-#pragma unroll
-    for (int k = 0; k < kMcRows; ++k) {
-      if (k >= nrow) break;
-      const int64_t l = l0 + k;
-      uint32_t out = sat15(q[k]);
-      if (is_double(e[k])) {  // rare: only then are the neighbours needed
-        uint32_t tt, xx, none[5];
-        const uint32_t left = k > 0 ? q[k - 1] : (l == 0 ? q[k] : mc_h84_row<false>(a, o, l - 1, c4, tt, xx, none));
-        const uint32_t right = k + 1 < nrow ? q[k + 1]
-                               : (l + 1 >= a.len ? q[k] : mc_h84_row<false>(a, o, l + 1, c4, tt, xx, none));
-        out = interp_word(q[k], left, right, e[k]);
+    const int64_t sp = t % strips;
+    const int64_t o = t / strips;
+    const int64_t l0 = sp * kMcStrip, l1 = min<int64_t>(l0 + kMcStrip, a.len);
+    // walk the strip with the previous / current / next decoded rows in registers
+    uint32_t e_cur, x_cur, e_nxt, x_nxt, prev = 0, none[5];
+    uint32_t cur = mc_h84_row<true>(a, o, l0, c4, e_cur, x_cur, c);
+    for (int64_t l = l0; l < l1; ++l) {
+      uint32_t nxt = cur;
+      if (l + 1 < l1) nxt = mc_h84_row<true>(a, o, l + 1, c4, e_nxt, x_nxt, c);
+      uint32_t out = sat15(cur);
+      if (is_double(e_cur)) {  // the neighbours only matter here; past the strip, recompute
+        // at most one neighbour lies outside the strip (strips hold >= 2 rows
+        // unless the sequence has one position): one recompute site
+        const bool out_l = l == l0 && l > 0, out_r = l + 1 == l1 && l + 1 < a.len;
+        uint32_t ext = cur;
+        if (out_l || out_r) {
+          uint32_t tt, xx;
+          ext = mc_h84_row<false>(a, o, out_l ? l - 1 : l + 1, c4, tt, xx, none);
+        }
+        const uint32_t left = l == 0 ? cur : (out_l ? ext : prev);
+        const uint32_t right = l + 1 >= a.len ? cur : (out_r && !out_l ? ext : nxt);
+        out = interp_word(cur, left, right, e_cur);
       }
-      c[4] += mc_ne_bytes(out ^ xw[k]);
+      c[4] += mc_ne_bytes(out ^ x_cur);
+      prev = cur;
+      cur = nxt;
+      e_cur = e_nxt;
+      x_cur = x_nxt;
     }
   }
   flush_stats_n<5>(a.stats, c);
@@ -254,7 +262,7 @@ KVECC_API int kvecc_mc_trial(const uint8_t *x, int64_t outer, int64_t len, int64
       a.seedmul = (uint32_t)((uint64_t)seed * (uint64_t)((uint64_t)global_n * (uint64_t)nb));
       if (codec == KVECC_MC_H84_INTERP) {
         if (a.inner % 4) return set_error(KVECC_EINVAL, "mc_trial: interpolation needs heads*head_dim %% 4 == 0");
-        const int64_t items = outer * ((len + kMcRows - 1) / kMcRows) * (a.inner / 4);
+        const int64_t items = outer * ((len + kMcStrip - 1) / kMcStrip) * (a.inner / 4);
         KVECC_LAUNCH(mc_h84_interp_kernel, dim3(grid_for(items, kBlock, kMcPerCu)), dim3(kBlock), 0, st, a);
       } else if (codec == KVECC_MC_H84) {
         KVECC_LAUNCH((mc_hamming_kernel<true, 8>), dim3(grid_for((units + 3) / 4, kBlock, kMcPerCu)),

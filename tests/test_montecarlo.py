@@ -332,3 +332,91 @@ def test_config5_full_shape_hip_sweep_equals_host_backend(gpu):
         assert a == b, (a, b)
         assert a["flips"] > 0 and a["corrected"] > 0
     assert any(r["mismatches"] > 0 for r in rows_h)  # residual errors are counted, not zero by accident
+
+
+class ThreadedOracleShard(OracleShard):
+    """OracleShard whose Philox draws run on host threads: the oracle's flat
+    injection is shard-aware (global_n, offset0), so contiguous slices of the
+    shard inject independently and give the single call's bits."""
+
+    THREADS = 16
+
+    def __init__(self, cfg, rank, world):  # noqa: D107  (the base draws x single-threaded; redo it threaded)
+        from oracle import oracle
+        self.o = oracle
+        self.cfg = cfg
+        self.dev = torch.device("cpu")
+        b, l, h, d = cfg.shape
+        self.b0, self.b1 = mc.shard_bounds(b, rank, world)
+        self.sb = self.b1 - self.b0
+        per_b = l * h * d
+        self.n_total, self.off = b * per_b, self.b0 * per_b
+        self.g = (d + 2) // 3
+        self.m_total, self.m_off = b * l * h * self.g, self.b0 * l * h * self.g
+        x, _ = self._inject(np.zeros(self.sb * per_b, np.uint8), 0.5, 4, cfg.data_seed, self.n_total, self.off)
+        self.x = x.reshape(self.sb, l, h, d)
+
+    def _inject(self, data, ber, n_bits, seed, global_n, offset0):
+        from concurrent.futures import ThreadPoolExecutor
+        flat = data.reshape(-1)
+        n = flat.size
+        cuts = [n * k // self.THREADS for k in range(self.THREADS + 1)]
+
+        def part(k):
+            a, b = cuts[k], cuts[k + 1]
+            out, _, st = self.o.inject(flat[a:b], ber, n_bits, seed, global_n=global_n, offset0=offset0 + a)
+            return out, st
+
+        with ThreadPoolExecutor(self.THREADS) as pool:
+            res = list(pool.map(part, range(self.THREADS)))
+        return (np.concatenate([r[0] for r in res]).reshape(data.shape),
+                (sum(r[1][0] for r in res), sum(r[1][1] for r in res)))
+
+    def run_trial(self, codec, ber, seed, row):
+        o = self.o
+        b, l, h, d = self.cfg.shape
+        if codec == "golay":
+            pad = np.zeros((self.sb, l, h, 3 * self.g), np.uint8)
+            pad[..., :d] = self.x
+            cw = o.golay_encode(pad.reshape(-1, 3))
+            noisy, (fl, af) = self._inject(cw, ber, 24, seed, self.m_total, self.m_off)
+            trip, _, (c, u) = o.golay_decode(noisy)
+            out = trip.reshape(self.sb, l, h, 3 * self.g)[..., :d]
+        else:
+            enc = o.hamming74_encode if codec == "hamming74" else o.hamming84_encode
+            cw = enc(self.x.reshape(-1))
+            noisy, (fl, af) = self._inject(cw, ber, mc.N_BITS[codec], seed, self.n_total, self.off)
+            if codec == "hamming74":
+                out, _, (c,) = o.hamming74_decode(noisy)
+                u = 0
+            else:
+                out, et, (c, u) = o.hamming84_decode(noisy)
+                if codec == "hamming84_interp":
+                    out = o.interpolate_kernel(out, et, self.sb, l, h * d)
+            out = out.reshape(self.x.shape)
+        mism = int((out != self.x).sum())
+        row += torch.tensor([fl, af, c, u, mism], dtype=torch.int64)
+        return row
+
+
+@pytest.mark.gpu
+def test_config5_full_shape_fused_trials_equal_oracle(gpu):
+    """Config 5 at its own shape, [8,4096,32,128], anchored on the C oracle
+    (not the host backend, which shares codec_math.h with the kernels): rank 5
+    of 8 -- one full batch row at global offset 5/8 of the tensor, every Philox
+    key at full-size global_n -- through the fused one-launch trial, every
+    codec at BER 1e-2, every counter equal."""
+    cfg = mc.MonteCarloConfig(bers=(1e-2,), seeds=(997,))
+    assert cfg.shape == (8, 4096, 32, 128)
+    hip = mc.HipShard(cfg, 5, 8, gpu)
+    assert hip.fused
+    ora = ThreadedOracleShard(cfg, 5, 8)
+    assert np.array_equal(hip.x.cpu().numpy(), ora.x)
+    for codec, ber, seed in cfg.trials():
+        a = torch.zeros(5, dtype=torch.int64, device=gpu)
+        b = torch.zeros(5, dtype=torch.int64)
+        hip.run_trial(codec, ber, seed, a)
+        hip.finish()
+        ora.run_trial(codec, ber, seed, b)
+        assert a.cpu().tolist() == b.tolist(), (codec, a.cpu().tolist(), b.tolist())
+        assert b[0] > 0 and b[4] > 0

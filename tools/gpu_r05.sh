@@ -37,6 +37,8 @@ for s in $STEPS; do
     test)   run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    mctest) run pytest_mc 600 python -u -m pytest tests/test_montecarlo.py -m gpu -x -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     exp)    run exp_r05 600 python tools/exp/run_r05.py all ;;
     valu)   run valu_rate 300 python tools/exp/run_valu_rate.py ;;
