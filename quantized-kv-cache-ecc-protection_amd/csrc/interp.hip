@@ -23,7 +23,10 @@
 
 namespace kvecc {
 
-constexpr int kRows = 8;
+constexpr int kRows = 4;                       // positions per wave of a tile
+constexpr int kTileWavesI = 8;                  // waves per workgroup tile
+constexpr int kTileRows = kRows * kTileWavesI;  // 32 positions per tile
+constexpr int kTileThreads = kTileWavesI * kWave;
 
 // sat15 / avg_up / is_double / interp_word (four bytes per word): codec_math.h
 __device__ __forceinline__ u32x4 interp_vec(u32x4 q, u32x4 l, u32x4 r, u32x4 e) {
@@ -35,10 +38,6 @@ __device__ __forceinline__ u32x4 interp_vec(u32x4 q, u32x4 l, u32x4 r, u32x4 e) 
   return o;
 }
 
-// vector path: inner % 16 == 0; work item = (o, row block, column chunk).  All
-// kRows + 2 q rows (with the one-row halo each side) and kRows err rows of the
-// item are loaded before any is used, non-temporally, so a lane keeps ~18
-// 16-byte loads in flight.
 // any byte of the word == 2 / > 15
 __device__ __forceinline__ uint32_t seen_double(u32x4 e) {
   return is_double(e.x) | is_double(e.y) | is_double(e.z) | is_double(e.w);
@@ -47,74 +46,87 @@ __device__ __forceinline__ uint32_t seen_over15(u32x4 q) {
   return (q.x | q.y | q.z | q.w) & 0xF0F0F0F0u;
 }
 
+// vector path (inner % 16 == 0): workgroup tiles of 64 column chunks (1 KiB)
+// x kTileRows positions.  Wave w owns positions [w kRows, w kRows + kRows) of
+// the tile and loads its q and err rows once, non-temporally; it publishes its
+// first and last q row in LDS and takes its neighbour waves' edge rows from
+// there after one barrier, so only the tile's two outer halo rows come from
+// HBM: 2 / 32 of q re-read instead of the 2 / 8 of the round-1 per-lane row
+// blocks (63.5 against 68.9 us at [8,4096,32,128], tools/exp/run_r05.py,
+// profiles/r05/exp_r05.log).  Ragged shapes: lanes past the last chunk and
+// rows past the sequence end load and store nothing; the clamped neighbours
+// (q[max(l-1,0)], q[min(l+1,len-1)]) come from the same rows.
 // RECORD: no gate; flags[0] = epoch if any err == 2, flags[1] = epoch if any
-// q > 15 (one plain store per workgroup that saw one; no zeroing pass)
+// q > 15, one store per wave that saw one and found the word not yet stamped
+// (no barrier after the stores, no zeroing pass)
 template <bool RECORD>
-__global__ __launch_bounds__(kBlock) void interp_vec_kernel(const u32x4 *__restrict__ q,
-                                                            const u32x4 *__restrict__ err,
-                                                            u32x4 *__restrict__ out, int64_t outer,
-                                                            int64_t len, int64_t chunks,
-                                                            const int32_t *__restrict__ gate,
-                                                            int32_t *__restrict__ flags,
-                                                            int32_t epoch) {
+__global__ __launch_bounds__(kTileThreads) void interp_tile_kernel(const u32x4 *__restrict__ q,
+                                                                  const u32x4 *__restrict__ err,
+                                                                  u32x4 *__restrict__ out, int64_t len,
+                                                                  int64_t chunks,
+                                                                  const int32_t *__restrict__ gate,
+                                                                  int32_t *__restrict__ flags, int32_t epoch) {
+  __shared__ u32x4 edge[2][kTileWavesI][kWave];  // [first, last row][wave][lane]
   const bool pass = !RECORD && gate != nullptr && *gate == 0;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = threadIdx.x / kWave;
+  const int64_t cgroups = (chunks + kWave - 1) / kWave;
+  const int64_t rtiles = (len + kTileRows - 1) / kTileRows;
+  const int64_t t = blockIdx.x;
+  const int64_t cg = t % cgroups;
+  const int64_t rt = (t / cgroups) % rtiles;
+  const int64_t o = t / (cgroups * rtiles);
+  const int64_t c = cg * kWave + lane;
+  const bool col = c < chunks;
+  const int64_t l0 = rt * kTileRows + (int64_t)w * kRows;
+  const int nrow = (int)max<int64_t>(0, min<int64_t>(kRows, len - l0));  // wave-uniform
+  const int64_t base = o * len * chunks + c;
+  u32x4 qr[kRows + 2], er[kRows];
+#pragma unroll
+  for (int k = 0; k < kRows; ++k)
+    if (k < nrow && col) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
+  if (!pass) {
+#pragma unroll
+    for (int k = 0; k < kRows; ++k)
+      if (k < nrow && col) er[k] = ld_stream(err + base + (l0 + k) * chunks);
+  }
+  // the tile's outer neighbours: the row above the first wave, the row below
+  // the wave holding the tile's (or the sequence's) last row
+  const bool top = w == 0 && l0 > 0;
+  const bool last = nrow > 0 && (w == kTileWavesI - 1 || l0 + kRows >= len);
+  const bool bottom = last && l0 + nrow < len;
+  if (!pass && col && top) qr[0] = ld_stream(q + base + (l0 - 1) * chunks);
+  if (!pass && col && bottom) qr[kRows + 1] = ld_stream(q + base + (l0 + nrow) * chunks);
+  if (!pass) {
+    if (nrow > 0) {
+      edge[0][w][lane] = qr[1];
+      edge[1][w][lane] = qr[kRows];  // (a partial wave is the tile's last: never read)
+    }
+    __syncthreads();
+    if (nrow > 0 && col) {
+      if (l0 == 0) qr[0] = qr[1];                  // q[max(l-1, 0)]
+      else if (w > 0) qr[0] = edge[1][w - 1][lane];
+      if (!last) qr[kRows + 1] = edge[0][w + 1][lane];
+      else if (!bottom) qr[nrow + 1] = qr[nrow];   // q[min(l+1, len-1)]
+      else if (nrow < kRows) qr[nrow + 1] = qr[kRows + 1];
+    }
+  }
   uint32_t dbl = 0, over = 0;
-  const int64_t rblocks = (len + kRows - 1) / kRows;
-  const int64_t items = outer * rblocks * chunks;
-  for (int64_t it = (int64_t)blockIdx.x * kBlock + threadIdx.x; it < items;
-       it += (int64_t)gridDim.x * kBlock) {
-    const int64_t c = it % chunks;
-    const int64_t t = it / chunks;
-    const int64_t rb = t % rblocks;
-    const int64_t o = t / rblocks;
-    const int64_t l0 = rb * kRows;
-    const int64_t base = o * len * chunks + c;  // vector index of (o, l=0, c)
-    if (l0 + kRows <= len) {  // full row block
-      u32x4 qr[kRows + 2], er[kRows];
-      qr[0] = ld_stream(q + base + (l0 > 0 ? l0 - 1 : 0) * chunks);
 #pragma unroll
-      for (int k = 0; k < kRows; ++k) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
-      qr[kRows + 1] = ld_stream(q + base + (l0 + kRows < len ? l0 + kRows : len - 1) * chunks);
-      if (!pass) {
-#pragma unroll
-        for (int k = 0; k < kRows; ++k) er[k] = ld_stream(err + base + (l0 + k) * chunks);
-      }
-#pragma unroll
-      for (int k = 0; k < kRows; ++k) {
-        st_stream(out + base + (l0 + k) * chunks,
-                  pass ? qr[k + 1] : interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]));
-        if (RECORD) {
-          dbl |= seen_double(er[k]);
-          over |= seen_over15(qr[k + 1]);
-        }
-      }
-      continue;
-    }
-    const int nrow = (int)(len - l0);  // ragged last block
-    if (pass) {
-      for (int k = 0; k < nrow; ++k) out[base + (l0 + k) * chunks] = q[base + (l0 + k) * chunks];
-      continue;
-    }
-    u32x4 prev = q[base + (l0 > 0 ? l0 - 1 : 0) * chunks];
-    u32x4 cur = q[base + l0 * chunks];
-    for (int k = 0; k < nrow; ++k) {
-      const int64_t l = l0 + k;
-      u32x4 next = q[base + (l + 1 < len ? l + 1 : len - 1) * chunks];
-      u32x4 e = err[base + l * chunks];
-      out[base + l * chunks] = interp_vec(cur, prev, next, e);
-      if (RECORD) {
-        dbl |= seen_double(e);
-        over |= seen_over15(cur);
-      }
-      prev = cur;
-      cur = next;
+  for (int k = 0; k < kRows; ++k) {
+    if (k >= nrow || !col) break;
+    const u32x4 v = pass ? qr[k + 1] : interp_vec(qr[k + 1], qr[k], qr[k + 2], er[k]);
+    st_stream(out + base + (l0 + k) * chunks, v);
+    if (RECORD) {
+      dbl |= seen_double(er[k]);
+      over |= seen_over15(qr[k + 1]);
     }
   }
   if (RECORD) {
-    const bool d = __syncthreads_or(dbl != 0), o = __syncthreads_or(over != 0);
-    if (threadIdx.x == 0) {
-      if (d) flags[0] = epoch;
-      if (o) flags[1] = epoch;
+    const bool d = __any(dbl != 0), ov = __any(over != 0);
+    if (lane == 0) {
+      if (d && __builtin_nontemporal_load(flags) != epoch) flags[0] = epoch;
+      if (ov && __builtin_nontemporal_load(flags + 1) != epoch) flags[1] = epoch;
     }
   }
 }
@@ -265,10 +277,10 @@ static void launch_interp(const uint8_t *q, const uint8_t *err, uint8_t *out, in
                           int32_t epoch, hipStream_t st) {
   if (inner % 16 == 0 && aligned(q, 16) && aligned(err, 16) && aligned(out, 16)) {
     const int64_t chunks = inner / 16;
-    const int64_t items = outer * ((len + kRows - 1) / kRows) * chunks;
-    KVECC_LAUNCH((interp_vec_kernel<RECORD>), dim3(grid_for(items, kBlock, 16)), dim3(kBlock), 0,
-                 st, reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
-                 reinterpret_cast<u32x4 *>(out), outer, len, chunks, gate, flags, epoch);
+    const int64_t tiles = outer * ((len + kTileRows - 1) / kTileRows) * ((chunks + kWave - 1) / kWave);
+    KVECC_LAUNCH((interp_tile_kernel<RECORD>), dim3((unsigned)tiles), dim3(kTileThreads), 0, st,
+                 reinterpret_cast<const u32x4 *>(q), reinterpret_cast<const u32x4 *>(err),
+                 reinterpret_cast<u32x4 *>(out), len, chunks, gate, flags, epoch);
   } else {
     KVECC_LAUNCH((interp_scalar_kernel<RECORD>), dim3(grid_for(outer * len * inner, kBlock)),
                  dim3(kBlock), 0, st, q, err, out, outer, len, inner, gate, flags, epoch);

@@ -191,53 +191,54 @@ __global__ __launch_bounds__(kBlock) void decode_dequant_kernel(const uint8_t *_
   if (stats) flush_stats2(stats, n1, n2);
 }
 
-// 16 / sizeof(TO) codewords per lane per access (4 for fp32, 8 for fp16/bf16;
-// d must be a multiple): each lane reads 4 or 8 codeword bytes and writes one
-// contiguous 16-byte output vector, so every wave-instruction covers one
-// contiguous span; non-temporal, kU accesses in flight per lane.  Row indices
-// are a shift when the chunks per row are a power of two (shift >= 0), else a
-// 32-bit division (64-bit division is ~100 instructions).
-template <typename TO, int kU>
-__global__ __launch_bounds__(kBlock) void decode_dequant_wide_kernel(const uint32_t *__restrict__ cw,
+// Wave tiles: a wave owns T x 64 consecutive 16-byte output vectors (fp16 /
+// bf16: 8 codewords per vector, T = 4; fp32: 4 codewords, T = 2); load u and
+// store u of every lane cover one contiguous span (512 / 256 B of codewords,
+// 1 KiB of output) and the grid is full, so each wave writes T KiB and
+// retires.  At [8*4096*32, 128] (tools/exp/run_r05.py, profiles/r05/exp_r05.log)
+// fp16 66.2 vs 68.9 us for the grid-strided kernel (1 vector per wave: 83.9),
+// fp32 107.3 vs 119.7 (T = 4 / 8: 109.3 / 110.9).  Row scales: a shift when
+// the vectors per row are a power of two, else a 32-bit division.
+template <typename TO>
+constexpr int kDdTile = sizeof(TO) == 4 ? 2 : 4;
+template <typename TO>
+__global__ __launch_bounds__(kBlock) void decode_dequant_tile_kernel(const void *__restrict__ cwv,
                                                                      const float *__restrict__ scales,
-                                                                     TO *__restrict__ out,
-                                                                     uint32_t nchunk, int shift,
-                                                                     uint32_t total, int zero_doubles,
+                                                                     u32x4 *__restrict__ out, uint32_t nchunk,
+                                                                     int shift, uint32_t total, int zero_doubles,
                                                                      uint64_t *__restrict__ stats) {
-  constexpr int kW = 4 / sizeof(TO);  // codeword words per access
+  constexpr int T = kDdTile<TO>, kW = 4 / (int)sizeof(TO);  // codeword words per vector
   using InT = typename std::conditional<kW == 1, uint32_t, u32x2>::type;
-  const uint32_t stride = gridDim.x * kBlock;
+  const InT *cw = reinterpret_cast<const InT *>(cwv);
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) / kWave;
+  const uint32_t base = wave * (kWave * T) + lane;
   uint32_t n1 = 0, n2 = 0;
-  auto one = [&](InT in, uint32_t i) {
-    uint32_t w[kW];
-    __builtin_memcpy(w, &in, sizeof(in));
-    const float s = scales[shift >= 0 ? i >> shift : i / nchunk];
-    TO o[4 * kW];
+  InT w[T];
+  float s[T];
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    const uint32_t i = base + u * kWave;
+    w[u] = i < total ? ld_stream(cw + i) : InT{};  // codeword 0: no error counted
+    s[u] = i < total ? scales[shift >= 0 ? i >> shift : i / nchunk] : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    const uint32_t i = base + u * kWave;
+    uint32_t wd[kW], nb[2] = {0u, 0u};
+    __builtin_memcpy(wd, &w[u], sizeof(wd));
 #pragma unroll
     for (int k = 0; k < kW; ++k) {
       uint32_t q, t;
-      h84_decode4(w[k], q, t, n1, n2);
+      h84_decode4(wd[k], q, t, n1, n2);
       if (zero_doubles) {  // double errors -> data 0 (fused_kernels.py:344)
-        const uint32_t dbl = (t >> 1) & ~t & 0x01010101u;  // type == 2
+        const uint32_t dbl = (t >> 1) & ~t & 0x01010101u;
         q &= ~(dbl * 0xFFu);
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[4 * k + e] = from_f32<TO>(dequant1(q >> (8 * e) & 0xFFu, s));
+      nb[k] = q;
     }
-    u32x4 b;
-    __builtin_memcpy(&b, o, 16);
-    st_stream(reinterpret_cast<u32x4 *>(out) + i, b);
-  };
-  const InT *src = reinterpret_cast<const InT *>(cw);
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  for (; i + (kU - 1) * stride < total; i += kU * stride) {
-    InT w[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) w[u] = ld_stream(src + i + u * stride);
-#pragma unroll
-    for (int u = 0; u < kU; ++u) one(w[u], i + u * stride);
+    if (i < total) st_stream(out + i, dq16<TO>(nb, s[u], false));
   }
-  for (; i < total; i += stride) one(ld_stream(src + i), i);
   if (stats) flush_stats2(stats, n1, n2);
 }
 
@@ -279,9 +280,6 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
   }
 }
 
-// fp16/bf16 decode+dequant workgroups per CU (grid cap): 64 measured best
-// against 16 / 32 / 256 (73.4 vs 77.8 / 74.4 / 103.3 us fp16; profiles/r03/dd_ab2.log)
-constexpr int kDdPerCu = 64;
 template <typename TO>
 static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t rows, int64_t d,
                       int zero_doubles, uint64_t *stats, hipStream_t st) {
@@ -291,17 +289,10 @@ static void launch_dd(const uint8_t *cw, const float *scales, void *out, int64_t
     const uint32_t total = (uint32_t)(rows * (d / kCw));
     const uint32_t nchunk = (uint32_t)(d / kCw);
     const int shift = (nchunk & (nchunk - 1)) == 0 ? __builtin_ctz(nchunk) : -1;
-    // deep grids, few accesses in flight per lane (tools/exp/run_dequant.py at
-    // [8,4096,32,128]): fp16/bf16 1 access and 64 workgroups per CU, 86.8 ->
-    // 76.2 us; fp32 4 accesses and 128 per CU, 131.8 -> 119.5 us
-    if (sizeof(TO) == 2)
-      KVECC_LAUNCH((decode_dequant_wide_kernel<TO, 1>), dim3(grid_for(total, kBlock, kDdPerCu)),
-                   dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o, nchunk,
-                   shift, total, zero_doubles, stats);
-    else
-      KVECC_LAUNCH((decode_dequant_wide_kernel<TO, 4>), dim3(grid_for(total, kBlock * 4, 128)),
-                   dim3(kBlock), 0, st, reinterpret_cast<const uint32_t *>(cw), scales, o, nchunk,
-                   shift, total, zero_doubles, stats);
+    // full-grid wave tiles (decode_dequant_tile_kernel)
+    KVECC_LAUNCH((decode_dequant_tile_kernel<TO>), dim3((unsigned)cdiv(total, (int64_t)kBlock * kDdTile<TO>)),
+                 dim3(kBlock), 0, st, cw, scales, reinterpret_cast<u32x4 *>(out), nchunk, shift, total,
+                 zero_doubles, stats);
   } else if (d % 4 == 0 && aligned(cw, 4) && aligned(out, 4 * sizeof(TO))) {
     int64_t total = rows * (d / 4);
     KVECC_LAUNCH((decode_dequant_kernel<TO, 4>), dim3(grid_for(total, kBlock)), dim3(kBlock),

@@ -222,3 +222,46 @@ def test_packed_decode_sweep_hip_vs_host(gpu, case):
     # nothing written outside the outputs
     assert bool((out_big[:off] == 0xEE).all()) and bool((out_big[off + n_out:] == 0xEE).all()), case
     assert bool((flag_big[:off] == 0xEE).all()) and bool((flag_big[off + n_flag:] == 0xEE).all()), case
+
+
+# ---- interpolation (workgroup tiles of 64 column chunks x 32 positions) -------------
+
+def _interp_cases():
+    rng = random.Random(4242)
+    cases = []
+    for i in range(24):
+        inner = rng.choice([16, 48, 160, 1008, 1024, 1040, 4096, 24, 7])
+        length = rng.choice([1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 65, 100, 257])
+        outer = rng.choice([1, 2, 3, 5])
+        cases.append((i, outer, length, inner, rng.choice([0.0, 0.02, 0.3])))
+    return cases
+
+
+INTERP_CASES = _interp_cases()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", INTERP_CASES, ids=[f"i{c[0]}" for c in INTERP_CASES])
+def test_interp_tile_sweep_hip_vs_oracle(gpu, oracle, case):
+    """interpolate_double_errors along the middle axis of [outer, len, inner] at
+    ragged lengths (tiles that end mid-wave, waves that end mid-tile), column
+    counts that leave a partial 64-chunk group, and the scalar path (inner % 16
+    != 0); both the gated kernel and the recording pass (the API)."""
+    import numpy as np
+
+    import kvecc
+    from kvecc import ops
+    i, outer, length, inner, pdbl = case
+    rng = np.random.default_rng(i)
+    q = rng.integers(0, 16, size=(outer, length, inner), dtype=np.int64).astype(np.uint8)
+    e = rng.choice(np.array([0, 1, 2, 3], np.uint8), size=q.shape,
+                   p=[1 - pdbl - 0.1, 0.05, pdbl, 0.05])
+    want = oracle.interpolate_double_errors(q, e, seq_dim=1)
+    got = kvecc.interpolate_double_errors(torch.from_numpy(q).to(gpu), torch.from_numpy(e).to(gpu), seq_dim=1)
+    assert np.array_equal(got.cpu().numpy(), want), case
+    # the plain kernel (every element through the formula) against the oracle's kernel semantics
+    out = torch.empty(q.size, dtype=torch.uint8, device=gpu)
+    ops.interpolate_into(torch.from_numpy(q).to(gpu).view(-1), torch.from_numpy(e).to(gpu).view(-1), out,
+                         outer, length, inner)
+    assert np.array_equal(out.cpu().numpy().reshape(q.shape),
+                          oracle.interpolate_kernel(q, e, outer, length, inner).reshape(q.shape)), case

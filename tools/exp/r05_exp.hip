@@ -164,9 +164,60 @@ __global__ __launch_bounds__(kBlock) void interp_rec_kernel(const u32x4 *__restr
   }
 }
 
+// decode + dequantize to fp32, wave tiles of T x 64 output vectors (4 codewords
+// per lane per vector), full grid
+template <int T, int BS>
+__global__ __launch_bounds__(BS) void dd32_tile_kernel(const uint32_t *__restrict__ cw,
+                                                       const float *__restrict__ scales,
+                                                       u32x4 *__restrict__ out, uint32_t total,
+                                                       int shift, uint64_t *__restrict__ stats) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * BS + threadIdx.x) >> 6;
+  const uint32_t base = wave * (64 * T) + lane;
+  uint32_t n1 = 0, n2 = 0;
+  uint32_t w[T];
+  float s[T];
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    const uint32_t i = base + u * 64;
+    w[u] = i < total ? ld_stream(cw + i) : 0u;
+    s[u] = i < total ? scales[i >> shift] : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < T; ++u) {
+    const uint32_t i = base + u * 64;
+    uint32_t q, t;
+    h84_decode4(w[u], q, t, n1, n2);
+    const uint32_t dbl = (t >> 1) & ~t & 0x01010101u;
+    uint32_t nb[1] = {q & ~(dbl * 0xFFu)};
+    const u32x4 o = dq16<float>(nb, s[u], false);
+    if (i < total) st_stream(out + i, o);
+  }
+  flush_stats2<BS>(stats, n1, n2);
+}
+
 }  // namespace kvecc
 
 using namespace kvecc;
+
+extern "C" KVECC_API int r05_dd32(int v, const void *cw, const float *sc, void *out, int64_t rows, int64_t d,
+                                  uint64_t *stats, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t nchunk = (uint32_t)(d / 4), total = (uint32_t)(rows * nchunk);
+  const int shift = __builtin_ctz(nchunk);
+  switch (v) {
+#define DD32(V, T, BS)                                                                                \
+  case V:                                                                                             \
+    hipLaunchKernelGGL((dd32_tile_kernel<T, BS>), dim3((total + 64 * T * (BS / 64) - 1) / (64 * T * (BS / 64))), \
+                       dim3(BS), 0, s, (const uint32_t *)cw, sc, (u32x4 *)out, total, shift, stats);   \
+    break;
+    DD32(0, 2, 256) DD32(1, 4, 256) DD32(2, 8, 256) DD32(3, 4, 512) DD32(4, 8, 512)
+#undef DD32
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
 
 extern "C" KVECC_API int r05_interp_rec(int mode, const void *q, const void *e, void *o, int64_t outer,
                                         int64_t len, int64_t chunks, int32_t *flags, int32_t epoch,

@@ -21,6 +21,7 @@ lib.r05_interp.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_in
 lib.r05_interp_rec.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP,
                                ctypes.c_int32, VP]
 lib.r05_dd.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
+lib.r05_dd32.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
 dev = torch.device("cuda:0")
 S = VP(torch.cuda.current_stream().cuda_stream)
 ROUNDS = int(os.environ.get("ROUNDS", "8"))
@@ -107,3 +108,27 @@ if which in ("dd", "all"):
         print(f"dd {k}: rc={rc} equal={torch.equal(out, ref)} stats={ops.read_stats(st) == ops.read_stats(st0)}",
               flush=True)
     ab(cases, rows * (3 * D + 4), "dd_fp16")
+
+if which in ("dd32", "all"):
+    rows = B * L * H
+    g = torch.Generator().manual_seed(1)
+    cw = ops.hamming84_encode(torch.randint(0, 16, (rows * D,), generator=g, dtype=torch.uint8).to(dev))
+    ops.inject_into(cw, cw, 1e-3, 8, seed=42)
+    cw = cw.view(rows, D)
+    sc = (torch.rand(rows, generator=g) * 0.1 + 0.01).to(dev)
+    ref = torch.empty(rows, D, dtype=torch.float32, device=dev)
+    st0 = ops.new_stats(dev)
+    ops.decode_dequant_h84_into(cw, sc, ref, True, st0)
+    out = torch.empty_like(ref)
+    st = ops.new_stats(dev)
+    cases = {"prod": lambda: ops.decode_dequant_h84_into(cw, sc, out, True, st)}
+    for v in range(5):
+        cases[f"v{v}"] = (lambda v=v: lib.r05_dd32(v, P(cw), P(sc), P(out), rows, D, P(st), S))
+    for k, fn in cases.items():
+        out.fill_(float("nan"))
+        st.zero_()
+        rc = fn()
+        torch.cuda.synchronize()
+        print(f"dd32 {k}: rc={rc if isinstance(rc, int) else 0} equal={torch.equal(out, ref)} "
+              f"stats={ops.read_stats(st) == ops.read_stats(st0)}", flush=True)
+    ab(cases, rows * (5 * D + 4), "dd_fp32")
