@@ -21,6 +21,8 @@ lib.r05_interp.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_in
 lib.r05_interp_rec.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, VP,
                                ctypes.c_int32, VP]
 lib.r05_dd.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
+lib.r05_quant.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP]
+lib.r05_rows_enc.argtypes = [ctypes.c_int, VP, VP, ctypes.c_int64, ctypes.c_int64, VP]
 lib.r05_dd32.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
 dev = torch.device("cuda:0")
 S = VP(torch.cuda.current_stream().cuda_stream)
@@ -132,3 +134,42 @@ if which in ("dd32", "all"):
         print(f"dd32 {k}: rc={rc if isinstance(rc, int) else 0} equal={torch.equal(out, ref)} "
               f"stats={ops.read_stats(st) == ops.read_stats(st0)}", flush=True)
     ab(cases, rows * (5 * D + 4), "dd_fp32")
+
+if which in ("quant", "all"):
+    from kvecc import _lib
+    rows = B * L * H
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(rows, D, generator=g).to(dev).to(torch.float16)
+    cw0 = torch.empty(rows, D, dtype=torch.uint8, device=dev)
+    sc0 = torch.empty(rows, dtype=torch.float32, device=dev)
+    ops.quantize_encode_rows_into(x, _lib.CODEC_H84, cw0, sc0)
+    cw = torch.empty_like(cw0)
+    sc = torch.empty_like(sc0)
+    cases = {"prod": lambda: ops.quantize_encode_rows_into(x, _lib.CODEC_H84, cw, sc)}
+    for v in range(4):
+        cases[f"v{v}"] = (lambda v=v: lib.r05_quant(v, P(x), P(cw), P(sc), rows, D, S))
+    for k, fn in cases.items():
+        cw.zero_()
+        sc.zero_()
+        fn()
+        torch.cuda.synchronize()
+        print(f"quant {k}: equal={torch.equal(cw, cw0) and torch.equal(sc, sc0)}", flush=True)
+    ab(cases, rows * (3 * D + 4), "quant_fp16")
+
+if which in ("rows", "all"):
+    rows = B * L * H
+    g = torch.Generator().manual_seed(9)
+    x = torch.randint(0, 16, (rows, D), generator=g, dtype=torch.uint8).to(dev)
+    G = (D + 2) // 3
+    ref = torch.empty(rows, G, dtype=torch.int32, device=dev)
+    ops.golay_encode_rows_into(x, ref)
+    out = torch.empty_like(ref)
+    cases = {"prod": lambda: ops.golay_encode_rows_into(x, out)}
+    for v in range(3):
+        cases[f"v{v}"] = (lambda v=v: lib.r05_rows_enc(v, P(x), P(out), rows, D, S))
+    for k, fn in cases.items():
+        out.zero_()
+        rc = fn()
+        torch.cuda.synchronize()
+        print(f"rows_enc {k}: rc={rc} equal={torch.equal(out, ref)}", flush=True)
+    ab(cases, rows * (D + 4 * G), "rows_enc")
