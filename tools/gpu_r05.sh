@@ -43,6 +43,14 @@ for s in $STEPS; do
     exp)    run exp_r05 600 python tools/exp/run_r05.py all ;;
     valu)   run valu_rate 300 python tools/exp/run_valu_rate.py ;;
     mc)     run mc_time 300 python tools/mc_time.py ;;
+    gqapmc) run gqa_pmc 900 bash tools/gpu_attn_gqa_pmc.sh "$TAG" ;;
+    configs) run configs 600 python tools/bench_configs.py ;;
+    shim)   run shim_eager 300 python tools/bench_shim.py
+            run shim_graph 300 python tools/bench_shim.py --graph ;;
+    attn)   run attn_mha 300 python tools/bench_attention.py --codec hamming84
+            run attn_gqa 300 python tools/bench_attention.py --codec hamming84 --kv-heads 8
+            run attn_pk 300 python tools/bench_attention.py --codec golay_packed
+            run attn_pk_gqa 300 python tools/bench_attention.py --codec golay_packed --kv-heads 8 ;;
     mcprof) run mc_trace 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/mc_trace" -o t -- \
               python "$ROOT/tools/mc_time.py" --only fused ;;
     injpmc)

@@ -2,7 +2,7 @@
 rocprofv3 kernel trace (and HBM counters) of the same bench.py command.
 
 The trace is taken WITHOUT name truncation, so template instances that share a
-kernel name (the int32 and packed fused Golay reads, interp_vec_kernel<false>
+kernel name (the int32 and packed fused Golay reads, interp_tile_kernel<false>
 and <true>, fp16 and fp32 decode+dequantize) are separate entries: no entry
 carries another configuration's average.  HBM traffic per launch = FETCH_SIZE
 x 2 (gfx950 tallies 128-B streaming reads at 64 B, MI355X_MICROARCH.md, HBM
@@ -42,13 +42,13 @@ SECTIONS = {
                           ("golay_rows", "kernel_ms", "decode")),
     "golay_rows.encode": ("golay_encode_rows_reg_kernel", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "encode")),
-    "interp": ("interp_vec_kernel<false>", ("interp", "bytes_per_launch"), ("interp", "kernel_ms")),
-    "interp.api": ("interp_vec_kernel<true>", ("interp", "api", "bytes_per_launch"), ("interp", "api", "kernel_ms")),
+    "interp": ("interp_tile_kernel<false>", ("interp", "bytes_per_launch"), ("interp", "kernel_ms")),
+    "interp.api": ("interp_tile_kernel<true>", ("interp", "api", "bytes_per_launch"), ("interp", "api", "kernel_ms")),
     "quantize_encode": ("quantize_encode_1c_kernel<__half", ("fused_quant", "quantize_encode", "bytes_per_launch"),
                         ("fused_quant", "quantize_encode", "kernel_ms")),
-    "decode_dequant": ("decode_dequant_wide_kernel<__half, 1>", ("fused_quant", "decode_dequant", "bytes_per_launch"),
+    "decode_dequant": ("decode_dequant_tile_kernel<__half>", ("fused_quant", "decode_dequant", "bytes_per_launch"),
                        ("fused_quant", "decode_dequant", "kernel_ms")),
-    "decode_dequant_fp32": ("decode_dequant_wide_kernel<float, 4>",
+    "decode_dequant_fp32": ("decode_dequant_tile_kernel<float>",
                             ("fused_quant", "decode_dequant_fp32", "bytes_per_launch"),
                             ("fused_quant", "decode_dequant_fp32", "kernel_ms")),
     "inject": ("inject_kernel<int, 24, false, true>", None, ("inject", "ms")),
