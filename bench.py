@@ -197,10 +197,10 @@ def interp_bench(dev, steps, warmup):
     out = torch.empty_like(q)
     ms = kernel_ms(dev, lambda: ops.interpolate_into(q, et, out, B, L, H * D), steps, warmup)
     ms_api = kernel_ms(dev, lambda: ops.interpolate_auto_into(q, et, out, B, L, H * D), steps, warmup)
-    r = hbm_roofline("interp_vec_kernel<false>", 3 * n, ms, "3 B/element (q, err in; out)")
+    r = hbm_roofline("interp_tile_kernel<false>", 3 * n, ms, "3 B/element (q, err in; out)")
     r.update({"workload": "interpolate_double_errors along L of the H(8,4) decode of [8,4096,32,128], BER 1e-3",
               "doubles": int((et == 2).sum()),
-              "api": hbm_roofline("interp_vec_kernel<true> (kvecc_interpolate_auto)", 3 * n, ms_api,
+              "api": hbm_roofline("interp_tile_kernel<true> (kvecc_interpolate_auto)", 3 * n, ms_api,
                                   "3 B/element"),
               "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} "
                         "warm-up calls and >= 0.25 s"})
@@ -222,13 +222,13 @@ def quant_bench(dev, steps, warmup):
     del x
     ops.inject_into(cw.view(-1), cw.view(-1), 1e-3, 8, seed=SEED)
     st = ops.new_stats(dev)
-    res = {"quantize_encode": hbm_roofline("quant_encode_kernel (fp16 -> H84)", rows * (3 * D + 4), ms_q,
+    res = {"quantize_encode": hbm_roofline("quantize_encode_tile_kernel (fp16 -> H84)", rows * (3 * D + 4), ms_q,
                                            "D*3+4 B/row (fp16 in, codeword + fp32 scale out)")}
     for name, dt, per in (("decode_dequant", torch.float16, 3 * D + 4),
                           ("decode_dequant_fp32", torch.float32, 5 * D + 4)):
         out = torch.empty(rows, D, dtype=dt, device=dev)
         ms = kernel_ms(dev, lambda: ops.decode_dequant_h84_into(cw, sc, out, True, st), steps, warmup)
-        res[name] = hbm_roofline(f"decode_dequant_h84_kernel (-> {str(dt)[6:]})", rows * per, ms,
+        res[name] = hbm_roofline(f"decode_dequant_tile_kernel (-> {str(dt)[6:]})", rows * per, ms,
                                  f"{'D*3+4' if per == 3 * D + 4 else 'D*5+4'} B/row (codeword + scale in, "
                                  f"{str(dt)[6:]} out)")
         del out

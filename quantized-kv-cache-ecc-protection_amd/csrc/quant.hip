@@ -78,79 +78,78 @@ __global__ __launch_bounds__(kBlock) void quantize_encode_kernel(const T *__rest
 }
 
 // Rows of at most 64 chunks (every row of the shim and the reference's tests):
-// each lane loads its one 16-byte chunk ONCE, non-temporally.  One row group
-// per wave-iteration and a deep grid (64 workgroups per CU, ~4 iterations per
-// wave) beat two groups in flight per iteration with 16 per CU, and a prefetch
-// of the next iteration's chunk: fp16 D=128 rows 77.7 -> 68.2 us
-// (tools/exp/run_quant.py).
+// each lane loads its one 16-byte chunk ONCE, non-temporally, on a full grid of
+// wave tiles -- a wave owns kQeTile row groups (64 / LPR rows each), issues all
+// their loads first, then quantizes and encodes them, and workgroups retire
+// instead of striding.  fp16 D=128 rows: 71.2 -> 63.2 us against round 4's
+// grid-strided one-group-per-iteration kernel (64 workgroups per CU), 77.6 with
+// one group per wave (profiles/r05/exp_r05e.log quant_fp16 v0-v3; 4 groups per
+// wave 63.2 as well).
+constexpr int kQeTile = 2;
 template <typename T, int VEC, int LPR>
-__global__ __launch_bounds__(kBlock) void quantize_encode_1c_kernel(const T *__restrict__ x, int codec,
-                                                                    int rule, uint8_t *__restrict__ cw,
-                                                                    float *__restrict__ scales,
-                                                                    int64_t rows, int64_t d) {
+__global__ __launch_bounds__(kBlock) void quantize_encode_tile_kernel(const T *__restrict__ x, int codec,
+                                                                      int rule, uint8_t *__restrict__ cw,
+                                                                      float *__restrict__ scales,
+                                                                      int64_t rows, int64_t d) {
   static_assert(sizeof(T) * VEC == 16, "one 16-byte chunk per lane");
-  constexpr int kU = 1;
   constexpr int rows_per_wave = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int sub = lane / LPR, li = lane % LPR;
   const int64_t nchunk = d / VEC;
-  const int64_t waves = (int64_t)gridDim.x * (kBlock / kWave);
   const int64_t wave_id = (int64_t)blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
-  const int64_t step = waves * rows_per_wave;
-  for (int64_t r0 = wave_id * rows_per_wave; r0 < rows; r0 += kU * step) {
-    Vec<T, VEC> v[kU];
-    bool live[kU];
+  const int64_t r0 = wave_id * rows_per_wave * kQeTile + sub;
+  Vec<T, VEC> v[kQeTile];
+  bool live[kQeTile];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t r = r0 + u * step + sub;
-      live[u] = r < rows && li < nchunk;
-      if (live[u]) {
-        const u32x4 raw = ld_stream(reinterpret_cast<const u32x4 *>(x + r * d + li * VEC));
-        __builtin_memcpy(&v[u], &raw, 16);
-      }
+  for (int u = 0; u < kQeTile; ++u) {
+    const int64_t r = r0 + u * rows_per_wave;
+    live[u] = r < rows && li < nchunk;
+    if (live[u]) {
+      const u32x4 raw = ld_stream(reinterpret_cast<const u32x4 *>(x + r * d + li * VEC));
+      __builtin_memcpy(&v[u], &raw, 16);
     }
+  }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t r = r0 + u * step + sub;
-      float f[VEC];
-      float amax = 0.0f;
+  for (int u = 0; u < kQeTile; ++u) {
+    const int64_t r = r0 + u * rows_per_wave;
+    float f[VEC];
+    float amax = 0.0f;
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        f[k] = live[u] ? to_f32<T>(v[u].v[k]) : 0.0f;
-        amax = fmaxf(amax, fabsf(f[k]));
-      }
-      amax = group_max_nonneg<LPR>(amax);
-      const float scale = row_scale(amax, rule);
-      if (!live[u]) continue;
-      if (li == 0) scales[r] = scale;
-      // x / scale: reciprocal + FMA correction for 16-bit inputs (codec_math.h
-      // div_recip, exhaustively checked), IEEE division otherwise
-      uint32_t nq[VEC];
-      if (sizeof(T) == 2 && recip_ok(scale)) {
-        const float inv = div_rn(1.0f, scale);
+    for (int k = 0; k < VEC; ++k) {
+      f[k] = live[u] ? to_f32<T>(v[u].v[k]) : 0.0f;
+      amax = fmaxf(amax, fabsf(f[k]));
+    }
+    amax = group_max_nonneg<LPR>(amax);
+    const float scale = row_scale(amax, rule);
+    if (!live[u]) continue;
+    if (li == 0) scales[r] = scale;
+    // x / scale: reciprocal + FMA correction for 16-bit inputs (codec_math.h
+    // div_recip, exhaustively checked), IEEE division otherwise
+    uint32_t nq[VEC];
+    if (sizeof(T) == 2 && recip_ok(scale)) {
+      const float inv = div_rn(1.0f, scale);
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) nq[k] = nibble_of_quotient(div_recip(f[k], scale, inv));
-      } else {
+      for (int k = 0; k < VEC; ++k) nq[k] = nibble_of_quotient(div_recip(f[k], scale, inv));
+    } else {
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) nq[k] = quantize_nibble(f[k], scale);
-      }
-      // four quantized nibbles per word, encoded SWAR (codec_math.h)
-      uint32_t wds[VEC / 4];
+      for (int k = 0; k < VEC; ++k) nq[k] = quantize_nibble(f[k], scale);
+    }
+    // four quantized nibbles per word, encoded SWAR (codec_math.h)
+    uint32_t wds[VEC / 4];
 #pragma unroll
-      for (int k = 0; k < VEC / 4; ++k) {
-        uint32_t wq = 0;
+    for (int k = 0; k < VEC / 4; ++k) {
+      uint32_t wq = 0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) wq |= nq[4 * k + e] << (8 * e);
-        wds[k] = codec == KVECC_CODEC_H84 ? h84_encode4(wq)
-                 : codec == KVECC_CODEC_H74 ? h74_encode4(wq)
-                                            : wq;
-      }
-      if (VEC == 8) {
-        uint64_t bits = (uint64_t)wds[0] | (uint64_t)wds[VEC / 4 - 1] << 32;
-        st_stream(reinterpret_cast<uint64_t *>(cw + r * d + li * VEC), bits);
-      } else {
-        st_stream(reinterpret_cast<uint32_t *>(cw + r * d + li * VEC), wds[0]);
-      }
+      for (int e = 0; e < 4; ++e) wq |= nq[4 * k + e] << (8 * e);
+      wds[k] = codec == KVECC_CODEC_H84 ? h84_encode4(wq)
+               : codec == KVECC_CODEC_H74 ? h74_encode4(wq)
+                                          : wq;
+    }
+    if (VEC == 8) {
+      uint64_t bits = (uint64_t)wds[0] | (uint64_t)wds[VEC / 4 - 1] << 32;
+      st_stream(reinterpret_cast<uint64_t *>(cw + r * d + li * VEC), bits);
+    } else {
+      st_stream(reinterpret_cast<uint32_t *>(cw + r * d + li * VEC), wds[0]);
     }
   }
 }
@@ -256,11 +255,12 @@ static void launch_qe(const void *x, int codec, int rule, uint8_t *cw, float *sc
   bool vec = d % V == 0 && aligned(x, 16) && aligned(cw, V);
   if (vec && d / V <= kWave) {
     const int lpr = lanes_per_row(d / V);
-    const unsigned grid = grid_for(cdiv(rows, kWave / lpr), kBlock / kWave, 64);
-#define KVECC_QE1C(L)                                                                         \
-  case L:                                                                                     \
-    KVECC_LAUNCH((quantize_encode_1c_kernel<T, V, L>), dim3(grid), dim3(kBlock), 0, st, xt, \
-                       codec, rule, cw, scales, rows, d);                                     \
+    const int64_t waves = cdiv(rows, (int64_t)(kWave / lpr) * kQeTile);
+    const unsigned grid = (unsigned)cdiv(waves, kBlock / kWave);
+#define KVECC_QE1C(L)                                                                           \
+  case L:                                                                                       \
+    KVECC_LAUNCH((quantize_encode_tile_kernel<T, V, L>), dim3(grid), dim3(kBlock), 0, st, xt, \
+                 codec, rule, cw, scales, rows, d);                                             \
     break;
     switch (lpr) {
       KVECC_QE1C(1) KVECC_QE1C(2) KVECC_QE1C(4) KVECC_QE1C(8) KVECC_QE1C(16) KVECC_QE1C(32)

@@ -34,13 +34,13 @@ DEFAULT = [
 ]
 
 
-def golay_caches(dev, packed, gen, nb):
+def golay_caches(dev, packed, gen, nb, ber=1e-2):
     g = (D + 2) // 3
     out = []
     for side in range(2):
         x = torch.randint(0, 16, (nb, 1, H, BS, D), generator=gen, dtype=torch.uint8).to(dev)
         cw = ops.golay_encode_rows(x).view(-1)
-        ops.inject_into(cw, cw, 1e-2, 24, seed=42 + side)
+        ops.inject_into(cw, cw, ber, 24, seed=42 + side)
         cw = cw.view(nb, 1, H, BS * g)
         if packed:
             cw = torch.stack([(cw >> (8 * k)) & 0xFF for k in range(3)], -1).to(torch.uint8)

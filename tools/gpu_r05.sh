@@ -44,6 +44,9 @@ for s in $STEPS; do
     valu)   run valu_rate 300 python tools/exp/run_valu_rate.py ;;
     mc)     run mc_time 300 python tools/mc_time.py ;;
     gqapmc) run gqa_pmc 900 bash tools/gpu_attn_gqa_pmc.sh "$TAG" ;;
+    gtf)    run gtf 600 python tools/exp/run_golay_tf_exp.py ;;
+    qtest)  run pytest_quant 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -k "quant or fused or dequant" \
+              --timeout 300 --timeout-method thread ;;
     configs) run configs 600 python tools/bench_configs.py ;;
     shim)   run shim_eager 300 python tools/bench_shim.py
             run shim_graph 300 python tools/bench_shim.py --graph ;;
