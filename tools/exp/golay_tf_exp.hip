@@ -26,7 +26,9 @@
 // the wave's staged tile (ds_xor), which phase 2 dequantizes as the product.
 //
 // VAR 0: the decoder above; 1: syndromes only, no queues (WRONG values: the
-// cost of the error path); 2: fast rounds only (WRONG on mixed errors).
+// cost of the error path); 2: fast rounds only (WRONG on mixed errors);
+// 3: the queued syndromes' corrections gathered from the global 16 KiB
+// correction table (L2-resident), 4 rounds of gathers in flight.
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/shim.hip"
 
 namespace kvecc {
@@ -133,6 +135,26 @@ __global__ __launch_bounds__(kTileBlock) void golay_tf_kernel(ShimTileArgs a) {
   // read), then decoded by slow rounds
   auto drain = [&]() {
     wave_lds_sync();
+    if (VAR == 3) {  // correction entries from the global table, 4 rounds' gathers in flight
+      const uint32_t *cor = a.atab + 4096;
+      for (uint32_t base = 0; base < fq_n; base += 4 * kWave) {
+        uint32_t e[4], c[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool on = base + k * kWave + lane < fq_n;
+          e[k] = on ? fq[base + k * kWave + lane] : 0u;
+          c[k] = on ? cor[e[k] & 0xFFFu] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (c[k] & 0x000F0F0Fu) tf_xor(stage, e[k] >> 12, c[k] & 0x000F0F0Fu);
+          bits += (c[k] >> 24) & 63u;
+          unc += c[k] >> 30;
+        }
+      }
+      fq_n = 0;
+      return;
+    }
     uint32_t sq_n = 0;
     for (uint32_t base = 0; base < fq_n; base += kWave) {
       const uint32_t cnt = min(fq_n - base, (uint32_t)kWave);
@@ -222,6 +244,8 @@ const Variant kVariants[] = {
     {"tf_fastonly", golay_tf_kernel<false, 2>},
     {"pk_tf", golay_tf_kernel<true, 0>},
     {"pk_tf_synonly", golay_tf_kernel<true, 1>},
+    {"gq", golay_tf_kernel<false, 3>},
+    {"pk_gq", golay_tf_kernel<true, 3>},
 };
 
 }  // namespace exp

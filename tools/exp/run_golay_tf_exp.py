@@ -25,7 +25,7 @@ from kvecc import _lib, ops  # noqa: E402
 from run_golay_read_exp import B, BS, D, H, L, golay_caches  # noqa: E402
 
 ROUNDS = int(os.environ.get("ROUNDS", "30"))
-DEFAULT = ["tf:0", "tf_fastonly:0", "tf_synonly:0", "pk_tf:0", "pk_tf_synonly:0"]
+DEFAULT = ["gq:0", "tf_fastonly:0", "tf_synonly:0", "pk_gq:0", "pk_tf_synonly:0"]
 
 
 def main():
