@@ -394,7 +394,7 @@ def rows_bench(dev, x, noisy_rows, steps, warmup):
     dec = sum(e[2].elapsed_time(e[3]) for e in ev) / steps
     nbytes = rows * (D + 4 * ((D + 2) // 3))
     return {"workload": "golay_encode_rows / golay_decode_rows, [8,4096,32,128] (43 codewords per head row)",
-            "kernels": ["golay_encode_rows_reg_kernel", "golay_decode_rows_reg_kernel"],
+            "kernels": ["golay_encode_rows_full_kernel", "golay_decode_rows_reg_kernel"],
             "kernel_ms": {"encode": enc, "decode": dec}, "bytes_per_launch": nbytes,
             "hbm_gbs": {"encode": nbytes / (enc * 1e-3) / 1e9, "decode": nbytes / (dec * 1e-3) / 1e9},
             "frac": {"encode": nbytes / (enc * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -595,12 +595,25 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
   }
 }
 
-__global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRowsArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t par[4096];
-  __shared__ __attribute__((aligned(16))) uint8_t in_all[kRegWaves][kRegEncIn];
-  __shared__ __attribute__((aligned(16))) uint8_t out_all[kRegWaves][kRegEncOut];
-  for (int i = threadIdx.x; i < 512; i += kRegBlock)
-    reinterpret_cast<u32x4 *>(par)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
+// Per-head rows encode on a full grid: one tile of `tr` rows per wave,
+// workgroups of kEncRowWaves waves retiring (no schedule, no counter slot).
+// The parity comes from two 64-entry tables, parity(d) = T[d & 63] ^ T[64 + (d >> 6)]
+// (256 B of LDS per workgroup, conflict-free), not the 8 KiB table a
+// persistent grid could afford to stage: [8,4096,32,128] 56.9 -> 55.8 us
+// (profiles/r05/exp_r05e.log rows_enc v0; 8-wave workgroups 60.1, 2-wave 56.7).
+// Phase 1 lands the tile's nibble rows in LDS (16-byte loads of the contiguous
+// tile), phase 2 packs 4 codewords per lane into an LDS codeword tile, phase 3
+// stores it contiguously in 16-byte non-temporal stores.
+constexpr int kEncRowWaves = 4;
+__global__ __launch_bounds__(kEncRowWaves * kWave) void golay_encode_rows_full_kernel(RegRowsArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t tlo[64], thi[64];
+  __shared__ __attribute__((aligned(16))) uint8_t in_all[kEncRowWaves][kRegEncIn];
+  __shared__ __attribute__((aligned(16))) uint8_t out_all[kEncRowWaves][kRegEncOut];
+  if (threadIdx.x < 64) {
+    const uint16_t *par = reinterpret_cast<const uint16_t *>(a.tab);
+    tlo[threadIdx.x] = par[threadIdx.x];
+    thi[threadIdx.x] = par[threadIdx.x << 6];
+  }
   const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
   uint8_t *sin = in_all[wave];
   uint32_t *sout = reinterpret_cast<uint32_t *>(out_all[wave]);
@@ -612,61 +625,46 @@ __global__ __launch_bounds__(kRegBlock) void golay_encode_rows_reg_kernel(RegRow
   const RegItems it(lane, a.gpr, d16);
   const uint8_t *nib = reinterpret_cast<const uint8_t *>(a.src);
   uint32_t *cw = reinterpret_cast<uint32_t *>(a.dst);
-
-  int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
+  const int64_t t = (int64_t)blockIdx.x * kEncRowWaves + wave;
   if (t >= a.ntiles) return;
-  const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
-  TileSchedule sched;
-  sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
-  u32x4 v[kRegChunks];
-  auto issue = [&](int64_t tt) {
-    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
-    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + tt * a.tr * a.d, rows * a.d);
+  const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - t * a.tr);
+  {  // ---- phase 1: land the nibble rows (chunk = lane + 64 i of the contiguous tile)
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + t * a.tr * a.d, rows * a.d);
+    u32x4 v[kRegChunks];
 #pragma unroll
     for (int i = 0; i < kRegChunks; ++i) {
       if (i * kWave >= (int)chunks) break;  // uniform
       v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (lane + kWave * i), 0, 2));
     }
-  };
-  issue(t);
-  for (;;) {
-    // ---- phase 1: land the nibble rows (chunk = lane + 64 i of the contiguous tile)
 #pragma unroll
     for (int i = 0; i < kRegChunks; ++i) {
       if (i * kWave >= (int)chunks) break;  // uniform
       if (it.r2[i] < a.tr) *reinterpret_cast<u32x4 *>(sin + it.r2[i] * a.lr + 16 * it.j2[i]) = v[i];
     }
-    wave_lds_sync();
-    const int64_t cur = t;
-    t = (int64_t)sched.next((uint32_t)t, lane);
-    const bool more = t < a.ntiles;
-    if (more) issue(t);
-    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - cur * a.tr);
-    // ---- phase 2: 4 codewords per lane into the LDS codeword tile
-#pragma unroll
-    for (int i = 0; i < kRegGroups; ++i) {
-      if (i * kWave >= (int)groups) break;  // uniform
-      const uint32_t r = it.r1[i], q = it.q1[i];
-      if (r < rows) {
-        const uint32_t *s = reinterpret_cast<const uint32_t *>(sin + r * a.lr + 12 * q);
-        uint32_t dd[4];
-        golay_unpack4(s[0], s[1], s[2], dd);
-        uint32_t *o = sout + r * a.g + 4 * q;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (4 * q + k < a.g) o[k] = dd[k] | (uint32_t)par[dd[k]] << 12;
-      }
-    }
-    wave_lds_sync();
-    // ---- phase 3: the tile's codewords, contiguous, as 16-byte stores
-    const uint32_t nw = rows * a.g;  // words
-    uint32_t *out = cw + cur * a.tr * a.g;
-    for (uint32_t k = lane; k < nw / 4; k += kWave)
-      st_stream(reinterpret_cast<u32x4 *>(out) + k, reinterpret_cast<const u32x4 *>(sout)[k]);
-    for (uint32_t k = nw / 4 * 4 + lane; k < nw; k += kWave) st_stream(out + k, sout[k]);  // last tile's tail
-    if (!more) break;
-    wave_lds_sync();
   }
+  wave_lds_sync();
+  // ---- phase 2: 4 codewords per lane into the LDS codeword tile
+#pragma unroll
+  for (int i = 0; i < kRegGroups; ++i) {
+    if (i * kWave >= (int)groups) break;  // uniform
+    const uint32_t r = it.r1[i], q = it.q1[i];
+    if (r < rows) {
+      const uint32_t *s = reinterpret_cast<const uint32_t *>(sin + r * a.lr + 12 * q);
+      uint32_t dd[4];
+      golay_unpack4(s[0], s[1], s[2], dd);
+      uint32_t *o = sout + r * a.g + 4 * q;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * q + k < a.g) o[k] = dd[k] | (uint32_t)(tlo[dd[k] & 63u] ^ thi[dd[k] >> 6]) << 12;
+    }
+  }
+  wave_lds_sync();
+  // ---- phase 3: the tile's codewords, contiguous, as 16-byte stores
+  const uint32_t nw = rows * a.g;  // words
+  uint32_t *out = cw + t * a.tr * a.g;
+  for (uint32_t k = lane; k < nw / 4; k += kWave)
+    st_stream(reinterpret_cast<u32x4 *>(out) + k, reinterpret_cast<const u32x4 *>(sout)[k]);
+  for (uint32_t k = nw / 4 * 4 + lane; k < nw; k += kWave) st_stream(out + k, sout[k]);  // last tile's tail
 }
 
 // tile geometry of the register-tile row kernels (0 rows: not applicable)
@@ -770,11 +768,10 @@ KVECC_API int kvecc_golay_encode_rows(const uint8_t *nibbles, int32_t *codewords
   const RegGeom rg = reg_geom(d, g, true);
   if (rg.tr > 0 && aligned(nibbles, 16) && aligned(codewords, 16) &&
       cdiv(rows, rg.tr) < (1LL << 31)) {
-    RegRowsArgs a{nibbles, codewords, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
-                  par, nullptr};
-    if (!(a.dyn = shim_dyn_slot(stream))) return KVECC_EHIP;
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(a.ntiles, kRegWaves), (int64_t)cu_count() * kRowsPerCu);
-    KVECC_LAUNCH(golay_encode_rows_reg_kernel, dim3(grid), dim3(kRegBlock), 0, as_stream(stream), a);
+    const RegRowsArgs a{nibbles, codewords, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr,
+                        rg.tr, par, nullptr};
+    KVECC_LAUNCH(golay_encode_rows_full_kernel, dim3((unsigned)cdiv(a.ntiles, kEncRowWaves)),
+                 dim3(kEncRowWaves * kWave), 0, as_stream(stream), a);
     return check_launch("golay_encode_rows");
   }
   if (row_tiled(d, g, false)) {

@@ -40,7 +40,7 @@ SECTIONS = {
                          ("fused_golay_decode", "hamming84", "interp", "kernel_ms")),
     "golay_rows.decode": ("golay_decode_rows_reg_kernel<true>", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "decode")),
-    "golay_rows.encode": ("golay_encode_rows_reg_kernel", ("golay_rows", "bytes_per_launch"),
+    "golay_rows.encode": ("golay_encode_rows_full_kernel", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "encode")),
     "interp": ("interp_tile_kernel<false>", ("interp", "bytes_per_launch"), ("interp", "kernel_ms")),
     "interp.api": ("interp_tile_kernel<true>", ("interp", "api", "bytes_per_launch"), ("interp", "api", "kernel_ms")),
