@@ -11,6 +11,7 @@
 #include "kvecc_oracle.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* ------------------------------------------------------------------------ */
@@ -282,6 +283,27 @@ void oracle_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *count, int64_t n
     flips += c;
     affected += c > 0;
   }
+  if (stats) {
+    stats[0] = flips;
+    stats[1] = affected;
+  }
+}
+
+/* the shim's per-row injection (kv_cache/ecc_shim.py:594-603, 644-652): each of
+ * `rows` contiguous rows of row_len codewords is injected as its own tensor,
+ * row r with seed seed0 + r (the write loop's config.seed + _injection_count,
+ * counted once per (batch, position, head) row) */
+void oracle_inject_rows_u8(const uint8_t *in, uint8_t *out, int64_t rows, int64_t row_len,
+                           int n_bits, int64_t seed0, float ber, int64_t *stats) {
+  uint8_t *cnt = (uint8_t *)malloc(row_len > 0 ? (size_t)row_len : 1u);
+  int64_t flips = 0, affected = 0, st[2];
+  for (int64_t r = 0; r < rows; ++r) {
+    oracle_inject_u8(in + r * row_len, out + r * row_len, cnt, row_len, n_bits, seed0 + r, ber,
+                     row_len, 0, st);
+    flips += st[0];
+    affected += st[1];
+  }
+  free(cnt);
   if (stats) {
     stats[0] = flips;
     stats[1] = affected;

@@ -58,6 +58,8 @@ float oracle_uint_to_uniform(uint32_t x);
 void oracle_inject_u8(const uint8_t *in, uint8_t *out, uint8_t *count, int64_t n,
                       int n_bits, int64_t seed, float ber, int64_t global_n,
                       int64_t offset0, int64_t *stats);
+void oracle_inject_rows_u8(const uint8_t *in, uint8_t *out, int64_t rows, int64_t row_len,
+                           int n_bits, int64_t seed0, float ber, int64_t *stats);
 void oracle_inject_i32(const int32_t *in, int32_t *out, uint8_t *count, int64_t n,
                        int n_bits, int64_t seed, float ber, int64_t global_n,
                        int64_t offset0, int64_t *stats);

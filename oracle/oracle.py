@@ -55,6 +55,7 @@ def lib():
             "oracle_philox4x32_10": [ctypes.c_uint32] * 6 + [_u32p],
             "oracle_inject_u8": [_u8p, _u8p, _u8p, _i64, _int, _i64, _f32, _i64, _i64, _i64p],
             "oracle_inject_i32": [_i32p, _i32p, _u8p, _i64, _int, _i64, _f32, _i64, _i64, _i64p],
+            "oracle_inject_rows_u8": [_u8p, _u8p, _i64, _i64, _int, _i64, _f32, _i64p],
             "oracle_inject_u8_vectorized": [_u8p, _u8p, _u8p, _i64, _int, _i64, _f32, _i64p],
             "oracle_inject_i32_vectorized": [_i32p, _i32p, _u8p, _i64, _int, _i64, _f32, _i64p],
             "oracle_interpolate": [_u8p, _u8p, _u8p, _i64, _i64, _i64],
@@ -175,6 +176,19 @@ def inject(data, ber, n_bits, seed=0, global_n=None, offset0=0):
     else:
         raise ValueError(f"Unsupported dtype: {flat.dtype}. Use uint8 or int32.")
     return out.reshape(data.shape), cnt, (int(st[0]), int(st[1]))
+
+
+def inject_rows(data, ber, n_bits, seed0):
+    """The shim's per-row injection (kv_cache/ecc_shim.py:594-603, 644-652): uint8
+    rows [R, row_len], row r its own tensor with seed seed0 + r.
+    -> (corrupted, (flips, affected))"""
+    data = _c(data, np.uint8)
+    rows, row_len = data.shape
+    out = np.empty_like(data)
+    st = np.zeros(2, np.int64)
+    lib().oracle_inject_rows_u8(_p(data, _u8p), _p(out, _u8p), rows, row_len, int(n_bits), int(seed0),
+                                float(ber), _p(st, _i64p))
+    return out, (int(st[0]), int(st[1]))
 
 
 def inject_vectorized(data, ber, n_bits, seed=0):

@@ -18,7 +18,8 @@ cast to fp16 (ecc_shim.py:1150-1151), which is what our fused read outputs.
     injection stream and error classes), logits close;
   * config 4 at its size (GPT-2 12 layers, seq 1024, fp16): every layer's K/V
     that the HIP backend reads equals, bit for bit, what the host backend reads
-    after writing the same inputs, with equal statistics.
+    after writing the same inputs, with equal statistics; and layers 0, 5 and 11
+    equal the reference's write/read loops restated with the C oracle.
 """
 
 import contextlib
@@ -218,3 +219,49 @@ def test_config4_full_size_fp16_kv_hip_equals_cpu_backend(gpu):
     assert not mism, f"K/V differ in layers {mism}"
     assert be._errors_corrected == st_h["errors_corrected"] and be._errors_detected == st_h["errors_detected"]
     assert be._injection_count == st_h["injection_count"]
+    # independent anchor at full size: the reference's write and read loops
+    # restated with the C oracle (not codec_math.h) for the first, a middle and
+    # the last layer -- quantize rows (absmax * RN(1/7)), Hamming(8,4) encode,
+    # per-row injection with seed 42 + _injection_count (+1 for V), decode,
+    # interpolation along the context, (q - 8) * scale in fp32, fp16
+    from oracle import oracle
+    rows = 1024 * 12
+    for (layer, k, v), (kh, vh) in zip(rec["write"], rec["kv"]):
+        if layer not in (0, 5, 11):
+            continue
+        for which, x, got in ((0, k, kh), (1, v, vh)):
+            q, sc = oracle.quantize_rows(x.float().cpu().numpy().reshape(1024, 12, 64), rule=1)
+            cw, _ = oracle.inject_rows(oracle.hamming84_encode(q).reshape(rows, 64), 1e-2, 8,
+                                       42 + layer * rows + which)
+            data, et, _ = oracle.hamming84_decode(cw)
+            qi = oracle.interpolate_kernel(data, et, 1, 1024, 12 * 64).reshape(1024, 12, 64)
+            deq = ((qi.astype(np.float32) - np.float32(8.0)) * sc[..., None]).astype(np.float16)
+            assert np.array_equal(deq.transpose(1, 0, 2), got.cpu().numpy()), (layer, which)
+
+
+def test_config4_full_size_host_backend_matches_oracle():
+    """The host backend's config-4 write/read (Hamming(8,4) + interpolation, BER
+    1e-2, 12 heads x 64, 1024 positions, fp16, absmax * RN(1/7) scales) against
+    the reference's loops restated with the C oracle, for two layers of random
+    K/V (the GPU test above anchors the HIP backend the same way)."""
+    from oracle import oracle
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    torch.manual_seed(0)
+    cfg = ECCShimConfig(backend="cpu", codec="hamming84", ber=1e-2, inject_errors=True, seed=42, block_size=16,
+                        use_interpolation=True, scale_rule="mul_inv7")
+    mgr = SimpleBlockManager(64, 16, 2, 12, 64, device="cpu", codec="hamming84")
+    be = ECCBackend(mgr, cfg, num_heads=12)
+    rows = 1024 * 12
+    for layer in range(2):
+        k, v = torch.randn(1, 1024, 768).half(), torch.randn(1, 1024, 768).half()
+        be.write(k, v, layer)
+        kc, vc = be.codec_backend.shim_read(mgr, layer, 1024, mgr.shim_codec, True, torch.float16, be._stats)
+        for which, x, got in ((0, k, kc), (1, v, vc)):
+            q, sc = oracle.quantize_rows(x.float().numpy().reshape(1024, 12, 64), rule=1)
+            cw, _ = oracle.inject_rows(oracle.hamming84_encode(q).reshape(rows, 64), 1e-2, 8,
+                                       42 + layer * rows + which)
+            data, et, _ = oracle.hamming84_decode(cw)
+            assert (et == 2).sum() > 1000  # the interpolation is exercised
+            qi = oracle.interpolate_kernel(data, et, 1, 1024, 12 * 64).reshape(1024, 12, 64)
+            deq = ((qi.astype(np.float32) - np.float32(8.0)) * sc[..., None]).astype(np.float16)
+            assert np.array_equal(deq.transpose(1, 0, 2), got.numpy()), (layer, which)
