@@ -26,7 +26,7 @@ B, CTX, D, BS = 8, 4096, 128, 16
 VARIANTS = [("mfma_g1_cu4", 1, 4, 1), ("mfma_g1_cu2", 1, 2, 1), ("mfma_g1_cu8", 1, 8, 1),
             ("mfma_g1_cu4_nofuse", 1, 4, 0)]
 GQA_VARIANTS = [("mfma_g4_cu4", 4, 4, 0), ("mfma_g4_cu4_fused", 4, 4, 1), ("mfma_g4_cu2_fused", 4, 2, 1),
-                ("mfma_g4_cu8_fused", 4, 8, 1)]
+                ("mfma_g4_cu8_fused", 4, 8, 1), ("mfma_g4_cu1", 4, 1, 0), ("mfma_g4_cu1_fused", 4, 1, 1)]
 
 
 def main():

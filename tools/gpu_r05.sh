@@ -47,6 +47,9 @@ for s in $STEPS; do
     gtf)    run gtf 600 python tools/exp/run_golay_tf_exp.py ;;
     qtest)  run pytest_quant 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -k "quant or fused or dequant" \
               --timeout 300 --timeout-method thread ;;
+    attnexp) run attn_exp 600 python tools/exp/run_attn_exp.py hamming84 golay_packed ;;
+    shimtest) run pytest_shim_fp16 600 python -u -m pytest tests/test_shim_fp16.py -m gpu -x -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
     configs) run configs 600 python tools/bench_configs.py ;;
     shim)   run shim_eager 300 python tools/bench_shim.py
             run shim_graph 300 python tools/bench_shim.py --graph ;;
