@@ -85,18 +85,19 @@ __global__ __launch_bounds__(kTileThreads) void interp_tile_kernel(const u32x4 *
 #pragma unroll
   for (int k = 0; k < kRows; ++k)
     if (k < nrow && col) qr[k + 1] = ld_stream(q + base + (l0 + k) * chunks);
-  if (!pass) {
-#pragma unroll
-    for (int k = 0; k < kRows; ++k)
-      if (k < nrow && col) er[k] = ld_stream(err + base + (l0 + k) * chunks);
-  }
   // the tile's outer neighbours: the row above the first wave, the row below
-  // the wave holding the tile's (or the sequence's) last row
+  // the wave holding the tile's (or the sequence's) last row -- issued before
+  // the err rows, so the edge waves' halo is not queued behind them
   const bool top = w == 0 && l0 > 0;
   const bool last = nrow > 0 && (w == kTileWavesI - 1 || l0 + kRows >= len);
   const bool bottom = last && l0 + nrow < len;
   if (!pass && col && top) qr[0] = ld_stream(q + base + (l0 - 1) * chunks);
   if (!pass && col && bottom) qr[kRows + 1] = ld_stream(q + base + (l0 + nrow) * chunks);
+  if (!pass) {
+#pragma unroll
+    for (int k = 0; k < kRows; ++k)
+      if (k < nrow && col) er[k] = ld_stream(err + base + (l0 + k) * chunks);
+  }
   if (!pass) {
     if (nrow > 0) {
       edge[0][w][lane] = qr[1];

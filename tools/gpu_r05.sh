@@ -50,6 +50,9 @@ for s in $STEPS; do
     attnexp) run attn_exp 600 python tools/exp/run_attn_exp.py hamming84 golay_packed ;;
     shimtest) run pytest_shim_fp16 600 python -u -m pytest tests/test_shim_fp16.py -m gpu -x -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
+    itest)  run pytest_interp 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -k "interp" \
+              --timeout 300 --timeout-method thread ;;
+    expi)   run exp_interp 600 python tools/exp/run_r05.py interp ;;
     configs) run configs 600 python tools/bench_configs.py ;;
     shim)   run shim_eager 300 python tools/bench_shim.py
             run shim_graph 300 python tools/bench_shim.py --graph ;;

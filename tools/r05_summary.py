@@ -43,7 +43,9 @@ SECTIONS = {
     "golay_rows.encode": ("golay_encode_rows_full_kernel", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "encode")),
     "interp": ("interp_tile_kernel<false>", ("interp", "bytes_per_launch"), ("interp", "kernel_ms")),
-    "interp.api": ("interp_tile_kernel<true>", ("interp", "api", "bytes_per_launch"), ("interp", "api", "kernel_ms")),
+    # the API call: the recording pass + the fix-up launch, summed (the bench times the whole call)
+    "interp.api": (("interp_tile_kernel<true>", "interp_fixup_kernel"), ("interp", "api", "bytes_per_launch"),
+                   ("interp", "api", "kernel_ms")),
     "quantize_encode": ("quantize_encode_tile_kernel<__half", ("fused_quant", "quantize_encode", "bytes_per_launch"),
                         ("fused_quant", "quantize_encode", "kernel_ms")),
     "decode_dequant": ("decode_dequant_tile_kernel<__half>", ("fused_quant", "decode_dequant", "bytes_per_launch"),
@@ -98,10 +100,19 @@ def main():
                    "instance in the traced bench.py run (warm-up launches included); the bench line's figures "
                    "are means of dispatch-stamped launches, so rocprof_mean_vs_bench is the like-for-like check", "sections": {}}
     for sec, (frag, bytes_path, ms_path) in SECTIONS.items():
-        name = pick(durs, frag)
-        if name is None:
-            continue
-        d = durs[name]
+        if isinstance(frag, tuple):  # a call of several kernels: per-launch durations summed
+            names = [pick(durs, f) for f in frag]
+            if None in names:
+                continue
+            n = min(len(durs[x]) for x in names)
+            d = [sum(durs[x][i] for x in names) for i in range(n)]
+            name = " + ".join(x.split("(")[0] for x in names)
+            frag = frag[0]
+        else:
+            name = pick(durs, frag)
+            if name is None:
+                continue
+            d = durs[name]
         bench_ms = get(line, ms_path)
         nbytes = get(line, bytes_path) if bytes_path else None
         if sec == "encode":
