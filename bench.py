@@ -330,8 +330,12 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
             "bytes_per_launch": rows * bytes_per_row,
             "bytes_per_token_row": bytes_per_row, "hbm_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
             "write_share": 2 * D / bytes_per_row,
-            "ceiling_note": "write-heavy mix: non-temporal write-only streams peak at 4.8-5.3 TB/s and "
-                            "read-only at 6.1-6.9 TB/s on MI355X (profiles/r02/hbm_ceiling.log)",
+            "ceiling_note": "this byte mix (59 % writes) through a random block table runs at best 147 us "
+                            "(0.77) in a no-decode probe (profiles/r03/fused/store_perm.log); the persistent "
+                            "grid the 32 KiB tables need: 159 us with no table lookups (0.71, "
+                            "profiles/r04/fused/read_exp_ab_a.log); a full grid with the tables made "
+                            "algebraic: 155 us with no error path, 160-182 us with one "
+                            "(profiles/r05/golay_tf_ab2.log)",
             "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} warm-up calls and >= 0.25 s"}
 
 
