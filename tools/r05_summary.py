@@ -43,7 +43,8 @@ SECTIONS = {
     "golay_rows.encode": ("golay_encode_rows_full_kernel", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "encode")),
     "interp": ("interp_tile_kernel<false>", ("interp", "bytes_per_launch"), ("interp", "kernel_ms")),
-    # the API call: the recording pass + the fix-up launch, summed (the bench times the whole call)
+    # the API call: the recording pass, then the fix-up launch -- from the first's start to the
+    # second's end per call, as the bench's events around the calls see it
     "interp.api": (("interp_tile_kernel<true>", "interp_fixup_kernel"), ("interp", "api", "bytes_per_launch"),
                    ("interp", "api", "kernel_ms")),
     "quantize_encode": ("quantize_encode_tile_kernel<__half", ("fused_quant", "quantize_encode", "bytes_per_launch"),
@@ -65,12 +66,28 @@ def get(d, path):
     return d
 
 
-def trace_durations(src):
-    durs = {}
+def trace_spans(src):
+    spans = {}
     for p in glob.glob(os.path.join(src, "prof", "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
-            durs.setdefault(r["Kernel_Name"], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    return durs
+            spans.setdefault(r["Kernel_Name"], []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    for v in spans.values():
+        v.sort()
+    return spans
+
+
+def call_spans(spans, first, then):
+    """Per launch of `first`: from its start to the end of the next `then` launch
+    (a call of two kernels on one stream, timed as the bench times it)."""
+    import bisect
+    nxt = spans[then]
+    starts = [a for a, _ in nxt]
+    out = []
+    for a, b in spans[first]:
+        i = bisect.bisect_left(starts, b)
+        if i < len(nxt):
+            out.append(nxt[i][1] - a)
+    return out
 
 
 def counters(src, sub):
@@ -93,20 +110,20 @@ def main():
     for ln in open(os.path.join(src, "bench.log")):
         if ln.startswith("{"):
             line = json.loads(ln)
-    durs = trace_durations(src)
+    spans = trace_spans(src)
+    durs = {k: [b - a for a, b in v] for k, v in spans.items()}
     fetch, write = counters(src, "pmc_fetch"), counters(src, "pmc_write")
     out = {"source": src, "bench_line": os.path.join(dst, "bench.log"),
            "note": "rocprofv3 --kernel-trace without name truncation; median and mean over every launch of the "
                    "instance in the traced bench.py run (warm-up launches included); the bench line's figures "
                    "are means of dispatch-stamped launches, so rocprof_mean_vs_bench is the like-for-like check", "sections": {}}
     for sec, (frag, bytes_path, ms_path) in SECTIONS.items():
-        if isinstance(frag, tuple):  # a call of several kernels: per-launch durations summed
+        if isinstance(frag, tuple):  # a call of two kernels: first start -> second end, per call
             names = [pick(durs, f) for f in frag]
             if None in names:
                 continue
-            n = min(len(durs[x]) for x in names)
-            d = [sum(durs[x][i] for x in names) for i in range(n)]
-            name = " + ".join(x.split("(")[0] for x in names)
+            d = call_spans(spans, names[0], names[1])
+            name = " -> ".join(x.split("(")[0] for x in names)
             frag = frag[0]
         else:
             name = pick(durs, frag)
