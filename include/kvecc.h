@@ -92,10 +92,13 @@ KVECC_API int kvecc_init_device(int device);
  * its slot, safe because hipStreamDestroy drains the queue first), and
  * launches captured into a graph a slot of their own per (capture, stream), so
  * launches that can overlap never share counters.  Slots (48 KiB each) come
- * from a pool that grows outside captures only: every eager launch of such a
- * kernel tops the free list back up to 32 slots, so 32 captures can follow any
- * eager launch; kvecc_reserve_counter_slots(device, n) makes n more available
- * ahead of a longer run of captures.  A captured slot is tied to its graph by
+ * from a pool that grows from eager launches only (never inside the launching
+ * stream's own capture): every eager launch of such a kernel tops the free list
+ * back up to 32 slots, so 32 captures can follow any eager launch;
+ * kvecc_reserve_counter_slots(device, n) makes n more available ahead of a
+ * longer run of captures.  Growth allocates in relaxed capture mode, so an
+ * eager launch beside another stream's global-mode capture (torch.cuda.graph's
+ * default) neither fails nor invalidates that capture.  A captured slot is tied to its graph by
  * a HIP user object and returns to the pool when the graph and all its
  * executable instances are destroyed.  A graph keeps its slots for every
  * replay: replay one graph on one stream at a time (two overlapping replays of

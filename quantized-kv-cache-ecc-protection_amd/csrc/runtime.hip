@@ -231,11 +231,17 @@ static SlotPool g_pool[kMaxDev];
 constexpr int kSlotChunk = 64;    // slots per allocation (3 MiB)
 constexpr int kSlotReserve = 32;  // free slots kept for graph captures
 
-static int grow_pool(int d, SlotPool &p) {  // p.mu held; not during a capture
+static int grow_pool(int d, SlotPool &p) {  // p.mu held; the caller's stream is not capturing
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return set_error(KVECC_ENODEV, "hipGetDevice failed");
   if (hipSetDevice(d) != hipSuccess) return set_error(KVECC_ENODEV, "hipSetDevice(%d) failed", d);
   hipError_t e = hipSuccess;
+  // another stream may be capturing in global mode (torch.cuda.graph's
+  // default), which prohibits hipMalloc and stream syncs from every thread in
+  // global / thread-local mode and would invalidate that capture: this
+  // thread allocates in relaxed mode, then restores its mode
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  const bool exchanged = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
   {
     uint32_t *mem = nullptr;
     const size_t bytes = sizeof(uint32_t) * (size_t)kSlotChunk * kSlotWords;
@@ -248,6 +254,7 @@ static int grow_pool(int d, SlotPool &p) {  // p.mu held; not during a capture
       for (int i = kSlotChunk - 1; i >= 0; --i) p.free.push_back(mem + (size_t)i * kSlotWords);
     }
   }
+  if (exchanged) (void)hipThreadExchangeStreamCaptureMode(&mode);
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return set_error(KVECC_EHIP, "counter slots: %s", hipGetErrorString(e));
   return KVECC_OK;
@@ -309,8 +316,15 @@ uint32_t *counter_slot(void *stream) {
   drain_returned(p);
   const bool capturing = cs == hipStreamCaptureStatusActive;
   if (!capturing) {
-    // keep the reserve for captures topped up (allocation is illegal during one)
-    if (p.free.size() <= (size_t)kSlotReserve && grow_pool(d, p) != KVECC_OK) return nullptr;
+    // keep the reserve for captures topped up (allocation is illegal during one).
+    // The reserve is a target: when growth fails -- e.g. another stream is
+    // capturing in global mode, which forbids hipMalloc from every thread -- an
+    // eager launch still takes a free slot, and the failed call's error is
+    // consumed so the launch does not report it
+    if (p.free.size() <= (size_t)kSlotReserve && grow_pool(d, p) != KVECC_OK) {
+      (void)hipGetLastError();
+      if (p.free.empty()) return nullptr;
+    }
     auto it = p.eager.find(key);
     if (it != p.eager.end()) return it->second;
     uint32_t *s = p.free.back();

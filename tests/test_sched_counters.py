@@ -199,3 +199,66 @@ def test_many_captures_on_one_stream_and_slot_release(gpu):
         time.sleep(0.1)
     assert nz == 0
     assert used2 <= used0 + 1, f"captured slots not returned: {used0} before, {used1} alive, {used2} after"
+
+
+def _hip_streams(n):
+    """n new HIP streams of the runtime torch loaded (torch.cuda.Stream() hands
+    out 32 pooled streams per priority round-robin: the 33rd is the 1st again,
+    possibly the capture stream itself)."""
+    import ctypes
+    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+    hip = ctypes.CDLL(path)
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    raw = []
+    for _ in range(n):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        raw.append(h.value)
+    return [torch.cuda.ExternalStream(h) for h in raw], lambda: [hip.hipStreamDestroy(h) for h in raw]
+
+
+def test_eager_launches_beside_a_global_capture_grow_the_pool(gpu):
+    """torch.cuda.graph captures in global mode by default, which forbids hipMalloc
+    and stream syncs from every thread.  While stream A captures, eager launches
+    on 70 new streams each take a slot of their own, so the pool grows past its
+    reserve in the middle of the capture (the library allocates in relaxed
+    mode); neither the eager results nor the capture may break."""
+    from kvecc import ops
+    dev = gpu
+    run, mk, _ = _workloads(dev)["golay_rows"]
+    base, st = mk(), ops.new_stats(dev)
+    run(base, st)
+    torch.cuda.synchronize()
+    base_st = ops.read_stats(st)
+    used0, _ = ops.counter_slots_check(dev)
+    side, destroy = _hip_streams(70)
+    outs = [mk() for _ in side]
+    for o in outs:
+        o[0].fill_(0xEE)
+    sts = [ops.new_stats(dev) for _ in side]
+    a = torch.cuda.Stream(dev)
+    gout, gst = mk(), ops.new_stats(dev)
+    with torch.cuda.stream(a):
+        run(gout, ops.new_stats(dev))  # eager warm-up on the capture stream
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=a):
+        run(gout, gst)
+        for s, o, t in zip(side, outs, sts):
+            with torch.cuda.stream(s):
+                run(o, t)
+    torch.cuda.synchronize()
+    bad = [i for i, (o, t) in enumerate(zip(outs, sts)) if not (_same(o, base) and ops.read_stats(t) == base_st)]
+    assert not bad, bad
+    used1, nz = ops.counter_slots_check(dev)
+    assert nz == 0 and used1 >= used0 + 70, (used0, used1)
+    gst.zero_()
+    for t in gout:
+        t.zero_()
+    with torch.cuda.stream(a):
+        g.replay()
+    torch.cuda.synchronize()
+    assert _same(gout, base) and ops.read_stats(gst) == base_st
+    del g
+    destroy()
