@@ -318,6 +318,78 @@ __global__ __launch_bounds__(W * 64) void rows_enc_full_kernel(RegRowsArgs a, co
   for (uint32_t k = nw / 4 * 4 + lane; k < nw; k += kWave) st_stream(out + k, sout[k]);
 }
 
+// the product's full-grid rows encode with T2 consecutive tiles per wave: the
+// loads of all T2 tiles issued first (T2x the bytes in flight per wave), then
+// each tile landed, encoded and stored in turn through the same LDS tiles
+template <int W, int T2>
+__global__ __launch_bounds__(W * 64) void rows_enc_multi_kernel(RegRowsArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t tlo[64], thi[64];
+  __shared__ __attribute__((aligned(16))) uint8_t in_all[W][kRegEncIn];
+  __shared__ __attribute__((aligned(16))) uint8_t out_all[W][kRegEncOut];
+  if (threadIdx.x < 64) {
+    const uint16_t *par = reinterpret_cast<const uint16_t *>(a.tab);
+    tlo[threadIdx.x] = par[threadIdx.x];
+    thi[threadIdx.x] = par[threadIdx.x << 6];
+  }
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  uint8_t *sin = in_all[wave];
+  uint32_t *sout = reinterpret_cast<uint32_t *>(out_all[wave]);
+  for (uint32_t r = 0; r < a.tr; ++r)
+    for (uint32_t b = a.d + lane; b < a.lr; b += kWave) sin[r * a.lr + b] = 0;
+  __syncthreads();
+  const uint32_t d16 = a.d / 16, groups = a.tr * a.gpr, chunks = a.tr * d16;
+  const RegItems it(lane, a.gpr, d16);
+  const uint8_t *nib = reinterpret_cast<const uint8_t *>(a.src);
+  uint32_t *cw = reinterpret_cast<uint32_t *>(a.dst);
+  const int64_t t0 = ((int64_t)blockIdx.x * W + wave) * T2;
+  if (t0 >= a.ntiles) return;
+  u32x4 v[T2][kRegChunks];
+#pragma unroll
+  for (int u = 0; u < T2; ++u) {
+    const int64_t t = t0 + u;
+    const uint32_t rows = t < a.ntiles ? (uint32_t)min<int64_t>(a.tr, a.rows - t * a.tr) : 0u;
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + (t < a.ntiles ? t : 0) * a.tr * a.d, rows * a.d);
+#pragma unroll
+    for (int i = 0; i < kRegChunks; ++i) {
+      if (i * kWave >= (int)chunks) break;
+      v[u][i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (lane + kWave * i), 0, 2));
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < T2; ++u) {
+    const int64_t t = t0 + u;
+    if (t >= a.ntiles) break;  // uniform
+    const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - t * a.tr);
+    if (u) wave_lds_sync();  // the previous tile's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < kRegChunks; ++i) {
+      if (i * kWave >= (int)chunks) break;
+      if (it.r2[i] < a.tr) *reinterpret_cast<u32x4 *>(sin + it.r2[i] * a.lr + 16 * it.j2[i]) = v[u][i];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < kRegGroups; ++i) {
+      if (i * kWave >= (int)groups) break;
+      const uint32_t r = it.r1[i], q = it.q1[i];
+      if (r < rows) {
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(sin + r * a.lr + 12 * q);
+        uint32_t dd[4];
+        golay_unpack4(s[0], s[1], s[2], dd);
+        uint32_t *o = sout + r * a.g + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (4 * q + k < a.g) o[k] = dd[k] | (uint32_t)(tlo[dd[k] & 63u] ^ thi[dd[k] >> 6]) << 12;
+      }
+    }
+    wave_lds_sync();
+    const uint32_t nw = rows * a.g;
+    uint32_t *out = cw + t * a.tr * a.g;
+    for (uint32_t k = lane; k < nw / 4; k += kWave)
+      st_stream(reinterpret_cast<u32x4 *>(out) + k, reinterpret_cast<const u32x4 *>(sout)[k]);
+    for (uint32_t k = nw / 4 * 4 + lane; k < nw; k += kWave) st_stream(out + k, sout[k]);
+  }
+}
+
 }  // namespace kvecc
 
 using namespace kvecc;
@@ -335,6 +407,11 @@ extern "C" KVECC_API int r05_rows_enc(int v, const uint8_t *nibbles, int32_t *co
     case 0: hipLaunchKernelGGL(rows_enc_full_kernel<4>, dim3((unsigned)cdiv(a.ntiles, 4)), dim3(256), 0, s, a, par); break;
     case 1: hipLaunchKernelGGL(rows_enc_full_kernel<8>, dim3((unsigned)cdiv(a.ntiles, 8)), dim3(512), 0, s, a, par); break;
     case 2: hipLaunchKernelGGL(rows_enc_full_kernel<2>, dim3((unsigned)cdiv(a.ntiles, 2)), dim3(128), 0, s, a, par); break;
+    case 3: hipLaunchKernelGGL((rows_enc_multi_kernel<4, 2>), dim3((unsigned)cdiv(a.ntiles, 8)), dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((rows_enc_multi_kernel<4, 3>), dim3((unsigned)cdiv(a.ntiles, 12)), dim3(256), 0, s, a); break;
+    case 5: hipLaunchKernelGGL((rows_enc_multi_kernel<8, 2>), dim3((unsigned)cdiv(a.ntiles, 16)), dim3(512), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((rows_enc_multi_kernel<2, 2>), dim3((unsigned)cdiv(a.ntiles, 4)), dim3(128), 0, s, a); break;
+    case 7: hipLaunchKernelGGL((rows_enc_multi_kernel<4, 1>), dim3((unsigned)cdiv(a.ntiles, 4)), dim3(256), 0, s, a); break;
     default: return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -53,6 +53,7 @@ for s in $STEPS; do
     itest)  run pytest_interp 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -k "interp" \
               --timeout 300 --timeout-method thread ;;
     expi)   run exp_interp 600 python tools/exp/run_r05.py interp ;;
+    expr)   run exp_rows 600 python tools/exp/run_r05.py rows ;;
     sched)  run pytest_sched 600 python -u -m pytest tests/test_sched_counters.py -m gpu -x -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
     configs) run configs 600 python tools/bench_configs.py ;;
