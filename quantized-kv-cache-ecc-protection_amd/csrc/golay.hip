@@ -599,59 +599,62 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
 // workgroups of kEncRowWaves waves retiring (no schedule, no counter slot).
 // The parity comes from two 64-entry tables, parity(d) = T[d & 63] ^ T[64 + (d >> 6)]
 // (256 B of LDS per workgroup, conflict-free), not the 8 KiB table a
-// persistent grid could afford to stage: [8,4096,32,128] 56.9 -> 55.8 us
-// (profiles/r05/exp_r05e.log rows_enc v0; 8-wave workgroups 60.1, 2-wave 56.7).
-// Phase 1 lands the tile's nibble rows in LDS (16-byte loads of the contiguous
-// tile), phase 2 packs 4 codewords per lane into an LDS codeword tile, phase 3
-// stores it contiguously in 16-byte non-temporal stores.
-constexpr int kEncRowWaves = 4;
+// persistent grid could afford to stage.  Each lane loads its 4-codeword
+// groups' 12 nibble bytes straight from HBM (buffer_load_dwordx3 at
+// r * d + 12 q, 4-byte aligned; a row's last group reads into the next row,
+// whose bytes are masked to the per-head zero padding), encodes them into a
+// wave-private LDS codeword tile, and the tile leaves contiguous as 16-byte
+// non-temporal stores (stored straight from registers the 16-byte stores are
+// misaligned: half rate).  [8,4096,32,128]: 56.9 us for round 4's
+// persistent kernel, 55.3 with the full grid and the nibbles landed in LDS
+// first, 52.2 loading them straight (profiles/r05/rows_enc_ab.log; 4-wave
+// workgroups 52.7, 2-wave 55.4).
+constexpr int kEncRowWaves = 8;
 __global__ __launch_bounds__(kEncRowWaves * kWave) void golay_encode_rows_full_kernel(RegRowsArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t tlo[64], thi[64];
-  __shared__ __attribute__((aligned(16))) uint8_t in_all[kEncRowWaves][kRegEncIn];
   __shared__ __attribute__((aligned(16))) uint8_t out_all[kEncRowWaves][kRegEncOut];
   if (threadIdx.x < 64) {
     const uint16_t *par = reinterpret_cast<const uint16_t *>(a.tab);
     tlo[threadIdx.x] = par[threadIdx.x];
     thi[threadIdx.x] = par[threadIdx.x << 6];
   }
-  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
-  uint8_t *sin = in_all[wave];
-  uint32_t *sout = reinterpret_cast<uint32_t *>(out_all[wave]);
-  // the per-head zero padding: row bytes [d, lr) stay 0 (phase 1 writes [0, d))
-  for (uint32_t r = 0; r < a.tr; ++r)
-    for (uint32_t b = a.d + lane; b < a.lr; b += kWave) sin[r * a.lr + b] = 0;
   __syncthreads();
-  const uint32_t d16 = a.d / 16, groups = a.tr * a.gpr, chunks = a.tr * d16;
-  const RegItems it(lane, a.gpr, d16);
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  uint32_t *sout = reinterpret_cast<uint32_t *>(out_all[wave]);
+  const uint32_t groups = a.tr * a.gpr;
+  const RegItems it(lane, a.gpr, a.d / 16);
   const uint8_t *nib = reinterpret_cast<const uint8_t *>(a.src);
   uint32_t *cw = reinterpret_cast<uint32_t *>(a.dst);
   const int64_t t = (int64_t)blockIdx.x * kEncRowWaves + wave;
   if (t >= a.ntiles) return;
   const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - t * a.tr);
-  {  // ---- phase 1: land the nibble rows (chunk = lane + 64 i of the contiguous tile)
-    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + t * a.tr * a.d, rows * a.d);
-    u32x4 v[kRegChunks];
+  // ---- the tile's groups, straight into registers (past the tile: 0)
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + t * a.tr * a.d, rows * a.d);
+  uint32_t w[kRegGroups][3];
 #pragma unroll
-    for (int i = 0; i < kRegChunks; ++i) {
-      if (i * kWave >= (int)chunks) break;  // uniform
-      v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16u * (lane + kWave * i), 0, 2));
-    }
-#pragma unroll
-    for (int i = 0; i < kRegChunks; ++i) {
-      if (i * kWave >= (int)chunks) break;  // uniform
-      if (it.r2[i] < a.tr) *reinterpret_cast<u32x4 *>(sin + it.r2[i] * a.lr + 16 * it.j2[i]) = v[i];
-    }
+  for (int i = 0; i < kRegGroups; ++i) {
+    if (i * kWave >= (int)groups) break;  // uniform
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, it.r1[i] * a.d + 12u * it.q1[i], 0, 2);
+    w[i][0] = v[0];
+    w[i][1] = v[1];
+    w[i][2] = v[2];
   }
-  wave_lds_sync();
-  // ---- phase 2: 4 codewords per lane into the LDS codeword tile
+  // ---- 4 codewords per lane into the LDS codeword tile
 #pragma unroll
   for (int i = 0; i < kRegGroups; ++i) {
     if (i * kWave >= (int)groups) break;  // uniform
     const uint32_t r = it.r1[i], q = it.q1[i];
     if (r < rows) {
-      const uint32_t *s = reinterpret_cast<const uint32_t *>(sin + r * a.lr + 12 * q);
+      // bytes at or past the row's end are the per-head padding: zero
+      const int valid = (int)a.d - 12 * (int)q;  // bytes of the group inside the row
+      uint32_t b[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int lo = valid - 4 * k;
+        b[k] = lo >= 4 ? w[i][k] : lo <= 0 ? 0u : w[i][k] & ((1u << (8 * lo)) - 1u);
+      }
       uint32_t dd[4];
-      golay_unpack4(s[0], s[1], s[2], dd);
+      golay_unpack4(b[0], b[1], b[2], dd);
       uint32_t *o = sout + r * a.g + 4 * q;
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -659,7 +662,7 @@ __global__ __launch_bounds__(kEncRowWaves * kWave) void golay_encode_rows_full_k
     }
   }
   wave_lds_sync();
-  // ---- phase 3: the tile's codewords, contiguous, as 16-byte stores
+  // ---- the tile's codewords, contiguous, as 16-byte stores
   const uint32_t nw = rows * a.g;  // words
   uint32_t *out = cw + t * a.tr * a.g;
   for (uint32_t k = lane; k < nw / 4; k += kWave)

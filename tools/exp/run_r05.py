@@ -165,7 +165,7 @@ if which in ("rows", "all"):
     ops.golay_encode_rows_into(x, ref)
     out = torch.empty_like(ref)
     cases = {"prod": lambda: ops.golay_encode_rows_into(x, out)}
-    for v in range(8):
+    for v in (0, 8, 9):
         cases[f"v{v}"] = (lambda v=v: lib.r05_rows_enc(v, P(x), P(out), rows, D, S))
     for k, fn in cases.items():
         out.zero_()
