@@ -16,6 +16,7 @@
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/quant.hip"
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/interp.hip"
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/golay.hip"
+#include "../../quantized-kv-cache-ecc-protection_amd/csrc/packed.hip"
 
 namespace kvecc {
 
@@ -390,6 +391,113 @@ __global__ __launch_bounds__(W * 64) void rows_enc_multi_kernel(RegRowsArgs a) {
   }
 }
 
+// rows encode with no input landing: each lane loads its 4-codeword groups'
+// 12 nibble bytes straight from HBM (buffer_load_dwordx3 at r*d + 12q, 4-byte
+// aligned; a row's last group reads into the next row, whose bytes are masked
+// to the per-head zero padding), encodes, and the codeword tile goes out
+// through LDS as in the product
+template <int W>
+__global__ __launch_bounds__(W * 64) void rows_enc_direct_kernel(RegRowsArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t tlo[64], thi[64];
+  __shared__ __attribute__((aligned(16))) uint8_t out_all[W][kRegEncOut];
+  if (threadIdx.x < 64) {
+    const uint16_t *par = reinterpret_cast<const uint16_t *>(a.tab);
+    tlo[threadIdx.x] = par[threadIdx.x];
+    thi[threadIdx.x] = par[threadIdx.x << 6];
+  }
+  __syncthreads();
+  const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
+  uint32_t *sout = reinterpret_cast<uint32_t *>(out_all[wave]);
+  const uint32_t d16 = a.d / 16, groups = a.tr * a.gpr;
+  const RegItems it(lane, a.gpr, d16);
+  const uint8_t *nib = reinterpret_cast<const uint8_t *>(a.src);
+  uint32_t *cw = reinterpret_cast<uint32_t *>(a.dst);
+  const int64_t t = (int64_t)blockIdx.x * W + wave;
+  if (t >= a.ntiles) return;
+  const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - t * a.tr);
+  const __amdgpu_buffer_rsrc_t rs = tile_rsrc(nib + t * a.tr * a.d, rows * a.d);
+  uint32_t w[kRegGroups][3];
+#pragma unroll
+  for (int i = 0; i < kRegGroups; ++i) {
+    if (i * kWave >= (int)groups) break;
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, it.r1[i] * a.d + 12u * it.q1[i], 0, 2);
+    w[i][0] = v[0];
+    w[i][1] = v[1];
+    w[i][2] = v[2];
+  }
+#pragma unroll
+  for (int i = 0; i < kRegGroups; ++i) {
+    if (i * kWave >= (int)groups) break;
+    const uint32_t r = it.r1[i], q = it.q1[i];
+    if (r < rows) {
+      // bytes at or past the row's end are the per-head padding: zero
+      const uint32_t past = 12u * q + 12u > a.d ? 12u * q + 12u - a.d : 0u;  // 0..11
+      uint32_t b[3] = {w[i][0], w[i][1], w[i][2]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int lo = 12 - (int)past - 4 * k;  // valid bytes of dword k
+        b[k] = lo >= 4 ? b[k] : lo <= 0 ? 0u : b[k] & ((1u << (8 * lo)) - 1u);
+      }
+      uint32_t dd[4];
+      golay_unpack4(b[0], b[1], b[2], dd);
+      uint32_t *o = sout + r * a.g + 4 * q;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * q + k < a.g) o[k] = dd[k] | (uint32_t)(tlo[dd[k] & 63u] ^ thi[dd[k] >> 6]) << 12;
+    }
+  }
+  wave_lds_sync();
+  const uint32_t nw = rows * a.g;
+  uint32_t *out = cw + t * a.tr * a.g;
+  for (uint32_t k = lane; k < nw / 4; k += kWave)
+    st_stream(reinterpret_cast<u32x4 *>(out) + k, reinterpret_cast<const u32x4 *>(sout)[k]);
+  for (uint32_t k = nw / 4 * 4 + lane; k < nw; k += kWave) st_stream(out + k, sout[k]);
+}
+
+// packed Golay encode on a full grid: a wave owns G groups of 8 codewords per
+// lane (one contiguous span), parity from the split 64-entry tables (256 B per
+// workgroup instead of 8 KiB), wave-private regrouping with no workgroup barrier
+template <int W, int G>
+__global__ __launch_bounds__(W * 64) void pk_enc_full_kernel(const uint32_t *__restrict__ nib,
+                                                             uint32_t *__restrict__ cw, int64_t nwt,
+                                                             const uint16_t *__restrict__ par) {
+  __shared__ __attribute__((aligned(16))) uint16_t tlo[64], thi[64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[W][G][kWaveCwBytes];
+  if (threadIdx.x < 64) {
+    tlo[threadIdx.x] = par[threadIdx.x];
+    thi[threadIdx.x] = par[threadIdx.x << 6];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int64_t t = (int64_t)blockIdx.x * W + wave;
+  if (t >= nwt) return;
+  const int64_t G0 = t * (kWave * G);  // first group of this wave
+  u32x3v n[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) n[g] = ld_stream(reinterpret_cast<const u32x3v *>(nib + (G0 + g * kWave + lane) * 3));
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t nn[3] = {n[g].x, n[g].y, n[g].z};
+    uint32_t d[8], c[8], w[6];
+    nib_unpack8(nn, d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = d[k] | (uint32_t)(tlo[d[k] & 63u] ^ thi[d[k] >> 6]) << 12;
+    cw_pack8(c, w);
+    u32x2 *dst = reinterpret_cast<u32x2 *>(&stage[wave][g][24 * lane]);
+    dst[0] = u32x2{w[0], w[1]};
+    dst[1] = u32x2{w[2], w[3]};
+    dst[2] = u32x2{w[4], w[5]};
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    uint8_t *out = reinterpret_cast<uint8_t *>(cw) + (G0 + g * kWave) * 24;
+    st_stream(reinterpret_cast<u32x4 *>(out) + lane, *reinterpret_cast<const u32x4 *>(&stage[wave][g][16 * lane]));
+    st_stream(reinterpret_cast<u32x2 *>(out + 1024) + lane,
+              *reinterpret_cast<const u32x2 *>(&stage[wave][g][1024 + 8 * lane]));
+  }
+}
+
 }  // namespace kvecc
 
 using namespace kvecc;
@@ -412,7 +520,31 @@ extern "C" KVECC_API int r05_rows_enc(int v, const uint8_t *nibbles, int32_t *co
     case 5: hipLaunchKernelGGL((rows_enc_multi_kernel<8, 2>), dim3((unsigned)cdiv(a.ntiles, 16)), dim3(512), 0, s, a); break;
     case 6: hipLaunchKernelGGL((rows_enc_multi_kernel<2, 2>), dim3((unsigned)cdiv(a.ntiles, 4)), dim3(128), 0, s, a); break;
     case 7: hipLaunchKernelGGL((rows_enc_multi_kernel<4, 1>), dim3((unsigned)cdiv(a.ntiles, 4)), dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((rows_enc_direct_kernel<4>), dim3((unsigned)cdiv(a.ntiles, 4)), dim3(256), 0, s, a); break;
+    case 9: hipLaunchKernelGGL((rows_enc_direct_kernel<8>), dim3((unsigned)cdiv(a.ntiles, 8)), dim3(512), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((rows_enc_direct_kernel<2>), dim3((unsigned)cdiv(a.ntiles, 2)), dim3(128), 0, s, a); break;
     default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" KVECC_API int r05_pk_enc(int v, const void *nib, void *cw, int64_t m, void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const uint16_t *par = golay_parity_table_dev();
+  const uint32_t *n = (const uint32_t *)nib;
+  uint32_t *c = (uint32_t *)cw;
+  switch (v) {
+#define PKE(V, W, G)                                                                                          \
+  case V: {                                                                                                   \
+    const int64_t nwt = m / (64 * 8 * G);                                                                     \
+    if (nwt * 64 * 8 * G != m) return -3;                                                                     \
+    hipLaunchKernelGGL((pk_enc_full_kernel<W, G>), dim3((unsigned)cdiv(nwt, W)), dim3(64 * W), 0, s, n, c, nwt, par); \
+    break;                                                                                                    \
+  }
+    PKE(0, 8, 2) PKE(1, 4, 2) PKE(2, 8, 1) PKE(3, 8, 4) PKE(4, 4, 4)
+#undef PKE
+    default:
+      return -1;
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

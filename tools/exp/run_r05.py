@@ -23,6 +23,7 @@ lib.r05_interp_rec.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.
 lib.r05_dd.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
 lib.r05_quant.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP]
 lib.r05_rows_enc.argtypes = [ctypes.c_int, VP, VP, ctypes.c_int64, ctypes.c_int64, VP]
+lib.r05_pk_enc.argtypes = [ctypes.c_int, VP, VP, ctypes.c_int64, VP]
 lib.r05_dd32.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
 dev = torch.device("cuda:0")
 S = VP(torch.cuda.current_stream().cuda_stream)
@@ -173,3 +174,19 @@ if which in ("rows", "all"):
         torch.cuda.synchronize()
         print(f"rows_enc {k}: rc={rc} equal={torch.equal(out, ref)}", flush=True)
     ab(cases, rows * (D + 4 * G), "rows_enc")
+
+if which in ("pk", "all"):
+    m = 45088768  # the headline's per-head codewords (bench.py packed section)
+    g = torch.Generator().manual_seed(11)
+    nib = torch.randint(0, 256, (m * 3 // 2,), generator=g, dtype=torch.uint8).to(dev)
+    ref = ops.golay_encode_packed(nib, m)
+    out = torch.empty_like(ref)
+    cases = {"prod": lambda: ops.golay_encode_packed_into(nib, out, m)}
+    for v in range(5):
+        cases[f"v{v}"] = (lambda v=v: lib.r05_pk_enc(v, P(nib), P(out), m, S))
+    for k, fn in cases.items():
+        out.zero_()
+        rc = fn()
+        torch.cuda.synchronize()
+        print(f"pk_enc {k}: rc={rc} equal={torch.equal(out, ref)}", flush=True)
+    ab(cases, int(4.5 * m), "pk_enc")

@@ -54,6 +54,7 @@ for s in $STEPS; do
               --timeout 300 --timeout-method thread ;;
     expi)   run exp_interp 600 python tools/exp/run_r05.py interp ;;
     expr)   run exp_rows 600 python tools/exp/run_r05.py rows ;;
+    exppk)  run exp_pk 600 python tools/exp/run_r05.py pk ;;
     rtest)  run pytest_rows 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -k "rows or geometry or shim or golay" \
               --timeout 300 --timeout-method thread ;;
     sched)  run pytest_sched 600 python -u -m pytest tests/test_sched_counters.py -m gpu -x -v -p no:cacheprovider \
