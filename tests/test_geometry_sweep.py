@@ -20,6 +20,7 @@ A failing case prints its parameters; keep it as a regression case below.
 """
 
 import math
+import os
 import random
 
 import pytest
@@ -27,13 +28,17 @@ import torch
 
 from tests.test_attention import _cache, _pack_golay, _torch_reference
 
-N_ATTN = 40
-N_ROWS = 24
-N_PACKED = 24
+# KVECC_SWEEP_SCALE=k multiplies every sweep's case count and KVECC_SWEEP_SEED=s
+# shifts its seeds (an extended run; the defaults are the suite's)
+SCALE = int(os.environ.get("KVECC_SWEEP_SCALE", "1"))
+SEED = int(os.environ.get("KVECC_SWEEP_SEED", "0"))
+N_ATTN = 40 * SCALE
+N_ROWS = 24 * SCALE
+N_PACKED = 24 * SCALE
 
 
 def _attn_cases():
-    rng = random.Random(20251018)
+    rng = random.Random(20251018 + SEED)
     cases = []
     for i in range(N_ATTN):
         codec = rng.choice(["hamming84", "golay", "golay_packed"])
@@ -128,7 +133,7 @@ def test_attention_sweep_hip(gpu, case):
 # ---- per-head Golay rows ----------------------------------------------------------
 
 def _rows_cases():
-    rng = random.Random(77)
+    rng = random.Random(77 + SEED)
     return [(i, rng.choice([1, 2, 3, 5, 20, 64, 100, 128, 129, 256]), rng.choice([1, 7, 63, 64, 65, 1000, 4097]),
              rng.choice([0, 1, 3, 17]), rng.choice([0.0, 1e-2, 5e-2])) for i in range(N_ROWS)]
 
@@ -165,7 +170,7 @@ def test_golay_rows_sweep_hip_vs_host(gpu, case):
 # ---- packed decodes ------------------------------------------------------------------
 
 def _packed_cases():
-    rng = random.Random(99)
+    rng = random.Random(99 + SEED)
     return [(i, rng.choice(["golay", "hamming84"]), rng.choice([1, 2, 3, 5, 31, 32, 33, 1000, 4095, 65537]),
              rng.choice([0, 1, 2, 3, 5, 16]), rng.choice([0.0, 1e-2, 5e-2])) for i in range(N_PACKED)]
 
@@ -227,9 +232,9 @@ def test_packed_decode_sweep_hip_vs_host(gpu, case):
 # ---- interpolation (workgroup tiles of 64 column chunks x 32 positions) -------------
 
 def _interp_cases():
-    rng = random.Random(4242)
+    rng = random.Random(4242 + SEED)
     cases = []
-    for i in range(24):
+    for i in range(24 * SCALE):
         inner = rng.choice([16, 48, 160, 1008, 1024, 1040, 4096, 24, 7])
         length = rng.choice([1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 65, 100, 257])
         outer = rng.choice([1, 2, 3, 5])

@@ -295,8 +295,13 @@ def _random_geometries(n, seed=2024):
     return out
 
 
+# KVECC_SWEEP_SCALE / KVECC_SWEEP_SEED: an extended run (tests/test_geometry_sweep.py)
+_SCALE = int(__import__("os").environ.get("KVECC_SWEEP_SCALE", "1"))
+_SEED = int(__import__("os").environ.get("KVECC_SWEEP_SEED", "0"))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch,ctx,hkv,d,bs,layers,interp", _random_geometries(16))
+@pytest.mark.parametrize("batch,ctx,hkv,d,bs,layers,interp", _random_geometries(16 * _SCALE, 2024 + _SEED))
 def test_hip_byte_read_random_geometry(gpu, batch, ctx, hkv, d, bs, layers, interp):
     from kvecc import cpu_ops, ops
     kc, vc, ks, vs, table = make_cache("hamming84", batch, ctx, hkv, d, bs, layers=layers, seed=ctx + d,
@@ -326,7 +331,7 @@ def _random_golay_geometries(n, seed=4048):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("codec,batch,ctx,hkv,d,bs,layers", _random_golay_geometries(12))
+@pytest.mark.parametrize("codec,batch,ctx,hkv,d,bs,layers", _random_golay_geometries(12 * _SCALE, 4048 + _SEED))
 def test_hip_golay_read_random_geometry(gpu, codec, batch, ctx, hkv, d, bs, layers):
     """The Golay wave-tile read (d % 8 == 0) on random geometries against the host twin."""
     from kvecc import cpu_ops, ops
