@@ -63,6 +63,11 @@ def _torch_reference(query, kc, vc, table, lens, ks, vs, layer, bs, codec):
         slot = pos % bs
         ok = blk >= 0
         pos, blk, slot = pos[ok], blk[ok], slot[ok]
+        if n and not bool(ok.any()):
+            # no valid token: the reference's constant (DESIGN §1 quirk 14,
+            # attention_ecc.py:342,391-423 / :806-807,885-886)
+            out[b] = -8.0 if codec == "hamming84" else 0.0
+            continue
         for side, cache, sc in ((0, kc, ks), (1, vc, vs)):
             rows = cache.view(cache.shape[0], cache.shape[1], kv_heads, bs, -1)[blk, layer, :, slot]
             if codec == "hamming84":
