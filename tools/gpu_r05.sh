@@ -55,6 +55,9 @@ for s in $STEPS; do
     expi)   run exp_interp 600 python tools/exp/run_r05.py interp ;;
     expr)   run exp_rows 600 python tools/exp/run_r05.py rows ;;
     exppk)  run exp_pk 600 python tools/exp/run_r05.py pk ;;
+    sweep40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=2 run pytest_sweep40 1100 python -u -m pytest \
+              tests/test_geometry_sweep.py tests/test_shim_read_batch.py -m gpu -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
     sweep8) KVECC_SWEEP_SCALE=8 KVECC_SWEEP_SEED=1 run pytest_sweep8 1000 python -u -m pytest \
               tests/test_geometry_sweep.py tests/test_shim_read_batch.py -m gpu -x -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
