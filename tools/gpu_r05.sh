@@ -55,6 +55,10 @@ for s in $STEPS; do
     expi)   run exp_interp 600 python tools/exp/run_r05.py interp ;;
     expr)   run exp_rows 600 python tools/exp/run_r05.py rows ;;
     exppk)  run exp_pk 600 python tools/exp/run_r05.py pk ;;
+    fuzz)   run pytest_fuzz 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
+    fuzz8)  KVECC_SWEEP_SCALE=8 KVECC_SWEEP_SEED=3 run pytest_fuzz8 1100 python -u -m pytest tests/test_gpu_fuzz.py \
+              -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=2 run pytest_sweep40 1100 python -u -m pytest \
               tests/test_geometry_sweep.py tests/test_shim_read_batch.py -m gpu -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
