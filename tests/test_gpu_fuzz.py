@@ -205,3 +205,42 @@ def test_fuzz_packed(gpu, case):
             assert torch.equal(a.cpu(), b), case
         else:
             assert a == b, case
+
+
+SHIM = _cases("shim", lambda r, i: (i, r.choice(["hamming84", "hamming74", "golay", "int4"]), r.choice([True, False]),
+                                    r.choice([16, 20, 32, 48, 64, 100, 128, 256]), r.choice([1, 4, 8, 16, 32]),
+                                    r.randint(1, 3), r.randint(1, 70), r.choice([1, 2, 4]), r.choice([1, 2]),
+                                    r.choice(["float32", "float16", "bfloat16"]), r.choice([0.0, 1e-2, 5e-2]),
+                                    r.choice(["div7", "mul_inv7"])))
+
+
+@pytest.mark.parametrize("case", SHIM, ids=[f"s{c[0]}" for c in SHIM])
+def test_fuzz_shim_write_read(gpu, case):
+    """ECCBackend write + read (ecc_shim.py:557-721, 990-1071) on random cache
+    geometries: the HIP backend's cache bits, scales, decoded K/V (attention
+    dtype) and statistics equal the host backend's."""
+    from kvecc.ecc_shim import ECCBackend, ECCShimConfig, SimpleBlockManager
+    i, codec, interp, d, bs, batch, s, hk, groups, dtype, ber, rule = case
+    interp = interp and codec == "hamming84"
+    if codec != "golay" and d % 4:
+        d += 4 - d % 4
+    dt = getattr(torch, dtype)
+    g = torch.Generator().manual_seed(7000 + i)
+    k = torch.randn(batch, s, hk * d, generator=g).to(dt)
+    v = torch.randn(batch, s, hk * d, generator=g).to(dt)
+    res = []
+    for dev, backend in ((gpu, "hip"), (torch.device("cpu"), "cpu")):
+        cfg = ECCShimConfig(codec=codec, ber=ber, inject_errors=ber > 0, seed=11 + i, block_size=bs,
+                            use_interpolation=interp, backend=backend, scale_rule=rule)
+        nblk = (s + bs - 1) // bs + 1
+        mgr = SimpleBlockManager(nblk, bs, 3, hk, d, device=dev, codec=codec)
+        be = ECCBackend(mgr, cfg, num_heads=hk * groups)
+        be._injection_count = i
+        be.write(k.to(dev), v.to(dev), layer_idx=1)
+        kt, vt = be.codec_backend.shim_read(mgr, 1, s, mgr.shim_codec, interp, dt, be._stats)
+        res.append((mgr.k_cache.cpu(), mgr.v_cache.cpu(), mgr.k_scales.cpu(), mgr.v_scales.cpu(),
+                    kt.cpu(), vt.cpu(), be._injection_count, be._errors_corrected, be._errors_detected))
+    h, c = res
+    for j in range(6):
+        assert torch.equal(h[j], c[j]), (case, j)
+    assert h[6:] == c[6:], (case, h[6:], c[6:])
