@@ -50,6 +50,23 @@ def test_bench_spawns_two_gloo_ranks(gpu):
 
 
 @pytest.mark.gpu
+def test_bench_rccl_world1(gpu):
+    """The RCCL path of the multi-GPU bench (init with device_id, barriers, the
+    per-rank all_gather and the statistics all_reduce) on a real "nccl" group of
+    one rank -- what every rank of the driver's 8-GPU run executes."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--dist",
+                        "--steps", "10", "--warmup", "2", "--no-cpu-baseline", "--no-inject", "--no-packed",
+                        "--no-fused", "--no-rows", "--roofline-samples", "2", "--no-sections"],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 1
+    assert line["config"]["process_group"] == {"backend": "nccl", "world_size": 1}
+    assert [p["rank"] for p in line["config"]["per_rank"]] == [0]
+    assert line["decode_stats"]["bits_corrected"] > 0
+
+
+@pytest.mark.gpu
 def test_bench_more_gpus_than_the_box_fails(gpu):
     import torch
     n = torch.cuda.device_count() + 1
