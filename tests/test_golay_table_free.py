@@ -1,6 +1,7 @@
 """The table-free Golay(24,12) correction of tools/exp/golay_tf_exp.hip against
 the reference's 4096-entry syndrome table (golden fixture, generated from the
-reference's config.py:403-457 ordering), on every syndrome, and its decode against the C oracle on all 2^24 words.
+reference's config.py:403-457 ordering) on every syndrome, and its decode
+against the C oracle on all 2^24 received words.
 
 B is symmetric with B B = I, so u = s B undoes the data half: the four weight
 tests (wt(s) <= 3; wt(u) <= 3; wt(s ^ B_i) <= 2; wt(u ^ B_j) <= 2) find the
