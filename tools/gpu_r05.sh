@@ -59,6 +59,11 @@ for s in $STEPS; do
               --timeout 300 --timeout-method thread ;;
     fuzz8)  KVECC_SWEEP_SCALE=8 KVECC_SWEEP_SEED=3 run pytest_fuzz8 1100 python -u -m pytest tests/test_gpu_fuzz.py \
               -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    fuzz40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=4 run pytest_fuzz40 1100 python -u -m pytest tests/test_gpu_fuzz.py \
+              -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    sweep40b) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=5 run pytest_sweep40b 1100 python -u -m pytest \
+              tests/test_geometry_sweep.py tests/test_shim_read_batch.py -m gpu -v -p no:cacheprovider \
+              --timeout 300 --timeout-method thread ;;
     sweep40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=2 run pytest_sweep40 1100 python -u -m pytest \
               tests/test_geometry_sweep.py tests/test_shim_read_batch.py -m gpu -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
