@@ -59,6 +59,8 @@ for s in $STEPS; do
               --timeout 300 --timeout-method thread ;;
     fuzz8)  KVECC_SWEEP_SCALE=8 KVECC_SWEEP_SEED=3 run pytest_fuzz8 1100 python -u -m pytest tests/test_gpu_fuzz.py \
               -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    gread)  run gread_ab 900 python tools/exp/run_golay_read_exp.py pers:2 pers_u16:2 pers_u16:3 pers_u16:4 pers:3 \
+              pers_b256_p50:3 pers_b256_p50:4 full1_u16:0:0 full2_u16:0:0 ;;
     fuzz40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=4 run pytest_fuzz40 1100 python -u -m pytest tests/test_gpu_fuzz.py \
               -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep40b) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=5 run pytest_sweep40b 1100 python -u -m pytest \
