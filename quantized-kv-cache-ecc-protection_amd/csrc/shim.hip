@@ -282,11 +282,19 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 //     slower), so the dynamic part is the tail: 65 % ran Golay 161.0 / packed
 //     147.0 / H(8,4)+interp 156.2 us against 161.6 / 148.0 / 159.8 at 75 and
 //     166-168 / 153-155 / 164-166 at 85-90 (profiles/r03/fused/static_pct_ab1.log).
-constexpr int kTileBlock = 512;                    // 8 waves per workgroup
+//   * round 5: the Golay read's workgroups went from 8 waves, 2 per CU and a
+//     65 % static share to 4 waves, 3 per CU (12 waves per CU, each workgroup
+//     staging the 32 KiB of tables for 4 waves) and a 30 % static share: int32
+//     161.7 -> 158.8 us, packed 147.6 -> 143.5 (interleaved A/B,
+//     profiles/r05/golay_read_ab3.log; 50 / 40 / 20 / 10 % 160.7 / 159.4 /
+//     159.2 / 158.9, 4 waves at 2 per CU 169.8).
+constexpr int kTileBlock = 512;                    // 8 waves per workgroup (byte-codec reads)
 constexpr int kTileWaves = kTileBlock / kWave;
-constexpr int kShimTilePerCu = 2;                  // Golay read: persistent grid
+constexpr int kGolayTileBlock = 256;               // Golay read: 4 waves per workgroup
+constexpr int kGolayTileWaves = kGolayTileBlock / kWave;
+constexpr int kShimTilePerCu = 3;                  // Golay read: persistent grid
 constexpr int kShimBytesLdsPad = 16384;            // byte-codec reads: caps 4 workgroups per CU
-constexpr uint32_t kShimReadStaticPct = 65;        // static share of the dynamic-tail schedule
+constexpr uint32_t kShimReadStaticPct = 30;        // Golay read: static share of the dynamic-tail schedule
 constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
 constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
 constexpr int kTileChunks = 5;                     // 8-value output chunks per lane per tile (max)
@@ -416,24 +424,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_out(const ShimTileArgs &a
 }
 
 template <typename TO, bool STATS, bool PACKED>
-__global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
+__global__ __launch_bounds__(kGolayTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kGolayTileWaves][kTileStage];
   // row scales of the staged tile: written in phase 1, read in phase 2 (a
   // scale kept in a register across the next tile's prefetch made the compiler
   // wait for that prefetch before phase 2)
-  __shared__ float scale_all[kTileWaves][kWave];
+  __shared__ float scale_all[kGolayTileWaves][kWave];
   {
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab);
     u32x4 *dst = reinterpret_cast<u32x4 *>(tab);
 #pragma unroll
-    for (int i = threadIdx.x; i < 2048; i += kTileBlock) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 2048; i += kGolayTileBlock) dst[i] = src[i];
   }
   __syncthreads();
   // wave-uniform from here on (readfirstlane: the compiler cannot prove it)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
-  const uint32_t nwaves = gridDim.x * kTileWaves;
+  const uint32_t nwaves = gridDim.x * kGolayTileWaves;
   const uint32_t groups = a.tr * a.gpr;  // <= 64 * kTileGroups (host check)
   constexpr int V = kVpl<TO>, NC = kTileChunks * 8 / V;  // output chunks per lane (max)
   const uint32_t dv = a.d / V;
@@ -466,7 +474,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_golay_tiles_kernel(ShimT
   }
   uint32_t bits = 0, unc = 0;
   // waves retire independently: no workgroup barrier below
-  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  const uint32_t gw = blockIdx.x * kGolayTileWaves + wave;
   uint32_t u = gw;
   if (u >= a.units) return;
   TileSchedule sched;
@@ -913,7 +921,7 @@ static void launch_read(int codec, int interp, const ShimReadArgs &a, hipStream_
 
 // the Golay read's persistent grid: kShimTilePerCu workgroups per CU
 static unsigned tile_grid(uint32_t units) {
-  return (unsigned)std::min<int64_t>(cdiv(units, kTileWaves), (int64_t)cu_count() * kShimTilePerCu);
+  return (unsigned)std::min<int64_t>(cdiv(units, kGolayTileWaves), (int64_t)cu_count() * kShimTilePerCu);
 }
 
 template <typename TO>
@@ -921,13 +929,13 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
   const unsigned grid = tile_grid(a.units);
   constexpr unsigned pad = 0;
   if (a.stats && packed)
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kTileBlock), pad, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, true>), dim3(grid), dim3(kGolayTileBlock), pad, st, a);
   else if (a.stats)
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, false>), dim3(grid), dim3(kTileBlock), pad, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, true, false>), dim3(grid), dim3(kGolayTileBlock), pad, st, a);
   else if (packed)
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, true>), dim3(grid), dim3(kTileBlock), pad, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, true>), dim3(grid), dim3(kGolayTileBlock), pad, st, a);
   else
-    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kTileBlock), pad, st, a);
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kGolayTileBlock), pad, st, a);
 }
 
 // byte codecs: a full grid, one tile per wave; 16 KiB of dynamic LDS caps 4

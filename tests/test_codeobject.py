@@ -94,8 +94,8 @@ def test_hot_kernel_budgets(kernels, pattern, limit):
 # Each kernel's static LDS and workgroup size are fixed by those constants, so a
 # build with other values (an experiment's) fails here.
 SHIPPED = [
-    # fused Golay read: 512 threads, 32 KiB tables + 8 x (2304 B tile + 256 B scales)
-    (r"shim_read_golay_tiles_kernelI6__half", 512, 32768 + 8 * (2304 + 256)),
+    # fused Golay read: 256 threads, 32 KiB tables + 4 x (2304 B tile + 256 B scales)
+    (r"shim_read_golay_tiles_kernelI6__half", 256, 32768 + 4 * (2304 + 256)),
     # fused byte-codec read: 512 threads, 8 x (2304 + 256) B (+16 KiB dynamic at launch)
     (r"shim_read_bytes_tiles_kernelI6__half", 512, 8 * (2304 + 256)),
     # interpolating H(8,4) read: the same plus one "decoded" word per wave

@@ -409,6 +409,14 @@ static const Variant kVariants[] = {
     GVP("pk_pers_b256", 256, true, 65),
     GVP("pk_pers_b384", 384, true, 65),
     GVP("pk_pers_b768", 768, true, 65),
+    GVP("pk_pers_b256_p50", 256, true, 50),
+    GVP("pk_pers_b256_p40", 256, true, 40),
+    GVP("pers_b256_p40", 256, false, 40),
+    GVP("pers_b256_p30", 256, false, 30),
+    GVP("pers_b256_p20", 256, false, 20),
+    GVP("pers_b256_p10", 256, false, 10),
+    GVP("pk_pers_b256_p30", 256, true, 30),
+    GVP("pk_pers_b256_p20", 256, true, 20),
     // global correction table, split parity in LDS (0.5 KiB staged per workgroup)
     GV("full1_gc", 1, 1, 0, 3, 1, 0, 512, false),
     GV("full2_gc", 1, 2, 0, 3, 1, 0, 512, false),

@@ -61,6 +61,13 @@ for s in $STEPS; do
               -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gread)  run gread_ab 900 python tools/exp/run_golay_read_exp.py pers:2 pers_u16:2 pers_u16:3 pers_u16:4 pers:3 \
               pers_b256_p50:3 pers_b256_p50:4 full1_u16:0:0 full2_u16:0:0 ;;
+    gread2) ROUNDS=60 run gread_ab2 900 python tools/exp/run_golay_read_exp.py pers:2 pers_b256:3 pers_b256_p50:3 \
+              pers_b256_p40:3 pers_b256_p75:3 pers_b512_p50:2 pk_pers:2 pk_pers_b256:3 pk_pers_b256_p50:3 pk_pers_b256_p40:3 ;;
+    gread3) ROUNDS=60 run gread_ab3 900 python tools/exp/run_golay_read_exp.py pers:2 pers_b256_p50:3 pers_b256_p40:3 \
+              pers_b256_p30:3 pers_b256_p20:3 pers_b256_p10:3 pers_b256_p40:2 pk_pers:2 pk_pers_b256_p40:3 \
+              pk_pers_b256_p30:3 pk_pers_b256_p20:3 ;;
+    gread4) ROUNDS=60 run gread_ab4 900 python tools/exp/run_golay_read_exp.py pers:2 pers_b256_p30:3 pk_pers:2 \
+              pk_pers_b256_p30:3 ;;
     fuzz40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=4 run pytest_fuzz40 1100 python -u -m pytest tests/test_gpu_fuzz.py \
               -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep40b) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=5 run pytest_sweep40b 1100 python -u -m pytest \
