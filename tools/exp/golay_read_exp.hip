@@ -417,6 +417,12 @@ static const Variant kVariants[] = {
     GVP("pers_b256_p10", 256, false, 10),
     GVP("pk_pers_b256_p30", 256, true, 30),
     GVP("pk_pers_b256_p20", 256, true, 20),
+    GVP("pers_b128_p30", 128, false, 30),
+    GVP("pers_b384_p30", 384, false, 30),
+    {"pers_u16_b256_p30", golay_read_exp_kernel<0, 1, 0, 4, 0, 0, 256, false, 30>, 0, 1, 256},
+    {"pers_u16_b512_p30", golay_read_exp_kernel<0, 1, 0, 4, 0, 0, 512, false, 30>, 0, 1, 512},
+    {"pers_splitp_b256_p30", golay_read_exp_kernel<0, 1, 0, 0, 1, 0, 256, false, 30>, 0, 1, 256},
+    {"pk_pers_u16_b256_p30", golay_read_exp_kernel<0, 1, 0, 4, 0, 0, 256, true, 30>, 0, 1, 256},
     // global correction table, split parity in LDS (0.5 KiB staged per workgroup)
     GV("full1_gc", 1, 1, 0, 3, 1, 0, 512, false),
     GV("full2_gc", 1, 2, 0, 3, 1, 0, 512, false),

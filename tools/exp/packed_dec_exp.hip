@@ -135,6 +135,10 @@ static const Variant kVariants[] = {
     {"pk_b256_p50", pkdec_exp_kernel<0, false, 256, 50>, 256},
     {"pk_b384", pkdec_exp_kernel<0, false, 384, 75>, 384},
     {"pk_b384_p50", pkdec_exp_kernel<0, false, 384, 50>, 384},
+    {"pk_b256_p30", pkdec_exp_kernel<0, false, 256, 30>, 256},
+    {"pk_b256_p40", pkdec_exp_kernel<0, false, 256, 40>, 256},
+    {"pk_b256_p20", pkdec_exp_kernel<0, false, 256, 20>, 256},
+    {"pk_p30", pkdec_exp_kernel<0, false, 512, 30>, 512},
 };
 
 }  // namespace exp

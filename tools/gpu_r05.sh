@@ -68,6 +68,12 @@ for s in $STEPS; do
               pk_pers_b256_p30:3 pk_pers_b256_p20:3 ;;
     gread4) ROUNDS=60 run gread_ab4 900 python tools/exp/run_golay_read_exp.py pers:2 pers_b256_p30:3 pk_pers:2 \
               pk_pers_b256_p30:3 ;;
+    gread5) ROUNDS=60 run gread_ab5 900 python tools/exp/run_golay_read_exp.py pers_b256_p30:3 pers_b128_p30:4 \
+              pers_b128_p30:5 pers_b128_p30:6 pers_b384_p30:2 pers_u16_b256_p30:3 pers_u16_b256_p30:4 \
+              pers_u16_b256_p30:5 pers_u16_b512_p30:2 pers_u16_b512_p30:3 pers_splitp_b256_p30:3 pers_splitp_b256_p30:4 \
+              pk_pers_b256_p30:3 pk_pers_u16_b256_p30:3 pk_pers_u16_b256_p30:4 ;;
+    pkdec)  ROUNDS=60 run pkdec_ab 900 python tools/exp/run_packed_dec_exp.py pk:2 pk_p50:2 pk_p30:2 pk_b256:3 \
+              pk_b256_p50:3 pk_b256_p40:3 pk_b256_p30:3 pk_b256_p20:3 pk_b256_p30:4 pk_b256_p50:4 ;;
     fuzz40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=4 run pytest_fuzz40 1100 python -u -m pytest tests/test_gpu_fuzz.py \
               -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep40b) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=5 run pytest_sweep40b 1100 python -u -m pytest \
