@@ -35,7 +35,7 @@ namespace kvecc {
 constexpr int kGroups = 2;                          // 4-codeword groups per lane per tile
 constexpr int kDecBlock = 512, kEncBlock = 1024;    // threads per workgroup
 constexpr int kDecPerCu = 32, kEncPerCu = 16;       // workgroups per CU (grid-strided)
-constexpr int kRowsPerCu = 2;                       // register-tile row kernels (512 threads, ~50 KB LDS)
+constexpr int kRowsPerCu = 3;                       // rows decode: persistent workgroups per CU (256 threads, ~41 KB LDS)
 constexpr int kDecTile = kDecBlock * kGroups * 4;   // 4096 codewords
 constexpr int kEncTile = kEncBlock * kGroups * 4;   // 8192 codewords
 constexpr int kWaveCw = kWave * kGroups * 4;        // codewords per wave per tile
@@ -469,8 +469,12 @@ __global__ __launch_bounds__(kBlock) void golay_decode_rows_tiled_kernel(
 // current tile's stores.  Per-lane offsets are 32-bit inside a tile, tile
 // bases 64-bit and wave-uniform (descriptors in SGPRs).
 // dynamic tail schedule (kvecc_internal.h TileSchedule), as the fused reads
-constexpr int kRegBlock = 512;
+// the rows decode's persistent shape: 4-wave workgroups at 3 per CU with a 30 %
+// static share (as the fused Golay read, shim.hip): 52.6 -> 51.7 us against 8 waves,
+// 2 per CU and 75 % (profiles/r05/rows_dec_ab.log; 4 per CU 57.1)
+constexpr int kRegBlock = 256;
 constexpr int kRegWaves = kRegBlock / kWave;
+constexpr uint32_t kRowsDecStaticPct = 30;
 constexpr int kRegGroups = 4;        // 4-codeword groups per lane per tile (max)
 constexpr int kRegChunks = 3;        // 16-byte nibble chunks per lane per tile (max)
 constexpr int kRegDecStage = 2304;   // decode: LDS nibble rows per wave
@@ -511,11 +515,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void *base, ui
                                            (int)uni(bytes), 0x00020000);
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRowsArgs a) {
+// BLOCK / PCT: workgroup size and static share (the product's: kRegBlock, kRowsDecStaticPct;
+// tools/exp/r05_exp.hip instantiates others)
+template <bool STATS, int BLOCK = kRegBlock, uint32_t PCT = kRowsDecStaticPct>
+__global__ __launch_bounds__(BLOCK) void golay_decode_rows_reg_kernel(RegRowsArgs a) {
+  constexpr int kW = BLOCK / kWave;
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kRegWaves][kRegDecStage];
-  for (int i = threadIdx.x; i < 2048; i += kRegBlock)
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kW][kRegDecStage];
+  for (int i = threadIdx.x; i < 2048; i += BLOCK)
     reinterpret_cast<u32x4 *>(tab)[i] = reinterpret_cast<const u32x4 *>(a.tab)[i];
   __syncthreads();
   const uint32_t wave = uni((uint32_t)threadIdx.x / kWave), lane = threadIdx.x % kWave;
@@ -526,11 +533,11 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
   uint8_t *nib = reinterpret_cast<uint8_t *>(a.dst);
   uint32_t bits = 0, unc = 0;
 
-  int64_t t = (int64_t)blockIdx.x * kRegWaves + wave;
+  int64_t t = (int64_t)blockIdx.x * kW + wave;
   if (t >= a.ntiles) return;  // no workgroup barrier below
-  const int64_t tstride = (int64_t)gridDim.x * kRegWaves;
+  const int64_t tstride = (int64_t)gridDim.x * kW;
   TileSchedule sched;
-  sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane);
+  sched.init((uint32_t)a.ntiles, a.dyn, (uint32_t)t, (uint32_t)tstride, lane, PCT);
   u32x4 w[kRegGroups];
   auto issue = [&](int64_t tt) {
     const uint32_t rows = (uint32_t)min<int64_t>(a.tr, a.rows - tt * a.tr);
@@ -588,7 +595,7 @@ __global__ __launch_bounds__(kRegBlock) void golay_decode_rows_reg_kernel(RegRow
     bits = wave_sum(bits);
     unc = wave_sum(unc);
     if (lane == 0) {
-      uint64_t *slot = a.stats + ((blockIdx.x * kRegWaves + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      uint64_t *slot = a.stats + ((blockIdx.x * kW + wave) % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
       if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
       if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
     }

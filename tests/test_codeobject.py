@@ -81,7 +81,7 @@ def test_fused_read_tiles_fit_two_workgroups_per_cu(kernels):
 @pytest.mark.parametrize("pattern,limit", [
     (r"^_ZN5kvecc19golay_decode_kernel", 64),       # the headline decode
     (r"^_ZN5kvecc19golay_encode_kernel", 64),
-    (r"golay_decode_rows_reg_kernel", 128),         # per-head rows decode (512 threads, 2 per CU)
+    (r"golay_decode_rows_reg_kernel", 128),         # per-head rows decode (256 threads, 3 per CU)
     (r"golay_encode_rows_full_kernel", 64),         # per-head rows encode (full grid)
 ])
 def test_hot_kernel_budgets(kernels, pattern, limit):
@@ -103,7 +103,7 @@ SHIPPED = [
     # packed Golay decode wave tiles: 512 threads, 24 KiB tables + 8 x 3 KiB stage
     (r"golay_decode_packed_wave_kernel", 512, 24576 + 8 * 3072),
     # per-head rows register tiles: 512 threads
-    (r"golay_decode_rows_reg_kernel", 512, None),
+    (r"golay_decode_rows_reg_kernelILb1ELi256ELj30E", 256, None),
     # per-head rows encode on a full grid: 512 threads, split parity (256 B) + 8 x 2816 B codeword tiles
     (r"golay_encode_rows_full_kernel", 512, 256 + 8 * 2816),
     (r"^_ZN5kvecc19golay_decode_kernel", 512, None),

@@ -549,6 +549,31 @@ extern "C" KVECC_API int r05_pk_enc(int v, const void *nib, void *cw, int64_t m,
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// per-head rows decode at other workgroup sizes / static shares / workgroups per CU
+extern "C" KVECC_API int r05_rows_dec(int v, const int32_t *cw, uint8_t *nib, int64_t rows, int64_t d,
+                                      uint64_t *stats, int per_cu, void *stream) {
+  const int64_t g = (d + 2) / 3;
+  const RegGeom rg = reg_geom(d, g, false);
+  if (rg.tr == 0) return -3;
+  RegRowsArgs a{cw, nib, rows, cdiv(rows, rg.tr), (uint32_t)d, (uint32_t)g, rg.gpr, rg.lr, rg.tr,
+                golay_attn_table_dev(), stats};
+  a.dyn = shim_dyn_slot(stream);
+  hipStream_t s = (hipStream_t)stream;
+  switch (v) {
+#define RD(V, B, P)                                                                                             \
+  case V:                                                                                                       \
+    hipLaunchKernelGGL((golay_decode_rows_reg_kernel<true, B, P>),                                              \
+                       dim3((unsigned)std::min<int64_t>(cdiv(a.ntiles, B / 64), (int64_t)cu_count() * per_cu)), \
+                       dim3(B), 0, s, a);                                                                       \
+    break;
+    RD(0, 512, 75) RD(1, 512, 50) RD(2, 512, 30) RD(3, 256, 75) RD(4, 256, 50) RD(5, 256, 30) RD(6, 256, 20)
+#undef RD
+    default:
+      return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 extern "C" KVECC_API int r05_quant(int v, const void *x, void *cw, float *sc, int64_t rows, int64_t d, void *stream) {
   hipStream_t s = (hipStream_t)stream;
   // fp16, D = 128: 16 lanes per row, 4 rows per row group

@@ -24,6 +24,7 @@ lib.r05_dd.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64,
 lib.r05_quant.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP]
 lib.r05_rows_enc.argtypes = [ctypes.c_int, VP, VP, ctypes.c_int64, ctypes.c_int64, VP]
 lib.r05_pk_enc.argtypes = [ctypes.c_int, VP, VP, ctypes.c_int64, VP]
+lib.r05_rows_dec.argtypes = [ctypes.c_int, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, ctypes.c_int, VP]
 lib.r05_dd32.argtypes = [ctypes.c_int, VP, VP, VP, ctypes.c_int64, ctypes.c_int64, VP, VP]
 dev = torch.device("cuda:0")
 S = VP(torch.cuda.current_stream().cuda_stream)
@@ -190,3 +191,28 @@ if which in ("pk", "all"):
         torch.cuda.synchronize()
         print(f"pk_enc {k}: rc={rc} equal={torch.equal(out, ref)}", flush=True)
     ab(cases, int(4.5 * m), "pk_enc")
+
+if which in ("rowsdec", "all"):
+    rows = B * L * H
+    G = (D + 2) // 3
+    g = torch.Generator().manual_seed(13)
+    x = torch.randint(0, 16, (rows, D), generator=g, dtype=torch.uint8).to(dev)
+    cw = ops.golay_encode_rows(x).view(-1)
+    ops.inject_into(cw, cw, 1e-2, 24, seed=42)
+    cw = cw.view(rows, G)
+    ref = torch.empty(rows, D, dtype=torch.uint8, device=dev)
+    st0 = ops.new_stats(dev)
+    ops.golay_decode_rows_into(cw, ref, stats=st0)
+    out = torch.empty_like(ref)
+    st = ops.new_stats(dev)
+    cases = {"prod": lambda: ops.golay_decode_rows_into(cw, out, stats=st)}
+    for v, pc in ((0, 2), (1, 2), (2, 2), (3, 3), (4, 3), (5, 3), (6, 3), (5, 4), (3, 4)):
+        cases[f"v{v}:{pc}"] = (lambda v=v, pc=pc: lib.r05_rows_dec(v, P(cw), P(out), rows, D, P(st), pc, S))
+    for k, fn in cases.items():
+        out.zero_()
+        st.zero_()
+        rc = fn()
+        torch.cuda.synchronize()
+        print(f"rows_dec {k}: rc={rc} equal={torch.equal(out, ref)} stats={ops.read_stats(st) == ops.read_stats(st0)}",
+              flush=True)
+    ab(cases, rows * (4 * G + D), "rows_dec")

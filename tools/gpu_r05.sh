@@ -55,6 +55,7 @@ for s in $STEPS; do
     expi)   run exp_interp 600 python tools/exp/run_r05.py interp ;;
     expr)   run exp_rows 600 python tools/exp/run_r05.py rows ;;
     exppk)  run exp_pk 600 python tools/exp/run_r05.py pk ;;
+    exprd)  run exp_rowsdec 600 python tools/exp/run_r05.py rowsdec ;;
     fuzz)   run pytest_fuzz 900 python -u -m pytest tests/test_gpu_fuzz.py -m gpu -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
     fuzz8)  KVECC_SWEEP_SCALE=8 KVECC_SWEEP_SEED=3 run pytest_fuzz8 1100 python -u -m pytest tests/test_gpu_fuzz.py \
