@@ -38,7 +38,7 @@ SECTIONS = {
     "fused_h84.interp": ("shim_read_h84_interp_kernel<__half, true>",
                          ("fused_golay_decode", "hamming84", "interp", "bytes_per_launch"),
                          ("fused_golay_decode", "hamming84", "interp", "kernel_ms")),
-    "golay_rows.decode": ("golay_decode_rows_reg_kernel<true>", ("golay_rows", "bytes_per_launch"),
+    "golay_rows.decode": ("golay_decode_rows_reg_kernel<true", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "decode")),
     "golay_rows.encode": ("golay_encode_rows_full_kernel", ("golay_rows", "bytes_per_launch"),
                           ("golay_rows", "kernel_ms", "encode")),
