@@ -83,6 +83,9 @@ for s in $STEPS; do
     sweep40c) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=6 run pytest_sweep40c 1100 python -u -m pytest \
               tests/test_geometry_sweep.py tests/test_shim_read_batch.py tests/test_gpu_fuzz.py -m gpu -v \
               -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    sweep40d) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=7 run pytest_sweep40d 1100 python -u -m pytest \
+              tests/test_geometry_sweep.py tests/test_shim_read_batch.py tests/test_gpu_fuzz.py -m gpu -v \
+              -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sweep40) KVECC_SWEEP_SCALE=40 KVECC_SWEEP_SEED=2 run pytest_sweep40 1100 python -u -m pytest \
               tests/test_geometry_sweep.py tests/test_shim_read_batch.py -m gpu -v -p no:cacheprovider \
               --timeout 300 --timeout-method thread ;;
