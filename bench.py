@@ -49,9 +49,10 @@ DECODE_BYTES_PER_CW = 8  # 4 B codeword in, 3 B triplet + 1 B count out (SURVEY 
 ENCODE_BYTES_PER_CW = 7  # 3 B triplet in, 4 B codeword out
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -90,17 +91,35 @@ def parse():
                     help="skip the fused quantize+encode / decode+dequantize roofline section")
     ap.add_argument("--no-pipeline", action="store_true", help="skip the encode+inject+decode pipeline")
     ap.add_argument("--no-montecarlo", action="store_true", help="skip the config-5 sweep section")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the strong-scaling section (the headline's one tensor split over the ranks)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak (default): every rank owns a whole [8,4096,32,128] tensor; strong: the ONE "
+                         "[8,4096,32,128] tensor is split along B over the ranks (at most 8)")
     ap.add_argument("--no-sections", action="store_true",
                     help="headline only: skip every optional section and the CPU baselines")
+    ap.add_argument("--sections", default=None,
+                    help="comma-separated sections to run, every other one skipped: " + ",".join(SECTIONS))
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--inject-pmc-json", default=os.path.join(REPO, "profiles", "inject_valu.json"),
                     help="VALU instructions per Philox (rocprofv3 SQ_INSTS_VALU pass) for the inject roofline")
-    a = ap.parse_args()
-    if a.no_sections:
-        for k in ("no_cpu_baseline", "no_inject", "no_packed", "no_fused", "no_rows", "no_interp",
-                  "no_quant", "no_pipeline", "no_montecarlo"):
-            setattr(a, k, True)
+    a = ap.parse_args(argv)
+    if a.no_sections and a.sections is None:
+        a.sections = ""
+    if a.sections is not None:
+        keep = {s.strip() for s in a.sections.split(",") if s.strip()}
+        unknown = keep - set(SECTIONS)
+        if unknown:
+            ap.error(f"unknown section(s) {sorted(unknown)}; known: {','.join(SECTIONS)}")
+        for s, flag in SECTIONS.items():
+            setattr(a, flag, s not in keep)
     return a
+
+
+# section name -> the --no-* flag that skips it
+SECTIONS = {"cpu": "no_cpu_baseline", "inject": "no_inject", "packed": "no_packed", "fused": "no_fused",
+            "rows": "no_rows", "interp": "no_interp", "quant": "no_quant", "pipeline": "no_pipeline",
+            "montecarlo": "no_montecarlo", "strong": "no_strong"}
 
 
 def cpu_baseline(budget_s, threads):
@@ -257,22 +276,157 @@ def quant_bench(dev, steps, warmup):
     return res
 
 
-def montecarlo_bench(dev):
-    """BASELINE config 5 on this GPU: the 36-trial codec sweep (4 codecs x BER
+def table_digest(rows):
+    """sha256 of the sweep's [trials x 5] counter table as little-endian int64,
+    rows in trial order: equal for every world size when the sharding is exact."""
+    import hashlib
+    import struct
+    from kvecc.montecarlo import STAT_NAMES
+    flat = [int(r[k]) for r in rows for k in STAT_NAMES]
+    return hashlib.sha256(struct.pack(f"<{len(flat)}q", *flat)).hexdigest()
+
+
+def gather_floats(dist, world, dev, vals, gloo):
+    """Every rank's `vals` (a list of floats), rank order; [vals] without a group."""
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    if dist is None:
+        return [t.tolist()]
+    if gloo:
+        t = t.cpu()
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def montecarlo_bench(dev, dist=None, rank=0, world=1, gloo=False):
+    """BASELINE config 5: the 36-trial codec sweep (4 codecs x BER
     {1e-4,1e-3,1e-2} x seeds {42,101,997}) at [8,4096,32,128] through
-    kvecc.montecarlo.run_sweep, one fused launch per trial (kvecc_mc_trial),
-    one statistics fold at the end; a warm-up sweep first, the second timed."""
+    kvecc.montecarlo.run_sweep -- evaluation/sweep.py:352-626 driven as
+    evaluation/experiments/monte_carlo.py:75-128 do, batch-sharded: rank r runs
+    batch rows shard_bounds(8, r, N) of every trial (one fused launch per trial,
+    kvecc_mc_trial, global Philox offsets), one statistics fold, and the sweep's
+    ONE all_reduce(SUM) of the int64 [36 x 5] table (RCCL over xGMI).  Every
+    rank runs it; a warm-up sweep first, the second timed between barriers
+    (the all-reduce inside), the slowest rank's time reported."""
     from kvecc import montecarlo as mc
     cfg = mc.MonteCarloConfig()
-    shard = mc.HipShard(cfg, 0, 1, dev)
-    mc.run_sweep(cfg, shard)
-    rows, sec = mc.run_sweep(cfg, shard)
+    shard = mc.HipShard(cfg, rank, world, dev)
+    mc.run_sweep(cfg, shard, dist, rank)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rows, compute_s = mc.run_sweep(cfg, shard, dist, rank)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    per_rank = gather_floats(dist, world, dev, [wall, compute_s, shard.b0, shard.b1], gloo)
+    sec = max(p[0] for p in per_rank)
     return {"workload": "config 5: 36 trials, 4 codecs x BER {1e-4,1e-3,1e-2} x seeds {42,101,997}, "
-                        "[8,4096,32,128], one GPU", "trials": len(rows), "ms": sec * 1e3,
+                        f"[8,4096,32,128] batch-sharded over {world} rank(s)",
+            "world": world, "trials": len(rows), "ms": sec * 1e3,
             "ms_per_trial": sec * 1e3 / len(rows), "fused": shard.fused,
             "values_per_s": len(rows) * B * L * H * D / sec,
+            "table_sha256": table_digest(rows),
+            "per_rank": [{"rank": r, "batch_rows": [int(p[2]), int(p[3])], "ms": p[0] * 1e3,
+                          "trials_ms": p[1] * 1e3} for r, p in enumerate(per_rank)],
+            "collective": ("one all_reduce(SUM) of the int64 [36 x 5] table "
+                           f"({dist.get_backend()})" if dist is not None else None),
+            "scaling": "strong (the config's one [8,4096,32,128] tensor split along B)",
             "bound": "valu (Philox per bit; the trial reads the ground truth once)",
-            "timing": "wall clock of run_sweep (device-synchronised), second of two sweeps"}
+            "timing": "wall clock of the second run_sweep between barriers (device-synchronised, the "
+                      "all-reduce included), max over ranks; trials_ms = the rank's trials alone"}
+
+
+def strong_setup(dev, rank, world):
+    """The headline's workload split along B: the ONE [8,4096,32,128] tensor
+    (seed 0, identical for every world size), rank r encoding / decoding batch
+    rows shard_bounds(8, r, N) with the injection told the global codeword
+    count and the shard's global offset -- the fault pattern, and so the
+    all-reduced statistics, of any world size equal the single-GPU run's."""
+    from kvecc import montecarlo as mc
+    if world > B:
+        raise ValueError(f"strong scaling splits B={B} rows: at most {B} ranks, got {world}")
+    b0, b1 = mc.shard_bounds(B, rank, world)
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 16, (B, L, H, D), generator=gen, dtype=torch.uint8)[b0:b1].to(dev)
+    per_b = L * H * ((D + 2) // 3)
+    return x, b0 * per_b, B * per_b
+
+
+def strong_section(dev, dist, rank, world, steps, warmup, gloo):
+    """Strong scaling beside the weak headline: the same encode +
+    decode step over the one [8,4096,32,128] tensor split along B, wall clock
+    of `steps` steps between barriers, slowest rank; statistics all-reduced."""
+    from kvecc import ops
+    x, off, gn = strong_setup(dev, rank, world)
+    h = Headline(dev, x, off, gn)
+    del x
+    for _ in range(warmup):
+        h.step()
+    h.stats.zero_()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        h.step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    st = ops.stats_totals(h.stats)
+    inj = ops.stats_totals(h.inj_stats)
+    if dist is not None:
+        if gloo:
+            st, inj = st.cpu(), inj.cpu()
+        dist.all_reduce(st, op=dist.ReduceOp.SUM)
+        dist.all_reduce(inj, op=dist.ReduceOp.SUM)
+    per_rank = gather_floats(dist, world, dev, [wall, h.m], gloo)
+    sec = max(p[0] for p in per_rank)
+    total = gn * steps
+    return {"workload": f"golay24 per-head encode+decode of ONE [B=8,L=4096,H=32,D=128] tensor split along "
+                        f"B over {world} rank(s)",
+            "world": world, "codewords_total": gn, "value": total / sec, "unit": "codewords/s",
+            "ms_per_step": sec / steps * 1e3, "steps": steps,
+            "decode_stats": dict(zip(("bits_corrected", "uncorrectable"), st.tolist())),
+            "inject_stats": dict(zip(("flips", "affected"), inj.tolist())),
+            "per_rank": [{"rank": r, "codewords": int(p[1]), "elapsed_s": p[0]} for r, p in enumerate(per_rank)],
+            "timing": f"wall clock of {steps} steps between barriers after {warmup} warm-up steps, max over ranks"}
+
+
+class Headline:
+    """One rank's resident encode+decode workload: nibbles x [b, L, H, D] padded
+    per head (ecc_shim.py:669-679, D=128 -> 43 codewords), encoded once and
+    corrupted at BER 1e-2 with the reference's Philox stream at global codeword
+    offset `offset0` of `global_n` (injection runs here, before any timing);
+    step() = golay_encode + golay_decode of those buffers."""
+
+    def __init__(self, dev, x, offset0, global_n):
+        from kvecc import ops
+        self.ops = ops
+        b = x.shape[0]
+        gsz = (D + 2) // 3
+        trip = torch.zeros(b, L, H, gsz * 3, dtype=torch.uint8, device=dev)
+        trip[..., :D] = x
+        self.trip = trip.view(-1, 3)
+        self.m = m = self.trip.shape[0]
+        self.cw = torch.empty(m, dtype=torch.int32, device=dev)
+        ops.golay_encode_into(self.trip.view(-1), self.cw, m)
+        self.noisy = torch.empty_like(self.cw)
+        self.inj_stats = ops.new_stats(dev)
+        self.offset0, self.global_n = offset0, global_n
+        ops.inject_into(self.cw, self.noisy, BER, 24, seed=SEED, stats=self.inj_stats, global_n=global_n,
+                        offset0=offset0)
+        self.out_trip = torch.empty(m * 3, dtype=torch.uint8, device=dev)
+        self.counts = torch.empty(m, dtype=torch.uint8, device=dev)
+        self.stats = ops.new_stats(dev)
+        torch.cuda.synchronize()
+
+    def step(self, st=None):
+        self.ops.golay_encode_into(self.trip.view(-1), self.cw, self.m)
+        self.ops.golay_decode_into(self.noisy, self.out_trip, self.counts, self.stats if st is None else st)
 
 
 def fused_decode_bench(dev, steps, warmup, packed=False):
@@ -499,20 +653,27 @@ def cpu_backend_baseline(budget_s, threads):
                       f"host threads; one_thread: median of {reps1} passes on 1 thread"}
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    args = parse(argv)
     # --gpus N > 1 without a launcher: start the N ranks as child processes
     # (before anything here touches the GPU) and exit with their status
     from kvecc import launch
-    rc = launch.launch_if_needed(os.path.abspath(__file__), sys.argv[1:], args.gpus, args.backend)
+    if args.gpus is None:  # under torchrun: the launcher's world
+        args.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    rc = launch.launch_if_needed(os.path.abspath(__file__), sys.argv[1:] if argv is None else list(argv),
+                                 args.gpus, args.backend)
     if rc is not None:
         sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    if world != args.gpus:  # only an explicit --gpus can disagree
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
+    if args.scaling == "strong" and world > B:
+        print(f"bench: --scaling strong splits B={B}: at most {B} ranks, got {world}", file=sys.stderr)
+        sys.exit(2)
+    gloo = args.backend == "gloo"
     # one GPU per rank; --backend gloo lets several ranks share one device to
     # rehearse the multi-rank path on a 1-GPU box (RCCL refuses that)
     ngpu = torch.cuda.device_count()
@@ -538,24 +699,21 @@ def main():
     kvecc.require_hip()
 
     # ---- synthetic INT4 KV tensor, resident in HBM ---------------------------
-    gen = torch.Generator().manual_seed(rank)
-    x = torch.randint(0, 16, (B, L, H, D), generator=gen, dtype=torch.uint8).to(dev)
     gsz = (D + 2) // 3                      # 43 codewords per head vector
-    trip = torch.zeros(B, L, H, gsz * 3, dtype=torch.uint8, device=dev)
-    trip[..., :D] = x                        # ecc_shim.py:669-679 per-head padding
-    trip = trip.view(-1, 3)
-    m = trip.shape[0]
+    if args.scaling == "weak":
+        # every rank owns a whole [8,4096,32,128] tensor (seed = rank), codeword
+        # offset rank*M of the concatenation
+        gen = torch.Generator().manual_seed(rank)
+        x = torch.randint(0, 16, (B, L, H, D), generator=gen, dtype=torch.uint8).to(dev)
+        m1 = B * L * H * gsz
+        hl = Headline(dev, x, rank * m1, m1 * world)
+    else:
+        x, off, gn = strong_setup(dev, rank, world)
+        hl = Headline(dev, x, off, gn)
     del x
-    cw = torch.empty(m, dtype=torch.int32, device=dev)
-    ops.golay_encode_into(trip.view(-1), cw, m)
-    noisy = torch.empty_like(cw)
-    inj_stats = ops.new_stats(dev)
-    ops.inject_into(cw, noisy, BER, 24, seed=SEED, stats=inj_stats, global_n=m * world,
-                    offset0=rank * m)
-    out_trip = torch.empty(m * 3, dtype=torch.uint8, device=dev)
-    counts = torch.empty(m, dtype=torch.uint8, device=dev)
-    stats = ops.new_stats(dev)
-    torch.cuda.synchronize()
+    trip, cw, noisy, out_trip, counts = hl.trip, hl.cw, hl.noisy, hl.out_trip, hl.counts
+    m, inj_stats, stats = hl.m, hl.inj_stats, hl.stats
+    total_m = hl.global_n  # codewords one step processes over all ranks
 
     kernel_timing = args.timing == "kernel"
 
@@ -618,14 +776,12 @@ def main():
         dec_ms = sum(e[1].elapsed_time(e[2]) for e in timed) / len(timed)
     tt = torch.tensor([elapsed, enc_ms, dec_ms], dtype=torch.float64, device=dev)
     st = ops.stats_totals(stats)
-    per_rank = [tt.tolist()]
+    per_rank = [tt.tolist() + [m]]
     world_info = {"backend": None, "world_size": 1}
     if dist is not None:
-        if args.backend == "gloo":  # gloo reduces host tensors
+        per_rank = gather_floats(dist, world, dev, tt.tolist() + [m], gloo)  # per-rank times, reported
+        if gloo:  # gloo reduces host tensors
             tt, st = tt.cpu(), st.cpu()
-        gathered = [torch.empty_like(tt) for _ in range(world)]
-        dist.all_gather(gathered, tt)                 # per-rank times, reported
-        per_rank = [g.tolist() for g in gathered]
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dist.all_reduce(st, op=dist.ReduceOp.SUM)     # the single stats all-reduce
         world_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
@@ -656,11 +812,32 @@ def main():
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
 
+    # ---- collective sections: every rank runs them, together, before the
+    # rank-0-only sections.  One rank: a failure is recorded like an optional
+    # section's.  Several ranks: a failure raises (a rank that skipped a
+    # collective would leave the others waiting), and the launcher stops them.
+    def collective(name, fn):
+        if dist is None:
+            return optional(name, fn)
+        try:
+            return fn()
+        finally:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
+    # strong scaling beside the weak headline (with --scaling strong the
+    # headline itself is the strong figure)
+    strong = None if args.no_strong or args.scaling == "strong" or world > B else collective(
+        "strong", lambda: strong_section(dev, dist, rank, world, args.steps, args.warmup, gloo))
+    # BASELINE config 5, batch-sharded over the ranks with one all-reduce
+    montecarlo = None if args.no_montecarlo else collective(
+        "montecarlo", lambda: montecarlo_bench(dev, dist, rank, world, gloo))
+
     # ---- injection throughput (VALU-bound, Philox4x32-10 per bit) ------------
     def inject_section():
         scratch = ops.new_stats(dev)
         inj_ms = kernel_ms(dev, lambda: ops.inject_into(cw, noisy, BER, 24, seed=SEED, stats=scratch,
-                                                        global_n=m * world, offset0=rank * m), 10, 3)
+                                                        global_n=total_m, offset0=hl.offset0), 10, 3)
         philox = m * 24  # one Philox4x32-10 per bit (fault_injection_triton.py:303-334)
         res = {"kernel": "inject_kernel<int32, 24> (with stats)", "ms": inj_ms,
                "codewords_per_s": m / (inj_ms * 1e-3), "philox_per_s": philox / (inj_ms * 1e-3),
@@ -699,7 +876,7 @@ def main():
 
         def one():
             ops.golay_encode_into(trip.view(-1), cw, m)
-            ops.inject_into(cw, noisy2, BER, 24, seed=SEED, global_n=m * world, offset0=rank * m)
+            ops.inject_into(cw, noisy2, BER, 24, seed=SEED, global_n=total_m, offset0=hl.offset0)
             ops.golay_decode_into(noisy2, out_trip, counts, scratch)
 
         for _ in range(2):
@@ -773,7 +950,6 @@ def main():
         "interp", lambda: interp_bench(dev, max(args.steps, 10), side_warmup))
     quant = None if args.no_quant else optional(
         "fused_quant", lambda: quant_bench(dev, max(args.steps, 10), side_warmup))
-    montecarlo = None if args.no_montecarlo or world > 1 else optional("montecarlo", lambda: montecarlo_bench(dev))
 
     fused = None
     if not args.no_fused:
@@ -790,8 +966,10 @@ def main():
             dist.destroy_process_group()
         return
 
-    total_cw = m * world * args.steps
+    total_cw = total_m * args.steps  # every rank's codewords over the slowest rank's time
     value = total_cw / elapsed
+    if args.scaling == "strong":  # shards differ in size: rank 0's own kernels and codewords
+        enc_ms, dec_ms = per_rank[0][1], per_rank[0][2]
     dec_gbs = DECODE_BYTES_PER_CW * m / (dec_ms * 1e-3) / 1e9
     enc_gbs = ENCODE_BYTES_PER_CW * m / (enc_ms * 1e-3) / 1e9
     traffic = None
@@ -821,18 +999,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8/int32 (bitwise)",
-        "data": "synthetic: torch.randint(0,16) INT4 nibbles, seed=rank; BER 1e-2 Philox corruption",
-        "config": {"workload": "golay24 per-head encode+decode, [B=8,L=4096,H=32,D=128] per GPU",
-                   "codewords_per_gpu": m, "ber": BER, "seed": SEED, "parallelism": f"dp{world}",
-                   "global_batch": B * world, "seq_len": L,
+        "data": ("synthetic: torch.randint(0,16) INT4 nibbles, seed=rank; BER 1e-2 Philox corruption"
+                 if args.scaling == "weak" else
+                 "synthetic: ONE torch.randint(0,16) [8,4096,32,128] tensor (seed 0) split along B; "
+                 "BER 1e-2 Philox corruption"),
+        "config": {"workload": ("golay24 per-head encode+decode, [B=8,L=4096,H=32,D=128] per GPU"
+                                if args.scaling == "weak" else
+                                "golay24 per-head encode+decode, ONE [B=8,L=4096,H=32,D=128] split along B"),
+                   "codewords_per_gpu": m, "codewords_per_step": total_m, "ber": BER, "seed": SEED,
+                   "parallelism": f"dp{world}",
+                   "global_batch": B * world if args.scaling == "weak" else B, "seq_len": L,
                    "process_group": world_info,
                    "launcher": ("self (bench.py spawned its ranks)" if os.environ.get(launch.ENV_LAUNCHED) == "1"
                                 else "external (torchrun)" if world > 1 else "single process"),
                    "per_rank": [{"rank": r, "elapsed_s": v[0], "encode_ms": v[1], "decode_ms": v[2],
-                                 "codewords_per_s": m * args.steps / v[0]}
+                                 "codewords": int(v[3]), "codewords_per_s": v[3] * args.steps / v[0]}
                                 for r, v in enumerate(per_rank)]},
         "hbm_gbs": {"decode": dec_gbs, "encode": enc_gbs,
                     "round_trip": (DECODE_BYTES_PER_CW + ENCODE_BYTES_PER_CW) * m
@@ -855,6 +1039,7 @@ def main():
         "golay_rows": rows,
         "interp": interp,
         "fused_quant": quant,
+        "strong_scaling": strong,
         "montecarlo": montecarlo,
         "packed": packed,
         "cpu_baseline": cpu,

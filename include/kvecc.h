@@ -107,6 +107,10 @@ KVECC_API int kvecc_reserve_counter_slots(int device, int n);
 /* Diagnostic (synchronises the device): slots handed out, and how many counter
  * words of all slots are non-zero -- 0 whenever no launch is in flight. */
 KVECC_API int kvecc_counter_slots_check(int device, int64_t *slots_in_use, int64_t *nonzero_words);
+/* Test hook: on != 0 makes the step that ties a captured launch's slot to its
+ * graph fail (as hipGraphRetainUserObject might); such a slot then stays with
+ * its capture for the life of the process instead of returning to the pool. */
+KVECC_API int kvecc_debug_fail_graph_retain(int on);
 /* Host copies of the code tables the kernels use (for verification):
  *   syndrome table as the reference builds it, config.py:403-457 -> int32[4096]
  *   H row masks, config.py:354-379 -> uint32[12]                              */

@@ -227,7 +227,13 @@ struct SlotPool {
   std::mutex ret_mu;
   std::vector<uint32_t *> returned;
 };
-static SlotPool g_pool[kMaxDev];
+// never destroyed: a graph user object's destructor (release_captured_slot)
+// may run from a HIP runtime thread or during runtime teardown at exit, after
+// static destructors; a heap array outlives both
+static SlotPool *const g_pool = new SlotPool[kMaxDev];
+// test hook (kvecc_debug_fail_graph_retain): make the graph-retain step of a
+// capture's slot fail, to exercise that branch
+static std::atomic<int> g_fail_retain{0};
 constexpr int kSlotChunk = 64;    // slots per allocation (3 MiB)
 constexpr int kSlotReserve = 32;  // free slots kept for graph captures
 
@@ -281,8 +287,8 @@ struct SlotRelease {
 
 static void release_captured_slot(void *arg) {  // HIP user-object destructor
   SlotRelease *r = static_cast<SlotRelease *>(arg);
-  SlotPool &p = g_pool[r->dev];
-  {
+  if (r->slot) {  // null: the slot was never tied to a graph and stays with its capture
+    SlotPool &p = g_pool[r->dev];
     std::lock_guard<std::mutex> lk(p.ret_mu);
     p.returned.push_back(r->slot);
   }
@@ -352,8 +358,15 @@ uint32_t *counter_slot(void *stream) {
     hipUserObject_t obj = nullptr;
     if (hipUserObjectCreate(&obj, r, release_captured_slot, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
       delete r;
-    } else if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
-      (void)hipUserObjectRelease(obj, 1);  // runs the destructor: the slot goes back
+    } else if (g_fail_retain.load(std::memory_order_relaxed) ||
+               hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+      // the graph does not hold the object, so nothing tells us when the graph
+      // dies: the slot must stay with this capture for the process's life (as
+      // with no graph handle).  Detach it before dropping our reference, whose
+      // destructor would otherwise return a slot the capture still uses
+      r->slot = nullptr;
+      (void)hipUserObjectRelease(obj, 1);
+      (void)hipGetLastError();
     }
   }
   return s;
@@ -401,6 +414,11 @@ KVECC_API int kvecc_reserve_counter_slots(int device, int n) {
     const int rc = grow_pool(device, p);
     if (rc != KVECC_OK) return rc;
   }
+  return KVECC_OK;
+}
+
+KVECC_API int kvecc_debug_fail_graph_retain(int on) {
+  g_fail_retain.store(on ? 1 : 0, std::memory_order_relaxed);
   return KVECC_OK;
 }
 

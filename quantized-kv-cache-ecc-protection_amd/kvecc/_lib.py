@@ -29,6 +29,7 @@ SIGNATURES = {
     "kvecc_init_device": [_int],
     "kvecc_reserve_counter_slots": [_int, _int],
     "kvecc_counter_slots_check": [_int, _vp, _vp],
+    "kvecc_debug_fail_graph_retain": [_int],
     "kvecc_golay_syndrome_table_host": [_vp],
     "kvecc_golay_h_row_masks_host": [_vp],
     "kvecc_ber_threshold": [_f32],

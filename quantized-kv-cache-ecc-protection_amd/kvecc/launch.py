@@ -74,17 +74,24 @@ def rank_env(rank: int, world: int, port: int, base=None) -> dict:
     return env
 
 
-def spawn(script: str, argv: list, world: int, timeout: float | None = None,
+def spawn(script, argv: list, world: int, timeout: float | None = None,
           poll: float = 0.2) -> int:
-    """Run `python script *argv` as `world` ranks; return the launch's exit code:
+    """Run `python script *argv` as `world` ranks -- `script` a path, or the
+    interpreter arguments that name the program, e.g. ["-m", "kvecc.montecarlo"]
+    (the package root then joins each rank's PYTHONPATH) -- and return the launch's exit code:
     0 when every rank exited 0, else the first failing rank's code (a rank
     killed by a signal gives 128 + signal).  When one rank fails the others
     are terminated, so a rank stuck in a collective does not hang the launch."""
     port = free_port()
+    prog = list(script) if isinstance(script, (list, tuple)) else [script]
     procs = []
     for r in range(world):
         out = None if r == 0 else 2  # fd 2: the other ranks' stdout joins stderr
-        procs.append(subprocess.Popen([sys.executable, script, *argv], env=rank_env(r, world, port),
+        env = rank_env(r, world, port)
+        if prog and prog[0] == "-m":  # a module: make its package importable in the rank
+            root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            env["PYTHONPATH"] = os.pathsep.join(p for p in (root, env.get("PYTHONPATH")) if p)
+        procs.append(subprocess.Popen([sys.executable, *prog, *argv], env=env,
                                       stdout=out, start_new_session=True))
     t0 = time.monotonic()
     rc = 0
@@ -129,7 +136,7 @@ def _stop(procs, grace: float = 10.0) -> None:
             p.wait()
 
 
-def launch_if_needed(script: str, argv: list, gpus: int, backend: str) -> int | None:
+def launch_if_needed(script, argv: list, gpus: int, backend: str) -> int | None:
     """In the parent of a multi-rank run: check the devices, spawn the ranks and
     return the exit code for sys.exit.  In a rank (or a single-rank run): None."""
     if not needs_spawn(gpus):

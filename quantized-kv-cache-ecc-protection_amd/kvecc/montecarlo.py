@@ -152,9 +152,12 @@ class HipShard:
         self.k = 0
         self.pending = None
         self._stat_chunks, self._queued = [], []  # fused: statistics buffers, (buffer, row) per trial
-        # the fused interpolating trial reads 4-value column chunks
-        self.fused = fused = fused and (h * d) % 4 == 0
-        if fused:
+        # the fused interpolating trial reads 4-value column chunks: at a
+        # geometry with heads*head_dim % 4 != 0 that one codec runs the
+        # kernel-by-kernel pipeline, every other codec stays fused
+        self._interp_unfused = fused and (h * d) % 4 != 0
+        self.bufs = None
+        if fused and not self._interp_unfused:
             return
         with torch.cuda.device(self.dev):
             self.bufs = [_TrialBuffers(ops, shape, self.g, self.dev) for _ in range(2)]
@@ -176,7 +179,7 @@ class HipShard:
         ops = self.ops
         if self.sb == 0:
             return row
-        if self.fused:
+        if self.uses_fused(codec):
             st = self._stats_buffer()
             golay = codec == "golay"
             ops.mc_trial_into(self.x, codec, ber, seed, self.m_total if golay else self.n_total,
@@ -241,11 +244,16 @@ class HipShard:
             row[4:5] += ops.stats_totals(buf.st_cmp, 1)
             buf.free.record(self.s_dec)
 
+    def uses_fused(self, codec):
+        """True when `codec`'s trials run as one kvecc_mc_trial launch."""
+        return self.fused and not (codec == "hamming84_interp" and self._interp_unfused)
+
     def finish(self):
-        """Fold the fused trials' statistics into their rows, or drain the
+        """Fold the fused trials' statistics into their rows and drain the
         pipeline; the caller's stream then holds every queued trial's counters."""
         if self.fused:
             self._fold()
+        if self.bufs is None:
             return
         self._drain()
         caller = torch.cuda.current_stream(self.dev)
@@ -417,7 +425,10 @@ def main(argv=None):
     args = ap.parse_args(argv)
     from . import launch
     gpus = args.gpus if args.gpus is not None else int(os.environ.get("WORLD_SIZE", "1"))
-    rc = launch.launch_if_needed(os.path.abspath(sys.argv[0]), list(sys.argv[1:] if argv is None else argv),
+    # the ranks run this module's entry point (not sys.argv[0], which under
+    # `python -m kvecc.montecarlo` is this file, unimportable as a script, and
+    # under another program calling main(argv) is that program)
+    rc = launch.launch_if_needed(["-m", "kvecc.montecarlo"], list(sys.argv[1:] if argv is None else argv),
                                  gpus, args.backend)
     if rc is not None:
         sys.exit(rc)

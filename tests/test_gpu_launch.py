@@ -97,3 +97,49 @@ def test_sweep_spawns_two_gloo_ranks_equal_to_one(gpu, tmp_path):
     r2, s2 = rows(two.stdout)
     assert s1["world"] == 1 and s2["world"] == 2 and s2["backend"] == "gloo"
     assert r1 == r2 and len(r1) == 2
+
+
+def _bench(*args, timeout=300):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args],
+                       capture_output=True, text=True, timeout=timeout, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    return _json_line(r.stdout)
+
+
+@pytest.mark.gpu
+def test_bench_sharded_sweep_and_strong_scaling_equal_one_rank(gpu):
+    """What the driver's N-GPU run records beside the weak headline: the config-5
+    sweep batch-sharded over the ranks with its one all-reduce, and the strong-
+    scaling split of the headline tensor.  Two gloo ranks sharing cuda:0 must
+    give the single rank's counter table (same sha256) and the same all-reduced
+    decode / injection statistics."""
+    common = ["--steps", "3", "--warmup", "1", "--roofline-samples", "1", "--sections", "montecarlo,strong"]
+    one = _bench("--gpus", "1", *common)
+    two = _bench("--gpus", "2", "--backend", "gloo", *common)
+    m1, m2 = one["montecarlo"], two["montecarlo"]
+    assert m1["world"] == 1 and m2["world"] == 2 and m1["trials"] == m2["trials"] == 36
+    assert m2["table_sha256"] == m1["table_sha256"]
+    assert [p["batch_rows"] for p in m2["per_rank"]] == [[0, 4], [4, 8]]
+    assert m2["collective"].endswith("(gloo)") and m1["collective"] is None
+    assert m2["ms"] == pytest.approx(max(p["ms"] for p in m2["per_rank"]))
+    s1, s2 = one["strong_scaling"], two["strong_scaling"]
+    assert s1["world"] == 1 and s2["world"] == 2
+    assert s1["codewords_total"] == s2["codewords_total"] == 8 * 4096 * 32 * 43
+    assert sum(p["codewords"] for p in s2["per_rank"]) == s2["codewords_total"]
+    assert s2["decode_stats"] == s1["decode_stats"] and s2["inject_stats"] == s1["inject_stats"]
+    assert s1["decode_stats"]["bits_corrected"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_strong_headline_two_ranks(gpu):
+    """--scaling strong: the headline itself splits the one tensor; value counts
+    the whole tensor per step over the slowest rank, statistics equal one rank's."""
+    common = ["--steps", "4", "--warmup", "1", "--roofline-samples", "1", "--no-sections", "--scaling", "strong"]
+    one = _bench("--gpus", "1", *common)
+    two = _bench("--gpus", "2", "--backend", "gloo", *common)
+    assert one["scaling"] == two["scaling"] == "strong"
+    total = 8 * 4096 * 32 * 43
+    assert two["config"]["codewords_per_step"] == total and two["config"]["codewords_per_gpu"] == total // 2
+    slowest = max(p["elapsed_s"] for p in two["config"]["per_rank"])
+    assert two["value"] == pytest.approx(total * 4 / slowest, rel=1e-6)
+    assert two["decode_stats"] == one["decode_stats"]

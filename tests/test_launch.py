@@ -118,3 +118,51 @@ def test_sweep_fails_fast_without_enough_gpus():
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 2, r.stderr
     assert "needs 4 GPUs" in r.stderr
+
+
+def test_bench_strong_scaling_rejects_more_ranks_than_rows():
+    """--scaling strong splits the B=8 rows of the one tensor: 9 ranks is an error before any GPU work."""
+    env = dict(os.environ, WORLD_SIZE="9", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "9", "--scaling", "strong",
+                        "--steps", "1"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2, r.stderr
+    assert "at most 8 ranks" in r.stderr
+
+
+def test_bench_sections_flag():
+    """--sections keeps exactly the named sections; an unknown name is a usage error."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = bench.parse(["--sections", "montecarlo,strong"])
+    assert not a.no_montecarlo and not a.no_strong
+    assert all(getattr(a, f) for s, f in bench.SECTIONS.items() if s not in ("montecarlo", "strong"))
+    a = bench.parse(["--no-sections"])
+    assert all(getattr(a, f) for f in bench.SECTIONS.values())
+    a = bench.parse([])
+    assert a.gpus is None and not any(getattr(a, f) for f in bench.SECTIONS.values())
+    with pytest.raises(SystemExit):
+        bench.parse(["--sections", "nope"])
+
+
+def test_spawn_module_form(tmp_path):
+    """spawn(["-m", module]) runs a module entry point in every rank (the sweep's
+    self-launch: `python -m kvecc.montecarlo --gpus N`), with kvecc importable."""
+    pkg = tmp_path / "mod_pkg"
+    pkg.mkdir()
+    (pkg / "__init__.py").write_text("")
+    (pkg / "rank.py").write_text("import kvecc.launch\n" + _RANK_SCRIPT)
+    code = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd")!r})
+        from kvecc import launch
+        sys.exit(launch.spawn(["-m", "mod_pkg.rank"], ["-1"], 2))
+    """)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", launch.ENV_LAUNCHED)}
+    env.pop("PYTHONPATH", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env,
+                       cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert json.loads(lines[0]) == {"world": 2, "sum": 3, "argv": ["-1"]}

@@ -277,8 +277,10 @@ def test_hip_sweep_gloo_world2_on_one_gpu_equals_single(gpu, tmp_path):
 def test_fused_trial_odd_geometry_equals_oracle(gpu, shape):
     """kvecc_mc_trial at geometries off the sweep's: head_dim not a multiple of
     3 (Golay padding) or 4, sequence lengths that end mid row-block (the
-    interpolating trial's edge rows), value counts not a multiple of 4, and
-    shards whose offset starts mid-tensor; every counter equals the oracle's."""
+    interpolating trial's edge rows), value counts not a multiple of 4 (the
+    Hamming kernels' tail; the interpolating trial alone takes the unfused
+    pipeline there), and shards whose offset starts mid-tensor; every counter
+    equals the oracle's."""
     cfg = mc.MonteCarloConfig(shape=shape, bers=(0.03, 0.15), seeds=(42,))
     for world, rank in ((1, 0), (2, 1)):
         if shard_empty(shape, world, rank):
@@ -286,8 +288,9 @@ def test_fused_trial_odd_geometry_equals_oracle(gpu, shape):
         hip = mc.HipShard(cfg, rank, world, gpu, fused=True)
         ora = OracleShard(cfg, rank, world)
         for codec, ber, seed in cfg.trials():
-            if codec == "hamming84_interp" and (shape[2] * shape[3]) % 4:
-                continue  # the fused interpolating trial needs heads*head_dim % 4 == 0
+            # only the interpolating trial needs heads*head_dim % 4 == 0 to run
+            # fused; it falls back to the kernel-by-kernel pipeline otherwise
+            assert hip.uses_fused(codec) == (codec != "hamming84_interp" or (shape[2] * shape[3]) % 4 == 0)
             a = torch.zeros(5, dtype=torch.int64, device=gpu)
             b = torch.zeros(5, dtype=torch.int64)
             hip.run_trial(codec, ber, seed, a)

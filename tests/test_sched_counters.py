@@ -262,3 +262,60 @@ def test_eager_launches_beside_a_global_capture_grow_the_pool(gpu):
     assert _same(gout, base) and ops.read_stats(gst) == base_st
     del g
     destroy()
+
+
+def test_failed_graph_retain_keeps_the_slot_with_its_capture(gpu):
+    """when the slot cannot be tied to its graph (the retain step
+    fails; forced here through kvecc_debug_fail_graph_retain), the slot must
+    stay with the capture for the process's life -- never go back to the pool
+    while the graph can still replay.  So: the graph still replays exactly
+    after 40 eager launches on new streams (each taking a slot of its own), and
+    destroying the graph does not return its slot."""
+    import gc
+    import time
+
+    from kvecc import _lib, ops
+    dev = gpu
+    run, mk, _ = _workloads(dev)["golay_rows"]
+    base, st = mk(), ops.new_stats(dev)
+    run(base, st)
+    torch.cuda.synchronize()
+    base_st = ops.read_stats(st)
+    s = torch.cuda.Stream(dev)
+    out, gs = mk(), ops.new_stats(dev)
+    with torch.cuda.stream(s):
+        run(out, ops.new_stats(dev))
+    torch.cuda.synchronize()
+    used0, _ = ops.counter_slots_check(dev)
+    _lib.call("kvecc_debug_fail_graph_retain", 1)
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            run(out, gs)
+    finally:
+        _lib.call("kvecc_debug_fail_graph_retain", 0)
+    torch.cuda.synchronize()
+    used1, _ = ops.counter_slots_check(dev)
+    assert used1 == used0 + 1, (used0, used1)
+    side, destroy = _hip_streams(40)
+    outs = [mk() for _ in side]
+    for sd, o in zip(side, outs):
+        with torch.cuda.stream(sd):
+            run(o, ops.new_stats(dev))
+    gs.zero_()
+    for t in out:
+        t.zero_()
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    assert _same(out, base) and ops.read_stats(gs) == base_st
+    assert all(_same(o, base) for o in outs)
+    used2, _ = ops.counter_slots_check(dev)
+    del g
+    gc.collect()
+    torch.cuda.synchronize()
+    time.sleep(0.5)
+    used3, nz = ops.counter_slots_check(dev)
+    assert nz == 0
+    assert used3 == used2, f"the unretained slot went back to the pool: {used2} -> {used3}"
+    destroy()

@@ -1,0 +1,198 @@
+// interp_read_exp.hip -- experimental forms of the fused H(8,4) + interpolation
+// read (csrc/shim.hip shim_read_h84_interp_kernel), NOT shipped: this file
+// #includes shim.hip for its tile helpers; tools/exp/run_interp_read_exp.py
+// times them against the product (kvecc_shim_read_batch) in one process.
+//
+// ipe_kernel<TO, STATS, WAVES, INTERP>: the plain read's structure (full grid,
+// one tile per wave, no start barrier, no LDS flags between waves) plus
+// interpolation where it is needed.  Only a double error in a tile's FIRST or
+// LAST row needs a row of another tile; a tile whose decode saw such a double
+// (a wave ballot, ~0.7 % of tiles at BER 1e-3 with 16-row tiles, against 5.6 %
+// holding any double) loads that row from memory and decodes it.  A double in
+// an interior row interpolates from the wave's own LDS tile.  WAVES = waves
+// per workgroup (the product: 8 -- and a workgroup retires only when its
+// slowest wave does).  INTERP=false: the plain read in the same frame.
+#include "../../quantized-kv-cache-ecc-protection_amd/csrc/shim.hip"
+
+namespace kvecc {
+namespace exp {
+
+template <typename TO, bool STATS, int WAVES, bool INTERP>
+__global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[WAVES][kTileStage];
+  __shared__ float scale_all[WAVES][kWave];
+  const uint32_t wave = WAVES == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  uint8_t *stage = stage_all[wave];
+  const uint32_t cpr = a.d / 16;
+  const uint32_t items = a.tr * cpr;
+  uint32_t ir[kByteTileItems], ic[kByteTileItems];
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    const uint32_t f = lane + kWave * i;
+    ir[i] = f / cpr;
+    ic[i] = f - ir[i] * cpr;
+  }
+  constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
+  const uint32_t gw = blockIdx.x * WAVES + wave;
+  if (gw >= a.units) return;
+  const ShimTile t = shim_tile(a, gw);
+  u32x4 w[kByteTileItems];
+  scale_all[wave][lane] = byte_tile_issue(a, t, lane, ir, ic, items, w);
+  uint32_t n1 = 0, n2 = 0;
+  bool dbl_any = false, dbl_top = false, dbl_bot = false;
+  const uint32_t off0 = INTERP ? a.d : 0u;  // tile row r at stage row r + 1
+#pragma unroll
+  for (int i = 0; i < kByteTileItems; ++i) {
+    if (i * kWave >= (int)items) break;  // uniform
+    const bool real = ir[i] < t.rows;
+    uint32_t dd = 0;
+    u32x4 d4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t q = w[i][k], tt = 0, s1 = 0, s2 = 0;
+      h84_decode4(w[i][k], q, tt, s1, s2);
+      if (real) {
+        if (STATS) {
+          n1 += s1;
+          n2 += s2;
+        }
+        dd |= s2;
+      }
+      d4[k] = INTERP ? q | tt << 4 : q;
+    }
+    if (INTERP) {
+      dbl_any |= dd != 0;
+      dbl_top |= dd != 0 && ir[i] == 0;
+      dbl_bot |= dd != 0 && ir[i] + 1 == t.rows;
+    }
+    if (real) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
+  }
+  bool tile_dbl = false;
+  if (INTERP) tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+  wave_lds_sync();
+  if (INTERP && tile_dbl) {  // wave-uniform
+    const bool need_top = __builtin_amdgcn_ballot_w64(dbl_top) != 0;
+    const bool need_bot = __builtin_amdgcn_ballot_w64(dbl_bot) != 0;
+    const bool below = lane >= cpr;
+    const uint32_t l = below ? lane - cpr : lane;
+    if (lane < 2 * cpr && (below ? need_bot : need_top)) {
+      const bool clamp = below ? t.pos0 + t.rows >= a.ctx : t.pos0 == 0;
+      u32x4 v;
+      if (clamp) {  // the context's first / last row: its own value (the composed read clamps)
+        v = reinterpret_cast<const u32x4 *>(stage + off0 + (below ? t.rows - 1 : 0u) * a.d)[l];
+      } else {
+        const uint32_t bh = t.bh, b = bh / a.hkv, h = bh - b * a.hkv;
+        const uint32_t pos = below ? t.pos0 + t.rows : t.pos0 - 1;
+        const int32_t blk = a.table[(int64_t)b * a.tstride + pos / a.bs];
+        u32x4 hw{0u, 0u, 0u, 0u};
+        if (blk >= 0) {
+          const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos % a.bs);
+          hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[t.side]) +
+                                                         row * a.d) + l);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t q = hw[k], tt = 0, s1 = 0, s2 = 0;
+          h84_decode4(hw[k], q, tt, s1, s2);
+          v[k] = q | tt << 4;
+        }
+      }
+      *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;
+    }
+    wave_lds_sync();
+  }
+  const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+  const bool dead = t.row0 < 0;
+  const uint32_t per = cpr * 16 / V;
+  const uint32_t m = uni((65536u + per - 1) / per);
+  auto phase2 = [&](auto interp_c) {
+    constexpr bool IP = decltype(interp_c)::value;
+#pragma unroll
+    for (int i = 0; i < NI2; ++i) {
+      if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
+      const uint32_t f = lane + kWave * i;
+      const uint32_t rr = __umul24(f, m) >> 16, c = f - rr * per;
+      const uint32_t r = min(rr, a.tr - 1);
+      const uint8_t *row = stage + off0 + r * a.d + V * c;
+      uint32_t q[2] = {0u, 0u};
+#pragma unroll
+      for (int k = 0; k < V / 4; ++k) {
+        const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
+        if (IP) {
+          const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+          const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+          q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+        } else {
+          q[k] = v & 0x0F0F0F0Fu;
+        }
+      }
+      tile_store(os, (rr * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+    }
+  };
+  if (tile_dbl)
+    phase2(std::integral_constant<bool, true>{});
+  else
+    phase2(std::integral_constant<bool, false>{});
+  if (STATS) {
+    n1 = wave_sum(n1);
+    n2 = wave_sum(n2);
+    if (lane == 0) {
+      uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+      if (n1) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)n1);
+      if (n2) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)n2);
+    }
+  }
+}
+
+}  // namespace exp
+}  // namespace kvecc
+
+#define EXP_API extern "C" __attribute__((visibility("default")))
+
+// variant: waves per workgroup (1, 2, 4, 8) x interp (0/1); lds_pad = dynamic LDS bytes
+EXP_API int kvecc_exp_ipe(int waves, int interp, int lds_pad, const void *k_cache, const void *v_cache,
+                          const float *k_scales, const float *v_scales, const int32_t *table, int64_t tstride,
+                          int64_t batch, int64_t ctx, int64_t hkv, int64_t d, int64_t block_size, void *k_out,
+                          void *v_out, uint64_t *stats, void *stream) {
+  using namespace kvecc;
+  ShimTileArgs a{};
+  a.cache[0] = k_cache;
+  a.cache[1] = v_cache;
+  a.scales[0] = k_scales;
+  a.scales[1] = v_scales;
+  a.out[0] = k_out;
+  a.out[1] = v_out;
+  a.table = table;
+  a.stats = stats;
+  a.tstride = (uint32_t)tstride;
+  a.hkv = (uint32_t)hkv;
+  a.d = a.g = a.lr = a.rowb = (uint32_t)d;
+  a.layers = 1;
+  a.bs = (uint32_t)block_size;
+  a.layer = 0;
+  a.ctx = (uint32_t)ctx;
+  const int64_t cpr = d / 16;
+  a.tr = (uint32_t)std::min<int64_t>({block_size, (int64_t)kTileStage / d - 2, (int64_t)kWave,
+                                      (int64_t)kWave * kByteTileItems / cpr});
+  a.tpb = (uint32_t)cdiv(block_size, a.tr);
+  a.nlb = (uint32_t)cdiv(ctx, block_size);
+  a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+  hipStream_t st = as_stream(stream);
+  const unsigned pad = (unsigned)lds_pad;
+#define IPE(W)                                                                                              \
+  case W:                                                                                                   \
+    if (interp)                                                                                             \
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, W, true>), dim3((unsigned)cdiv(a.units, W)), dim3(W * 64), \
+                   pad, st, a);                                                                             \
+    else                                                                                                    \
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, W, false>), dim3((unsigned)cdiv(a.units, W)), dim3(W * 64), \
+                   pad, st, a);                                                                             \
+    break;
+  switch (waves) {
+    IPE(1) IPE(2) IPE(4) IPE(8)
+    default: return set_error(KVECC_EINVAL, "waves");
+  }
+#undef IPE
+  return check_launch("exp_ipe");
+}
