@@ -681,38 +681,35 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
 }
 
 // ---- H(8,4) with double-error interpolation (ecc_shim.py:1038-1059,
-// interpolation_triton.py:120-159) on the same full grid, neighbour rows from
-// the workgroup.
-// Interpolating row r needs the decoded rows r - 1 and r + 1; for a tile's
-// first and last rows those are the rows at positions pos0 - 1 and pos0 + rows
-// (the tile's own first / last row at the context's ends, as the composed read
-// clamps).  The 8 waves of a workgroup hold 8 consecutive tiles of the static
-// order -- adjacent blocks of one (side, sequence, head) -- so those rows are
-// the previous wave's last decoded row and the next wave's first, already in
-// LDS.  Interpolation only changes a double error's value, so only a tile whose
-// decode saw a double (a wave ballot; ~5 % of tiles at BER 1e-3) reads
-// neighbours: it waits for its neighbour waves' "decoded" words and copies
-// their edge rows into its stage rows 0 and rows + 1; wave 0's row above and
-// wave 7's row below come from memory (one synchronous row).  No barrier after
-// the decode: with one, every wave waited for the slowest load of its
-// workgroup.  Phase 2 derives each item's (row, chunk) by a reciprocal
-// multiply: with the interpolating body present the compiler re-derived
-// per-item divisions after phase 1, on every wave's critical path.
-// [8,4096,32,128] K+V fp16, BER 1e-3: 142.5-150.3 us against 151.8-158.8 for
-// round 3's persistent grid prefetching every tile's neighbour rows; at 1e-2
-// (every tile holds doubles) 202.7-207.0 against 187.6-199.0
-// (profiles/r04/fused/interp_ladder_inc*.log, tools/exp/bytes_read_exp.hip).
+// interpolation_triton.py:120-159) on the same full grid.
+// Interpolating row r needs the decoded rows r - 1 and r + 1.  Only a double
+// error changes a value, so only a tile whose decode saw one interpolates (a
+// wave ballot: ~5.6 % of 16-row tiles at BER 1e-3), from its own LDS tile --
+// the tile is staged one row down, stage rows 0 and rows + 1 holding the
+// neighbour rows.  Those rows belong to other tiles, and only a double in the
+// tile's FIRST or LAST row reads them (a second ballot, ~0.7 % of tiles): that
+// wave loads the one row from memory (through the block table) and decodes it;
+// at the context's ends the row is the tile's own first / last row, as the
+// composed read clamps.  Every wave is independent -- no start barrier, no
+// flags between waves -- and workgroups are 2 waves, so a wave that does go
+// to memory holds one other wave's slot, not seven.  Phase 2 derives each
+// item's (row, chunk) by a reciprocal multiply (with the interpolating body
+// present the compiler otherwise re-derived per-item divisions after phase 1,
+// on every wave's critical path).
+// [8,4096,32,128] K+V fp16, BER 1e-3: 140.2 us, the plain read's time (140.2),
+// against 148.3 for round 5's kernel -- 8-wave workgroups exchanging edge rows
+// through LDS words behind a start barrier; 1e-2: 184.8 against 190.1; BER 0:
+// 139.9 against 142.4 (profiles/r06/interp_read_ab_*.txt,
+// tools/exp/interp_read_exp.hip: 1 / 4 / 8 waves per workgroup 140.4 / 140.8
+// / 143.0 at 1e-3).
+constexpr int kInterpWaves = 2;  // waves per workgroup of the interpolating read
+
 template <typename TO, bool STATS>
-__global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTileArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
-  __shared__ float scale_all[kTileWaves][kWave];
-  __shared__ uint32_t decoded[kTileWaves];  // wave w's tile is in its stage (1) or not yet (0)
+__global__ __launch_bounds__(kInterpWaves * kWave) void shim_read_h84_interp_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kInterpWaves][kTileStage];
+  __shared__ float scale_all[kInterpWaves][kWave];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
-  // LDS holds what the last workgroup on this CU left: clear the words before
-  // anyone looks (before any load, so the barrier waits for no memory)
-  if (lane == 0) __hip_atomic_store(&decoded[wave], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __syncthreads();
   uint8_t *stage = stage_all[wave];
   const uint32_t cpr = a.d / 16;
   const uint32_t items = a.tr * cpr;
@@ -724,90 +721,66 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTi
     ic[i] = f - ir[i] * cpr;
   }
   constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
+  const uint32_t gw = blockIdx.x * kInterpWaves + wave;
+  if (gw >= a.units) return;
+  const ShimTile t = shim_tile(a, gw);
+  u32x4 w[kByteTileItems];
+  scale_all[wave][lane] = byte_tile_issue(a, t, lane, ir, ic, items, w);
   uint32_t n1 = 0, n2 = 0;
-  // data | error type << 4 per byte; `dbl` collects the double errors
-  auto dec = [&](uint32_t cw, bool count, uint32_t &dbl) -> uint32_t {
+  bool dbl_any = false, dbl_top = false, dbl_bot = false;
+  const uint32_t off0 = a.d;  // tile row r at stage row r + 1
+  // data | error type << 4 per byte of 4 codewords
+  auto dec = [&](uint32_t cw, uint32_t &dbl) -> uint32_t {
     uint32_t q = cw, tt = 0, s1 = 0, s2 = 0;
     h84_decode4(cw, q, tt, s1, s2);
-    if (count) {
-      if (STATS) {
-        n1 += s1;
-        n2 += s2;
-      }
-      dbl |= s2;
+    if (STATS) {
+      n1 += s1;
+      n2 += s2;
     }
+    dbl |= s2;
     return q | tt << 4;
   };
-  const uint32_t gw = blockIdx.x * kTileWaves + wave;
-  const bool active = gw < a.units;  // every wave publishes its word
-  ShimTile t;
-  t.rows = 0;
-  t.row0 = -1;
-  t.pos0 = t.side = t.bh = 0;
-  bool tile_dbl = false;
-  const uint32_t off0 = a.d;  // tile row r at stage row r + 1; rows 0 and rows + 1: the neighbours
-  if (active) {
-    t = shim_tile(a, gw);
-    u32x4 w[kByteTileItems];
-    scale_all[wave][lane] = byte_tile_issue(a, t, lane, ir, ic, items, w);
-    bool dbl_any = false;
 #pragma unroll
-    for (int i = 0; i < kByteTileItems; ++i) {
-      if (i * kWave >= (int)items) break;  // uniform
-      // rows past the tile: no statistics, no doubles, no LDS store (it would
-      // land on the row-below slot)
-      const bool real = ir[i] < t.rows;
+  for (int i = 0; i < kByteTileItems; ++i) {
+    if (i * kWave >= (int)items) break;  // uniform
+    // rows past the tile: no statistics, no doubles, no LDS store (it would
+    // land on the row-below slot)
+    if (ir[i] < t.rows) {
       uint32_t dbl = 0;
-      const u32x4 d4{dec(w[i].x, real, dbl), dec(w[i].y, real, dbl), dec(w[i].z, real, dbl),
-                     dec(w[i].w, real, dbl)};
+      const u32x4 d4{dec(w[i].x, dbl), dec(w[i].y, dbl), dec(w[i].z, dbl), dec(w[i].w, dbl)};
       dbl_any |= dbl != 0;
-      if (real) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
+      dbl_top |= dbl != 0 && ir[i] == 0;
+      dbl_bot |= dbl != 0 && ir[i] + 1 == t.rows;
+      *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
     }
-    tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
   }
-  wave_lds_sync();  // this wave's rows are in LDS before its word says so
-  // release / acquire at workgroup scope: the waiting wave's stage reads are
-  // ordered after the flag it spins on (in the memory model, not by accident of
-  // LDS ordering); both cost a waitcnt
-  if (lane == 0) __hip_atomic_store(&decoded[wave], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (!active || t.rows == 0) return;
-  if (tile_dbl) {  // wave-uniform: the neighbour rows into stage rows 0 and rows + 1
-    const bool top_clamp = t.pos0 == 0, bot_clamp = t.pos0 + t.rows >= a.ctx;
-    const bool ext_a = !top_clamp && wave == 0;               // row above: the previous workgroup's
-    const bool ext_b = !bot_clamp && wave == kTileWaves - 1;  // row below: the next workgroup's
-    // the neighbour tiles exist (same sequence, inside the grid) and belong to
-    // this workgroup, whose waves all publish: the waits end
-    if (!top_clamp && !ext_a)
-      while (__hip_atomic_load(&decoded[wave - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-        __builtin_amdgcn_s_sleep(1);
-    if (!bot_clamp && !ext_b)
-      while (__hip_atomic_load(&decoded[wave + 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-        __builtin_amdgcn_s_sleep(1);
-    const bool below = lane >= cpr;
+  const bool tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+  wave_lds_sync();
+  if (tile_dbl) {  // wave-uniform: the neighbour rows the edge rows' doubles need
+    const bool need_top = __builtin_amdgcn_ballot_w64(dbl_top) != 0;
+    const bool need_bot = __builtin_amdgcn_ballot_w64(dbl_bot) != 0;
+    const bool below = lane >= cpr;  // lanes [0, cpr): the row above; [cpr, 2 cpr): below
     const uint32_t l = below ? lane - cpr : lane;
-    u32x4 hw{0u, 0u, 0u, 0u};
-    if (ext_a || ext_b) {  // one side at most (kTileWaves > 1)
-      const uint32_t bh = uni(t.bh), b = bh / a.hkv, h = bh - b * a.hkv;
-      const uint32_t pos = uni(ext_a ? t.pos0 - 1 : t.pos0 + t.rows);
-      const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + pos / a.bs);
-      if (blk >= 0 && l < cpr && below == ext_b) {
-        const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos - pos / a.bs * a.bs);
-        hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[uni(t.side)]) +
-                                                       row * a.d) + l);
-      }
-      uint32_t none = 0;  // neighbours add no statistics
-      hw = u32x4{dec(hw.x, false, none), dec(hw.y, false, none), dec(hw.z, false, none), dec(hw.w, false, none)};
-    }
-    if (lane < 2 * cpr) {
-      u32x4 v = hw;
-      if (below ? !ext_b : !ext_a) {
-        // the previous tile's last row: it holds tr rows, or, as the last
-        // chunk of the previous block (this tile starts a block), the block's
-        // remainder bs - (tpb - 1) tr
-        const uint32_t prev_rows = t.pos0 % a.bs ? a.tr : a.bs - (a.tpb - 1) * a.tr;
-        const uint8_t *src = below ? (bot_clamp ? stage + t.rows * a.d : stage_all[wave + 1] + off0)
-                                   : (top_clamp ? stage + off0 : stage_all[wave - 1] + prev_rows * a.d);
-        v = reinterpret_cast<const u32x4 *>(src)[l];
+    if (lane < 2 * cpr && (below ? need_bot : need_top)) {
+      u32x4 v;
+      if (below ? t.pos0 + t.rows >= a.ctx : t.pos0 == 0) {  // clamped: the tile's own edge row
+        v = reinterpret_cast<const u32x4 *>(stage + off0 + (below ? t.rows - 1 : 0u) * a.d)[l];
+      } else {
+        const uint32_t b = t.bh / a.hkv, h = t.bh - b * a.hkv;
+        const uint32_t pos = below ? t.pos0 + t.rows : t.pos0 - 1;
+        const int32_t blk = a.table[(int64_t)b * a.tstride + pos / a.bs];
+        u32x4 hw{0u, 0u, 0u, 0u};  // a missing block reads as zero codewords
+        if (blk >= 0) {
+          const int64_t row = (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + (pos % a.bs);
+          hw = ld_stream(reinterpret_cast<const u32x4 *>(reinterpret_cast<const uint8_t *>(a.cache[t.side]) +
+                                                         row * a.d) + l);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // decoded as the tile's rows; neighbours add no statistics
+          uint32_t q = hw[k], tt = 0, s1 = 0, s2 = 0;
+          h84_decode4(hw[k], q, tt, s1, s2);
+          v[k] = q | tt << 4;
+        }
       }
       *reinterpret_cast<u32x4 *>(stage + (below ? t.rows + 1 : 0u) * a.d + 16 * l) = v;
     }
@@ -834,7 +807,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_h84_interp_kernel(ShimTi
 #pragma unroll
       for (int k = 0; k < V / 4; ++k) {
         const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
-        if (IP) {
+        if (IP) {  // a neighbour row no double reads may be stale LDS: interp_word ignores it
           const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
           const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
           q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
@@ -954,11 +927,11 @@ static void launch_bytes_plain(const ShimTileArgs &a, hipStream_t st) {
 template <typename TO>
 static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
   if (codec == KVECC_CODEC_H84 && interp) {
-    const unsigned grid = (unsigned)cdiv(a.units, kTileWaves);
+    const unsigned grid = (unsigned)cdiv(a.units, kInterpWaves);
     if (a.stats)
-      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad, st, a);
+      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true>), dim3(grid), dim3(kInterpWaves * kWave), 0, st, a);
     else
-      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad, st, a);
+      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false>), dim3(grid), dim3(kInterpWaves * kWave), 0, st, a);
   } else if (codec == KVECC_CODEC_H84) {
     launch_bytes_plain<TO, KVECC_CODEC_H84>(a, st);
   } else if (codec == KVECC_CODEC_H74) {

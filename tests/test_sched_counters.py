@@ -117,6 +117,7 @@ def test_two_streams_and_graph_replay_keep_counters_private(gpu):
     torch.cuda.synchronize()
     for st in gst.values():
         st.zero_()
+    s3.wait_stream(torch.cuda.current_stream())  # the zeroing lands before the replays
     replays = 0
     for i in range(12):
         with torch.cuda.stream(s3):
@@ -183,6 +184,7 @@ def test_many_captures_on_one_stream_and_slot_release(gpu):
         gs.zero_()
         for t in out:
             t.zero_()
+        s.wait_stream(torch.cuda.current_stream())  # the zeroing lands before the replay
         with torch.cuda.stream(s):
             g.replay()
         torch.cuda.synchronize()
@@ -256,6 +258,7 @@ def test_eager_launches_beside_a_global_capture_grow_the_pool(gpu):
     gst.zero_()
     for t in gout:
         t.zero_()
+    a.wait_stream(torch.cuda.current_stream())  # the zeroing lands before the replay
     with torch.cuda.stream(a):
         g.replay()
     torch.cuda.synchronize()
@@ -305,6 +308,9 @@ def test_failed_graph_retain_keeps_the_slot_with_its_capture(gpu):
     gs.zero_()
     for t in out:
         t.zero_()
+    # the zeroing (default stream, behind the blocking side streams' launches)
+    # must land before the replay on the non-blocking capture stream
+    s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         g.replay()
     torch.cuda.synchronize()

@@ -248,13 +248,13 @@ def test_hip_batch_read_interp_vs_cpu(gpu, batch, ctx, hkv, d, bs, dtype):
     assert ops.read_stats(gst) == cpu_ops.read_stats(st)
 
 
-# many workgroups of 8 tiles (shim_read_h84_interp_kernel: one tile per wave,
-# neighbour rows from the adjacent waves, from memory at a workgroup's ends):
-# several tiles per block (bs 64 > 16 rows per tile), partial last blocks,
-# missing blocks (first, inner, last).  At low BER most tiles hold no double
-# error (no interpolation arithmetic, no neighbour rows) and a few need their
-# neighbours' rows; at 2e-2 every tile does, so every workgroup-boundary row
-# is read from memory and every inner one from a neighbour wave.
+# many tiles (shim_read_h84_interp_kernel: one tile per wave; a double in a
+# tile's first or last row reads the neighbour row from memory, an interior one
+# interpolates inside the tile): several tiles per block (bs 64 > 16 rows per
+# tile), partial last blocks, missing blocks (first, inner, last; a neighbour
+# row in a missing block reads as zero codewords).  At low BER most tiles hold
+# no double error (no interpolation arithmetic, no neighbour rows) and a few
+# need a neighbour row; at 2e-2 nearly every tile edge does.
 MANY_TILE_CASES = [(4, 2001, 4, 32, 6, 2e-2), (3, 5000, 8, 128, 64, 2e-2), (2, 4099, 16, 64, 16, 1e-3),
                    (3, 5000, 8, 128, 64, 1e-3), (4, 2001, 4, 32, 6, 3e-4), (2, 4099, 16, 128, 16, 0.0),
                    (2, 3001, 4, 256, 16, 2e-2), (3, 2500, 4, 128, 24, 2e-2)]
