@@ -28,14 +28,22 @@ def kv_cache_pair(shape, dtype, device):
     packed Golay attention at [8,4096,32,128] ran 62.6 / 80.7 / 74.2 us with V
     right after K against 56.1 / 74.2 / 71.5 us with a 12,800-byte skew
     (tools/exp/attn_alias.py, profiles/r02/attention/kv_skew.log).  Both views
-    are contiguous and 256-byte aligned; nothing else about the layout changes."""
+    are contiguous and 256-byte aligned; nothing else about the layout changes.
+
+    V is handed out as its OWN storage over its bytes of the allocation
+    (re-imported through DLPack, which keeps the allocation alive), not as a
+    view of K's storage.  The two never overlap, but torch.compile's
+    functionalization sees two views of one storage as aliased inputs: the
+    shim's cache-write operator, which mutates both, then got a synthetic base
+    and inductor cloned the WHOLE allocation around every layer's write (and
+    copied it back), instead of writing the caches in place."""
     n = 1
     for x in shape:
         n *= int(x)
     esz = torch.empty((), dtype=dtype).element_size()
     v_off = ((n * esz + 255) // 256 * 256 + KV_SKEW_BYTES) // esz
     buf = torch.zeros(v_off + n, dtype=dtype, device=device)
-    return buf[:n].view(shape), buf[v_off:v_off + n].view(shape)
+    return buf[:n].view(shape), torch.from_dlpack(buf[v_off:v_off + n].view(shape))
 
 
 class ECCCacheConfig:
