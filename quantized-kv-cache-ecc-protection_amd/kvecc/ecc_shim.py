@@ -206,8 +206,15 @@ class SimpleBlockManager:
         return self.seq_to_len.get(seq_id, 0)
 
     def reset(self):
+        # every block back in ascending order.  The reference appends the
+        # returned blocks to the free list (ecc_shim.py:349-353), so each reset
+        # rotates the physical ids the next forward gets; nothing observable
+        # depends on them (the caches are zeroed here), but torch.compile
+        # specialises a traced forward's allocation on the free list, and a
+        # rotating list recompiled the patched model on every forward
         for blocks in self.seq_to_blocks.values():
             self.free_blocks.extend(blocks)
+        self.free_blocks.sort()
         self.seq_to_blocks.clear()
         self.seq_to_len.clear()
         self._host_table.clear()

@@ -248,3 +248,33 @@ def test_inductor_writes_caches_in_place_cpu():
     code = "\n".join(codes)
     assert "torch.ops.kvecc.shim_write.default" in code and "torch.ops.kvecc.shim_read.default" in code
     assert "copy_" not in code, [ln for ln in code.splitlines() if "copy_" in ln]
+
+
+def test_compiled_patched_model_does_not_recompile_across_forwards_cpu():
+    """A whole patched model under torch.compile(fullgraph=True): the forwards a
+    serving / evaluation loop runs (reset_ecc_cache, then the model) hit the
+    first compiled graph.  The block manager's free list is traced (allocation
+    pops it); SimpleBlockManager.reset restores it to ascending order, where the
+    reference's rotating list forced a recompile per forward."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+    from kvecc.ecc_shim import ECCShimConfig, get_ecc_stats, patch_model_with_ecc_attention, reset_ecc_cache
+    torch.manual_seed(0)
+    model = GPT2LMHeadModel(GPT2Config(n_layer=2, n_head=4, n_embd=128, n_positions=128,
+                                       vocab_size=100)).eval()
+    cfg = ECCShimConfig(codec="hamming84", ber=1e-2, inject_errors=True, seed=42, block_size=16,
+                        use_interpolation=True, backend="cpu")
+    ids = torch.randint(0, 100, (1, 48), generator=torch.Generator().manual_seed(3))
+    with torch.no_grad(), patch_model_with_ecc_attention(model, cfg, num_blocks=12):
+        reset_ecc_cache(model)
+        ref = model(ids).logits
+        st = get_ecc_stats(model)
+        torch._dynamo.reset()
+        comp = torch.compile(model, fullgraph=True, backend="aot_eager")
+        reset_ecc_cache(model)
+        comp(ids)
+        with torch._dynamo.config.patch(error_on_recompile=True):
+            for _ in range(3):
+                reset_ecc_cache(model)
+                out = comp(ids).logits
+                assert get_ecc_stats(model) == st
+        assert torch.equal(out, ref)
