@@ -844,26 +844,28 @@ def main(argv=None):
                "flips": ops.read_stats(inj_stats)[0], "bound": "valu",
                "timing": "HIP events carried by the dispatch, mean of 10 launches after >= 3 warm-up calls"}
         # VALU roofline: wave-level VALU instructions per Philox from the committed
-        # SQ_INSTS_VALU pass (rocprofv3 cannot run inside this process) x the live
-        # Philox rate.  Peak = what the SIMDs issue for this kernel's opcode mix:
-        # each opcode's share (its gfx950 disassembly) at its measured issue cost
-        # (profiles/r05/valu_rate.json: 32-bit multiplies, shifts and add3 take
-        # 4.15 cycles per wave64 instruction, v_bitop3 3.7, v_add_u32 2.4).  The
-        # nominal 2-cycle rate of 256 CUs x 4 SIMD-32 x 2.4 GHz is reported beside it.
+        # counter pass (rocprofv3 cannot run inside this process) x the live
+        # Philox rate.  Peak = the VALU issue slots of 256 CUs x 4 SIMDs at the
+        # 2.4 GHz spec clock, one wave64 instruction per quad-cycle per SIMD, the
+        # pairs the SIMD dual-issues (SQ_ACTIVE_INST_VALU2: 5 % of this kernel's
+        # instructions) sharing a slot (profiles/inject_valu.json,
+        # tools/inject_summary.py).  The nominal 2-cycle rate -- every instruction
+        # paired -- is reported beside it, and valu_busy_pmc is the counters' own
+        # busy fraction: issue slots used / slots the launch had at its clock.
         nominal = 256 * 4 * 2.4e9 / 2
         if os.path.exists(args.inject_pmc_json):
             with open(args.inject_pmc_json) as f:
                 pmc = json.load(f)
             ipp = pmc["valu_insts_per_philox"]  # lane-instructions per Philox (SQ_INSTS_VALU x 64 / Philox)
             achieved = philox / (inj_ms * 1e-3) * ipp / 64  # wave-instructions per second
-            peak = pmc.get("mix_peak_wave_instr_per_s", nominal)
+            peak = pmc.get("issue_peak_wave_instr_per_s", nominal)
             res["roofline"] = {"bound": "valu", "achieved": achieved, "peak": peak,
                                "unit": "wave VALU instructions/s", "frac": achieved / peak,
-                               "peak_basis": "opcode mix of inject_kernel<int,24> at measured per-opcode issue cost",
+                               "peak_basis": pmc.get("peak_basis"),
+                               "dual_issue_frac": pmc.get("dual_issue_frac"),
                                "nominal_peak": nominal, "frac_of_nominal": achieved / nominal,
-                               "valu_insts_per_philox": ipp, "mix_cycles_per_wave_instr":
-                               pmc.get("mix_cycles_per_wave_instr"),
-                               "valu_busy_pmc": pmc.get("valu_busy"), "source": pmc.get("source")}
+                               "valu_insts_per_philox": ipp, "valu_busy_pmc": pmc.get("valu_busy"),
+                               "source": pmc.get("source")}
         return res
 
     inject = None if args.no_inject else optional("inject", inject_section)

@@ -1,14 +1,33 @@
-"""VALU roofline inputs of the injection kernels from rocprofv3 counter passes
-(tools/gpu_r05.sh, tools/inject_pmc.py) -> profiles/inject_valu.json.
+"""VALU roofline inputs of the injection kernels -> profiles/inject_valu.json.
 
-SQ_INSTS_VALU counts wave-level VALU instructions; a wave instruction covers
-64 lanes, so lane-instructions per Philox = SQ_INSTS_VALU * 64 / Philox per
-launch (Golay: M * 24, Hamming(8,4): V * 8).  SQ_ACTIVE_INST_VALU counts the
-quad-cycles in which a SIMD issued VALU work, so VALU-busy = 4 *
-SQ_ACTIVE_INST_VALU / (SIMDs * cycles of the launch), the cycles taken from the
-launch's kernel-trace duration at the 2.4 GHz shader clock.
+Counters (rocprofv3 --pmc passes of tools/inject_pmc.py and of the VALU
+microbenchmark tools/exp/run_valu_rate2.py, QUICK=1: tools/gpu_r06e.sh):
 
-usage: python tools/inject_summary.py gpurun_out/<tag> [profiles/<round>]"""
+  SQ_INSTS_VALU          wave-level VALU instructions issued
+  SQ_ACTIVE_INST_VALU2   quad-cycles in which a SIMD issued TWO VALU instructions
+                         (gfx950 dual issue)
+  SQ_BUSY_CYCLES         cycles with waves present, per shader engine (32 SEs):
+                         the launch's length in shader clocks, at the clock it ran
+
+A SIMD issues one wave64 VALU instruction per quad-cycle; some opcodes pair up
+(dual issue, two in one quad-cycle).  So the VALU issue slots a launch used are
+INSTS - VALU2, and the VALU-busy fraction is
+
+    (INSTS - VALU2) / (SIMDs * SQ_BUSY_CYCLES / SEs / 4)
+
+-- the counters and the launch's own clock, independent of the instruction count
+the roofline's `achieved` comes from.  (gfx950's SQ_ACTIVE_INST_VALU equals
+SQ_INSTS_VALU and SQ_THREAD_CYCLES_VALU equals 64 x SQ_INSTS_VALU for full waves:
+neither measures cycles; round 5's "valu_busy" was 2 x the issue fraction.)
+
+The peak the bench prices injection at is the issue-slot rate at the spec clock
+for the kernel's own pairing: SIMDs * 2.4e9 / 4 / (1 - VALU2/INSTS) wave-
+instructions per second.  The microbenchmark's pure single-opcode streams
+calibrate the busy fraction a VALU-only loop reaches (its loop's scalar
+instructions and the launch's ramp cost it ~10 %).
+
+usage: python tools/inject_summary.py gpurun_out/r06e [profiles/r06]
+"""
 import csv
 import glob
 import json
@@ -18,100 +37,88 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 M, V = 8 * 4096 * 32 * 43, 8 * 4096 * 32 * 128
-SIMDS, CLK = 256 * 4, 2.4e9
+SIMDS, SES, CLK = 256 * 4, 32, 2.4e9
 
 
-def rows(d):
-    out = []
+def dispatches(d):
+    """{dispatch id: {"name", counters..., "dur"}} of one rocprofv3 --pmc output directory."""
+    per = {}
     for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        out += list(csv.DictReader(open(p)))
-    return out
+        for r in csv.DictReader(open(p)):
+            e = per.setdefault(int(r["Dispatch_Id"]), {"name": r["Kernel_Name"]})
+            e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    for p in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(p)):
+            k = int(r["Dispatch_Id"])
+            if k in per:
+                per[k]["dur"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    return per
 
 
-KERNEL = "_ZN5kvecc13inject_kernelIiLi24ELb0ELb1EEEvPKT_PS1_PhNS_10InjectArgsEPm"  # inject_kernel<int, 24, false, true>
+def busy(e):
+    """VALU issue-slot busy fraction and the launch's clock from one dispatch's counters."""
+    cycles = e["SQ_BUSY_CYCLES"] / SES
+    slots = e["SQ_INSTS_VALU"] - e["SQ_ACTIVE_INST_VALU2"]
+    return slots / (SIMDS * cycles / 4), cycles / e["dur"] if e.get("dur") else None
 
 
-def isa_mix():
-    """Opcode shares of the Golay injection kernel's VALU instructions, from its
-    gfx950 disassembly (hipcc -S of csrc/inject.hip)."""
-    import collections
-    import subprocess
-    import tempfile
-    pkg = os.path.join(REPO, "quantized-kv-cache-ecc-protection_amd")
-    with tempfile.TemporaryDirectory() as t:
-        asm = os.path.join(t, "inject.s")
-        subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
-                               "-I" + os.path.join(REPO, "include"), "--cuda-device-only", "-S",
-                               os.path.join(pkg, "csrc", "inject.hip"), "-o", asm],
-                              stderr=subprocess.DEVNULL)
-        text = open(asm).read()
-    body = text[text.index(KERNEL + ":"):]
-    body = body[:body.index(".Lfunc_end")]
-    ops = collections.Counter(ln.split()[0].split("_e32")[0].split("_e64")[0]
-                              for ln in map(str.strip, body.splitlines()) if ln.startswith("v_"))
-    tot = sum(ops.values())
-    return {k: v / tot for k, v in ops.most_common()}
+def summarise(per, match):
+    es = [e for e in per.values() if match(e["name"]) and "SQ_ACTIVE_INST_VALU2" in e]
+    if not es:
+        return None
+    med = {c: statistics.median(e[c] for e in es) for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU2",
+                                                          "SQ_BUSY_CYCLES")}
+    b = [busy(e) for e in es]
+    return {"dispatches": len(es), "counters_median": med,
+            "dual_issue_frac": med["SQ_ACTIVE_INST_VALU2"] / med["SQ_INSTS_VALU"],
+            "valu_busy": statistics.median(x[0] for x in b),
+            "clock_hz": statistics.median(x[1] for x in b if x[1]),
+            "duration_s_under_pmc": statistics.median(e["dur"] for e in es if "dur" in e)}
 
 
-def mix_peak(mix, rates):
-    """Wave-instructions per second the chip issues for this opcode mix: every
-    opcode at its measured issue cost (tools/exp/run_valu_rate.py), opcodes
-    not measured at the 4-cycle cost of the 32-bit integer VOP3 ops."""
-    cyc = {k.split("(")[0]: v["cycles_per_wave_instr_per_simd"] for k, v in rates.items()}
-    per = sum(share * cyc.get(op, 4.15) for op, share in mix.items())
-    return SIMDS * CLK / per, per
+OPS = ["v_add_u32", "v_xor_b32", "v_mul_lo_u32", "v_mul_hi_u32", "v_lshlrev_b32", "v_add3_u32",
+       "v_bitop3_b32", "v_add_f32", "v_and_b32", "v_lshrrev_b32"]
 
 
 def main():
     src = sys.argv[1]
     dst = sys.argv[2] if len(sys.argv) > 2 else None
-    rates_path = os.path.join(REPO, "profiles", "r05", "valu_rate.json")
-    per = {}  # (dispatch id) -> {counter: value, name, dur}
-    for d in sorted(glob.glob(os.path.join(src, "inj_pmc*"))):
-        for r in rows(d):
-            if "inject" not in r["Kernel_Name"]:
-                continue
-            key = (os.path.basename(d), int(r["Dispatch_Id"]))
-            e = per.setdefault(key, {"name": r["Kernel_Name"]})
-            e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    trace = {}
-    for p in glob.glob(os.path.join(src, "inj_trace", "**", "*kernel_trace.csv"), recursive=True):
-        for r in csv.DictReader(open(p)):
-            if "inject" in r["Kernel_Name"]:
-                trace.setdefault(r["Kernel_Name"], []).append(
-                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-    res = {"source": f"{src} (rocprofv3 --pmc passes of tools/inject_pmc.py)", "kernels": {}}
-    for name in sorted({e["name"] for e in per.values()}):
-        es = [e for e in per.values() if e["name"] == name]
-        golay = "inject_kernel<int" in name
+    inj = dispatches(os.path.join(src, "inj_pmc3"))
+    res = {"source": f"{src}: rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CYCLES "
+                     "(+ SQ_THREAD_CYCLES_VALU) of tools/inject_pmc.py and tools/exp/run_valu_rate2.py",
+           "kernels": {}}
+    for name, golay in (("inject_kernel<int, 24, false, true>", True), ("inject_kernel<unsigned char, 8, false, true>", False)):
+        s = summarise(inj, lambda n, name=name: name in n)
+        if s is None:
+            continue
         philox = M * 24 if golay else V * 8
-        med = {c: statistics.median(e[c] for e in es if c in e)
-               for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES",
-                         "SQ_BUSY_CYCLES") if any(c in e for e in es)}
-        k = {"philox_per_launch": philox, "counters_median": med}
-        if "SQ_INSTS_VALU" in med:
-            k["valu_insts_per_philox"] = med["SQ_INSTS_VALU"] * 64 / philox
-        durs = [t for n, ts in trace.items() if n == name for t in ts]
-        if durs:
-            dur = statistics.median(durs)
-            k["duration_s"] = dur
-            if "SQ_ACTIVE_INST_VALU" in med:
-                k["valu_busy"] = 4 * med["SQ_ACTIVE_INST_VALU"] / (SIMDS * dur * CLK)
-            if "SQ_INSTS_VALU" in med:
-                k["valu_issue_frac"] = med["SQ_INSTS_VALU"] / dur / (SIMDS * CLK / 2)
-        res["kernels"][name.split("(")[0]] = k
-    gol = [k for n, k in res["kernels"].items() if "inject_kernel<int" in n]
-    if gol and "valu_insts_per_philox" in gol[0]:
-        res["valu_insts_per_philox"] = gol[0]["valu_insts_per_philox"]
-        res["valu_busy"] = gol[0].get("valu_busy")
-    if os.path.exists(rates_path):
-        mix = isa_mix()
-        peak, cyc = mix_peak(mix, json.load(open(rates_path)))
-        res["isa_mix"] = {k: round(v, 4) for k, v in mix.items() if v >= 0.002}
-        res["mix_cycles_per_wave_instr"] = cyc
-        res["mix_peak_wave_instr_per_s"] = peak
-        res["nominal_peak_wave_instr_per_s"] = SIMDS * CLK / 2
-        res["valu_rates"] = rates_path
+        s["philox_per_launch"] = philox
+        s["valu_insts_per_philox"] = s["counters_median"]["SQ_INSTS_VALU"] * 64 / philox
+        s["issue_peak_wave_instr_per_s"] = SIMDS * CLK / 4 / (1 - s["dual_issue_frac"])
+        res["kernels"][name] = s
+    gol = res["kernels"].get("inject_kernel<int, 24, false, true>")
+    if gol:
+        res.update({"valu_insts_per_philox": gol["valu_insts_per_philox"], "valu_busy": gol["valu_busy"],
+                    "dual_issue_frac": gol["dual_issue_frac"],
+                    "issue_peak_wave_instr_per_s": gol["issue_peak_wave_instr_per_s"],
+                    "nominal_peak_wave_instr_per_s": SIMDS * CLK / 2,
+                    "peak_basis": "one wave64 VALU instruction per quad-cycle per SIMD at 2.4 GHz, dual-issued "
+                                  "pairs (SQ_ACTIVE_INST_VALU2) sharing a slot; the nominal 2-cycle rate "
+                                  "assumes every instruction pairs"})
+    micro = dispatches(os.path.join(src, "valu_pmc3"))
+    cal = {}
+    for a in range(len(OPS)):
+        for b in range(len(OPS)):
+            tag = f"valu2_kernel<{a}, {b}, 16>"
+            s = summarise(micro, lambda n, tag=tag: tag in n)
+            if s:
+                cal[OPS[a] if a == b else f"{OPS[a]}+{OPS[b]}"] = {
+                    "dual_issue_frac": round(s["dual_issue_frac"], 4), "valu_busy": round(s["valu_busy"], 4),
+                    "clock_hz": s["clock_hz"]}
+    res["microbenchmark_W8_CH16"] = cal
+    rates = os.path.join(src, "valu_rate2.json")
+    if os.path.exists(rates):
+        res["chains_sweep"] = json.load(open(rates))["summary"]
     out = json.dumps(res, indent=1)
     print(out)
     if dst:
