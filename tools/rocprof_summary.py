@@ -1,5 +1,6 @@
-"""Round-5 evidence summary: every roofline figure in the bench line against the
-rocprofv3 kernel trace (and HBM counters) of the same bench.py command.
+"""Evidence summary: every roofline figure in the bench line against the
+rocprofv3 kernel trace (and HBM counters) of the same bench.py command
+(tools/gpu_session.sh steps bench, prof, pmc).
 
 The trace is taken WITHOUT name truncation, so template instances that share a
 kernel name (the int32 and packed fused Golay reads, interp_tile_kernel<false>
@@ -8,7 +9,7 @@ carries another configuration's average.  HBM traffic per launch = FETCH_SIZE
 x 2 (gfx950 tallies 128-B streaming reads at 64 B, MI355X_MICROARCH.md, HBM
 section) + WRITE_SIZE, each from its own --pmc pass.
 
-usage: python tools/r05_summary.py gpurun_out/<tag> profiles/r05/<name>
+usage: python tools/rocprof_summary.py gpurun_out/<tag> profiles/<round>/<name>
   expects <tag>/bench.log (the JSON line), <tag>/prof/*kernel_trace.csv and
   optionally <tag>/pmc_fetch, <tag>/pmc_write counter collections.
 """
