@@ -288,12 +288,17 @@ __global__ __launch_bounds__(kBlock) void shim_read_golay_kernel(ShimReadArgs a)
 //     161.7 -> 158.8 us, packed 147.6 -> 143.5 (interleaved A/B,
 //     profiles/r05/golay_read_ab3.log; 50 / 40 / 20 / 10 % 160.7 / 159.4 /
 //     159.2 / 158.9, 4 waves at 2 per CU 169.8).
-constexpr int kTileBlock = 512;                    // 8 waves per workgroup (byte-codec reads)
+constexpr int kTileBlock = 512;                    // rounds 3-5's 8-wave byte-codec reads (tools/exp forks)
 constexpr int kTileWaves = kTileBlock / kWave;
+// the byte-codec reads (plain and interpolating): 2-wave workgroups on a full
+// grid, one tile per wave; no dynamic LDS cap.  Plain H(8,4) -> fp16 at
+// [8,4096,32,128]: 137.9-138.8 us against 139.0-139.9 for 8-wave workgroups
+// capped at 4 per CU (profiles/r06/interp_read_ab_*.txt, "pl2" vs "plain")
+constexpr int kBytesReadWaves = 2;
 constexpr int kGolayTileBlock = 256;               // Golay read: 4 waves per workgroup
 constexpr int kGolayTileWaves = kGolayTileBlock / kWave;
 constexpr int kShimTilePerCu = 3;                  // Golay read: persistent grid
-constexpr int kShimBytesLdsPad = 16384;            // byte-codec reads: caps 4 workgroups per CU
+constexpr int kShimBytesLdsPad = 16384;            // rounds 3-5: capped the 8-wave reads at 4 per CU (tools/exp)
 constexpr uint32_t kShimReadStaticPct = 30;        // Golay read: static share of the dynamic-tail schedule
 constexpr int kTileStage = 2304;                   // LDS bytes per wave tile
 constexpr int kTileGroups = 4;                     // codeword groups per lane per tile (max)
@@ -603,9 +608,9 @@ __device__ __forceinline__ float byte_tile_issue(const ShimTileArgs &a, const Sh
 }
 
 template <typename TO, int CODEC, bool STATS>
-__global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kTileWaves][kTileStage];
-  __shared__ float scale_all[kTileWaves][kWave];  // row scales, staged like the rows
+__global__ __launch_bounds__(kBytesReadWaves * kWave) void shim_read_bytes_tiles_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kBytesReadWaves][kTileStage];
+  __shared__ float scale_all[kBytesReadWaves][kWave];  // row scales, staged like the rows
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
   uint8_t *stage = stage_all[wave];
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
     i2r[i] = f / (cpr * 16 / V);
     i2c[i] = f - i2r[i] * (cpr * 16 / V);
   }
-  const uint32_t gw = blockIdx.x * kTileWaves + wave;
+  const uint32_t gw = blockIdx.x * kBytesReadWaves + wave;
   if (gw >= a.units) return;
   const ShimTile t = shim_tile(a, gw);
   u32x4 w[kByteTileItems];
@@ -702,12 +707,11 @@ __global__ __launch_bounds__(kTileBlock) void shim_read_bytes_tiles_kernel(ShimT
 // 139.9 against 142.4 (profiles/r06/interp_read_ab_*.txt,
 // tools/exp/interp_read_exp.hip: 1 / 4 / 8 waves per workgroup 140.4 / 140.8
 // / 143.0 at 1e-3).
-constexpr int kInterpWaves = 2;  // waves per workgroup of the interpolating read
 
 template <typename TO, bool STATS>
-__global__ __launch_bounds__(kInterpWaves * kWave) void shim_read_h84_interp_kernel(ShimTileArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kInterpWaves][kTileStage];
-  __shared__ float scale_all[kInterpWaves][kWave];
+__global__ __launch_bounds__(kBytesReadWaves * kWave) void shim_read_h84_interp_kernel(ShimTileArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[kBytesReadWaves][kTileStage];
+  __shared__ float scale_all[kBytesReadWaves][kWave];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
   uint8_t *stage = stage_all[wave];
@@ -721,7 +725,7 @@ __global__ __launch_bounds__(kInterpWaves * kWave) void shim_read_h84_interp_ker
     ic[i] = f - ir[i] * cpr;
   }
   constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
-  const uint32_t gw = blockIdx.x * kInterpWaves + wave;
+  const uint32_t gw = blockIdx.x * kBytesReadWaves + wave;
   if (gw >= a.units) return;
   const ShimTile t = shim_tile(a, gw);
   u32x4 w[kByteTileItems];
@@ -911,27 +915,24 @@ static void launch_read_tiles(bool packed, const ShimTileArgs &a, hipStream_t st
     KVECC_LAUNCH((shim_read_golay_tiles_kernel<TO, false, false>), dim3(grid), dim3(kGolayTileBlock), pad, st, a);
 }
 
-// byte codecs: a full grid, one tile per wave; 16 KiB of dynamic LDS caps 4
-// workgroups per CU
+// byte codecs: a full grid, one tile per wave, 2-wave workgroups
 template <typename TO, int CODEC>
 static void launch_bytes_plain(const ShimTileArgs &a, hipStream_t st) {
-  const unsigned grid = (unsigned)cdiv(a.units, kTileWaves);
+  const unsigned grid = (unsigned)cdiv(a.units, kBytesReadWaves);
   if (a.stats)
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, true>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad, st,
-                 a);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, true>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
   else
-    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, false>), dim3(grid), dim3(kTileBlock), kShimBytesLdsPad,
-                 st, a);
+    KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, false>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
 }
 
 template <typename TO>
 static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
   if (codec == KVECC_CODEC_H84 && interp) {
-    const unsigned grid = (unsigned)cdiv(a.units, kInterpWaves);
+    const unsigned grid = (unsigned)cdiv(a.units, kBytesReadWaves);
     if (a.stats)
-      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true>), dim3(grid), dim3(kInterpWaves * kWave), 0, st, a);
+      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
     else
-      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false>), dim3(grid), dim3(kInterpWaves * kWave), 0, st, a);
+      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
   } else if (codec == KVECC_CODEC_H84) {
     launch_bytes_plain<TO, KVECC_CODEC_H84>(a, st);
   } else if (codec == KVECC_CODEC_H74) {

@@ -96,8 +96,8 @@ def test_hot_kernel_budgets(kernels, pattern, limit):
 SHIPPED = [
     # fused Golay read: 256 threads, 32 KiB tables + 4 x (2304 B tile + 256 B scales)
     (r"shim_read_golay_tiles_kernelI6__half", 256, 32768 + 4 * (2304 + 256)),
-    # fused byte-codec read: 512 threads, 8 x (2304 + 256) B (+16 KiB dynamic at launch)
-    (r"shim_read_bytes_tiles_kernelI6__half", 512, 8 * (2304 + 256)),
+    # fused byte-codec read: 128 threads (2 independent waves), 2 x (2304 + 256) B
+    (r"shim_read_bytes_tiles_kernelI6__half", 128, 2 * (2304 + 256)),
     # interpolating H(8,4) read: 128 threads (2 independent waves), 2 x (2304 + 256) B
     (r"shim_read_h84_interp_kernelI6__half", 128, 2 * (2304 + 256)),
     # packed Golay decode wave tiles: 512 threads, 24 KiB tables + 8 x 3 KiB stage

@@ -17,13 +17,13 @@
 namespace kvecc {
 namespace exp {
 
-template <typename TO, bool STATS, int WAVES, bool INTERP>
+template <typename TO, bool STATS, int WAVES, bool INTERP, int TPW = 1, bool PI = false, int LVL = 0, int N1 = 0,
+          int N2 = 0>
 __global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[WAVES][kTileStage];
-  __shared__ float scale_all[WAVES][kWave];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[WAVES][TPW][kTileStage];
+  __shared__ float scale_all[WAVES][TPW][kWave];
   const uint32_t wave = WAVES == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t lane = threadIdx.x % kWave;
-  uint8_t *stage = stage_all[wave];
   const uint32_t cpr = a.d / 16;
   const uint32_t items = a.tr * cpr;
   uint32_t ir[kByteTileItems], ic[kByteTileItems];
@@ -35,16 +35,30 @@ __global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
   }
   constexpr int V = kVpl<TO>, NI2 = kByteTileItems * 16 / V;
   const uint32_t gw = blockIdx.x * WAVES + wave;
-  if (gw >= a.units) return;
-  const ShimTile t = shim_tile(a, gw);
-  u32x4 w[kByteTileItems];
-  scale_all[wave][lane] = byte_tile_issue(a, t, lane, ir, ic, items, w);
+  if (gw * TPW >= a.units) return;
+  ShimTile tt_[TPW];
+  u32x4 ww_[TPW][kByteTileItems];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {  // every tile's loads first
+    if (gw * TPW + j < a.units) {
+      tt_[j] = shim_tile(a, gw * TPW + j);
+      scale_all[wave][j][lane] = byte_tile_issue(a, tt_[j], lane, ir, ic, items, ww_[j]);
+    } else {
+      tt_[j].rows = 0;
+    }
+  }
   uint32_t n1 = 0, n2 = 0;
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+  if (tt_[j].rows == 0 && gw * TPW + j >= a.units) break;
+  const ShimTile &t = tt_[j];
+  u32x4 (&w)[kByteTileItems] = ww_[j];
+  uint8_t *stage = stage_all[wave][j];
   bool dbl_any = false, dbl_top = false, dbl_bot = false;
   const uint32_t off0 = INTERP ? a.d : 0u;  // tile row r at stage row r + 1
 #pragma unroll
-  for (int i = 0; i < kByteTileItems; ++i) {
-    if (i * kWave >= (int)items) break;  // uniform
+  for (int i = 0; i < (N1 ? N1 : kByteTileItems); ++i) {
+    if (!N1 && i * kWave >= (int)items) break;  // uniform (N1: the host's fixed item count)
     const bool real = ir[i] < t.rows;
     uint32_t dd = 0;
     u32x4 d4;
@@ -69,9 +83,10 @@ __global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
     if (real) *reinterpret_cast<u32x4 *>(stage + off0 + ir[i] * a.d + 16 * ic[i]) = d4;
   }
   bool tile_dbl = false;
-  if (INTERP) tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
+  // LVL 2: never interpolate (wrong values: the structure's own cost)
+  if (INTERP && LVL < 2) tile_dbl = __builtin_amdgcn_ballot_w64(dbl_any) != 0;
   wave_lds_sync();
-  if (INTERP && tile_dbl) {  // wave-uniform
+  if (INTERP && tile_dbl && LVL == 0) {  // wave-uniform (LVL 1: no neighbour rows, wrong at tile edges)
     const bool need_top = __builtin_amdgcn_ballot_w64(dbl_top) != 0;
     const bool need_bot = __builtin_amdgcn_ballot_w64(dbl_bot) != 0;
     const bool below = lane >= cpr;
@@ -109,8 +124,8 @@ __global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
   auto phase2 = [&](auto interp_c) {
     constexpr bool IP = decltype(interp_c)::value;
 #pragma unroll
-    for (int i = 0; i < NI2; ++i) {
-      if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
+    for (int i = 0; i < (N2 ? N2 : NI2); ++i) {
+      if (!N2 && i * kWave >= (int)(items * 16 / V)) break;  // uniform (N2: fixed count, straight line)
       const uint32_t f = lane + kWave * i;
       const uint32_t rr = __umul24(f, m) >> 16, c = f - rr * per;
       const uint32_t r = min(rr, a.tr - 1);
@@ -119,7 +134,14 @@ __global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
 #pragma unroll
       for (int k = 0; k < V / 4; ++k) {
         const uint32_t v = reinterpret_cast<const uint32_t *>(row)[k];
-        if (IP) {
+        if (IP && PI) {  // neighbours read only by the lanes whose word holds a double
+          q[k] = v & 0x0F0F0F0Fu;
+          if (is_double((v >> 4) & 0x03030303u)) {
+            const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
+            const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
+            q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
+          }
+        } else if (IP) {
           const uint32_t up = reinterpret_cast<const uint32_t *>(row - a.d)[k];
           const uint32_t dn = reinterpret_cast<const uint32_t *>(row + a.d)[k];
           q[k] = interp_word(v & 0x0F0F0F0Fu, up & 0x0F0F0F0Fu, dn & 0x0F0F0F0Fu, (v >> 4) & 0x03030303u);
@@ -127,13 +149,14 @@ __global__ __launch_bounds__(WAVES * 64) void ipe_kernel(ShimTileArgs a) {
           q[k] = v & 0x0F0F0F0Fu;
         }
       }
-      tile_store(os, (rr * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][r], dead));
+      tile_store(os, (rr * a.d + V * c) * (uint32_t)sizeof(TO), dq16<TO>(q, scale_all[wave][j][r], dead));
     }
   };
   if (tile_dbl)
     phase2(std::integral_constant<bool, true>{});
   else
     phase2(std::integral_constant<bool, false>{});
+  }  // tiles of the wave
   if (STATS) {
     n1 = wave_sum(n1);
     n2 = wave_sum(n2);
@@ -180,17 +203,40 @@ EXP_API int kvecc_exp_ipe(int waves, int interp, int lds_pad, const void *k_cach
   a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
   hipStream_t st = as_stream(stream);
   const unsigned pad = (unsigned)lds_pad;
-#define IPE(W)                                                                                              \
-  case W:                                                                                                   \
+  // waves: W + 10 * (tiles per wave - 1)
+#define IPE(W, T)                                                                                           \
+  case W + 10 * (T - 1):                                                                                   \
     if (interp)                                                                                             \
-      KVECC_LAUNCH((exp::ipe_kernel<__half, true, W, true>), dim3((unsigned)cdiv(a.units, W)), dim3(W * 64), \
-                   pad, st, a);                                                                             \
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, W, true, T>), dim3((unsigned)cdiv(a.units, W * T)),       \
+                   dim3(W * 64), pad, st, a);                                                               \
     else                                                                                                    \
-      KVECC_LAUNCH((exp::ipe_kernel<__half, true, W, false>), dim3((unsigned)cdiv(a.units, W)), dim3(W * 64), \
-                   pad, st, a);                                                                             \
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, W, false, T>), dim3((unsigned)cdiv(a.units, W * T)),      \
+                   dim3(W * 64), pad, st, a);                                                               \
     break;
   switch (waves) {
-    IPE(1) IPE(2) IPE(4) IPE(8)
+    IPE(1, 1) IPE(2, 1) IPE(4, 1) IPE(8, 1) IPE(1, 2) IPE(2, 2) IPE(4, 2)
+    case 201:  // 2 waves, no neighbour rows (wrong at tile edges)
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, 2, true, 1, false, 1>), dim3((unsigned)cdiv(a.units, 2)),
+                   dim3(128), pad, st, a);
+      break;
+    case 202:  // 2 waves, never interpolating (wrong values)
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, 2, true, 1, false, 2>), dim3((unsigned)cdiv(a.units, 2)),
+                   dim3(128), pad, st, a);
+      break;
+    case 301:  // 2 waves, interpolating, fixed item counts (D = 128, 16-row tiles, fp16)
+    case 302:  // the same, plain
+      if (a.tr * (a.d / 16) != 2 * 64) return set_error(KVECC_EINVAL, "fixed item counts need 128 items");
+      if (waves == 301)
+        KVECC_LAUNCH((exp::ipe_kernel<__half, true, 2, true, 1, false, 0, 2, 4>), dim3((unsigned)cdiv(a.units, 2)),
+                     dim3(128), pad, st, a);
+      else
+        KVECC_LAUNCH((exp::ipe_kernel<__half, true, 2, false, 1, false, 0, 2, 4>), dim3((unsigned)cdiv(a.units, 2)),
+                     dim3(128), pad, st, a);
+      break;
+    case 102:  // 2 waves, per-item neighbour reads
+      KVECC_LAUNCH((exp::ipe_kernel<__half, true, 2, true, 1, true>), dim3((unsigned)cdiv(a.units, 2)), dim3(128),
+                   pad, st, a);
+      break;
     default: return set_error(KVECC_EINVAL, "waves");
   }
 #undef IPE

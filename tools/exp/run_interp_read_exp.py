@@ -56,7 +56,7 @@ def main():
             table.data_ptr()]
 
     def interp_of(r):
-        return r == "product" or r.startswith("ipe")
+        return r == "product" or (r.startswith("ipe") and not r.startswith("ipe302"))
 
     def call(r, ev=None):
         if ev is not None:
@@ -95,14 +95,19 @@ def main():
         same[r] = torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1]) and ops.read_stats(stats[r]) == ref[2]
     del refs
     times = {r: [] for r in runs}
+    block = int(os.environ.get("BLOCK", "1"))  # BLOCK > 1: bench-like blocks of launches per run
     for _ in range(ROUNDS):
         for r in runs:
-            ev = ops.kernel_timer(dev)
-            call(r, ev)
-            times[r].append(ev)
+            if block > 1:
+                for _ in range(100):
+                    call(r)
+            for _ in range(block):
+                ev = ops.kernel_timer(dev)
+                call(r, ev)
+                times[r].append(ev)
     torch.cuda.synchronize()
     nbytes = 2 * B * L * H * (D + 4 + 2 * D)
-    print(f"BER {BER}, {ROUNDS} rounds")
+    print(f"BER {BER}, {ROUNDS} rounds, blocks of {block}")
     for r in runs:
         us = [a.elapsed_time(b) * 1e3 for a, b in times[r]]
         med = statistics.median(us)

@@ -8,6 +8,7 @@
 # Steps
 #   test      the whole -m gpu suite              smoke    __graft_entry__.smoke()
 #   launch    tests/test_gpu_launch.py            bench    bench.py (every section)
+#   shimtest  the fused shim reads' tests, sweeps and fuzz   fused  bench.py --sections fused
 #   prof      rocprofv3 kernel trace + stats of bench.py (the roofline's kernel times)
 #   pmc       FETCH_SIZE / WRITE_SIZE passes of bench.py (traffic.json)
 #   injpmc    VALU counter passes of the injection + the VALU microbenchmark
@@ -58,6 +59,9 @@ for s in $STEPS; do
   case $s in
     test)    run pytest_gpu 1500 $PYT tests -m gpu -x -v ;;
     launch)  run pytest_launch 600 $PYT tests/test_gpu_launch.py -m gpu -x -v ;;
+    shimtest) run pytest_shim 900 $PYT tests/test_shim_read_batch.py tests/test_geometry_sweep.py tests/test_gpu_fuzz.py \
+               tests/test_shim.py tests/test_shim_fp16.py tests/test_sched_counters.py -m gpu -x -v ;;
+    fused)   run bench_fused 600 python bench.py --sections fused ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace -- \
