@@ -706,9 +706,14 @@ __global__ __launch_bounds__(kBytesReadWaves * kWave) void shim_read_bytes_tiles
 // through LDS words behind a start barrier; 1e-2: 184.8 against 190.1; BER 0:
 // 139.9 against 142.4 (profiles/r06/interp_read_ab_*.txt,
 // tools/exp/interp_read_exp.hip: 1 / 4 / 8 waves per workgroup 140.4 / 140.8
-// / 143.0 at 1e-3).
+// / 143.0 at 1e-3).  N1 > 0: the tile has exactly N1 * 64 phase-1 items (the
+// host checks), so both phases run a fixed item count with no per-item exit
+// test: the compiler then issues every item's LDS reads before the first wait
+// instead of one read-wait-store chain per item (140.0-140.7 against
+// 141.6-142.6 us at 1e-3; the plain read gains nothing from it,
+// profiles/r06/interp_read_fixed_*.txt).
 
-template <typename TO, bool STATS>
+template <typename TO, bool STATS, int N1 = 0>
 __global__ __launch_bounds__(kBytesReadWaves * kWave) void shim_read_h84_interp_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kBytesReadWaves][kTileStage];
   __shared__ float scale_all[kBytesReadWaves][kWave];
@@ -745,8 +750,8 @@ __global__ __launch_bounds__(kBytesReadWaves * kWave) void shim_read_h84_interp_
     return q | tt << 4;
   };
 #pragma unroll
-  for (int i = 0; i < kByteTileItems; ++i) {
-    if (i * kWave >= (int)items) break;  // uniform
+  for (int i = 0; i < (N1 ? N1 : kByteTileItems); ++i) {
+    if (!N1 && i * kWave >= (int)items) break;  // uniform (N1: the fixed count)
     // rows past the tile: no statistics, no doubles, no LDS store (it would
     // land on the row-below slot)
     if (ir[i] < t.rows) {
@@ -801,8 +806,8 @@ __global__ __launch_bounds__(kBytesReadWaves * kWave) void shim_read_h84_interp_
   auto phase2 = [&](auto interp_c) {
     constexpr bool IP = decltype(interp_c)::value;
 #pragma unroll
-    for (int i = 0; i < NI2; ++i) {
-      if (i * kWave >= (int)(items * 16 / V)) break;  // uniform
+    for (int i = 0; i < (N1 ? N1 * 16 / V : NI2); ++i) {
+      if (!N1 && i * kWave >= (int)(items * 16 / V)) break;  // uniform
       const uint32_t f = lane + kWave * i;
       const uint32_t rr = __umul24(f, m) >> 16, c = f - rr * per;
       const uint32_t r = min(rr, a.tr - 1);  // rows past the tile: stores dropped, reads in the tile
@@ -925,14 +930,26 @@ static void launch_bytes_plain(const ShimTileArgs &a, hipStream_t st) {
     KVECC_LAUNCH((shim_read_bytes_tiles_kernel<TO, CODEC, false>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
 }
 
+// the interpolating read with N1 fixed phase-1 items per lane (0: the generic count)
+template <typename TO, int N1>
+static void launch_interp_read(const ShimTileArgs &a, unsigned grid, hipStream_t st) {
+  if (a.stats)
+    KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true, N1>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
+  else
+    KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false, N1>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
+}
+
 template <typename TO>
 static void launch_bytes_tiles(int codec, int interp, const ShimTileArgs &a, hipStream_t st) {
   if (codec == KVECC_CODEC_H84 && interp) {
     const unsigned grid = (unsigned)cdiv(a.units, kBytesReadWaves);
-    if (a.stats)
-      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, true>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
+    const uint32_t items = a.tr * (a.d / 16);
+    if (items == 2 * kWave)  // e.g. head_dim 128 in 16-row tiles
+      launch_interp_read<TO, 2>(a, grid, st);
+    else if (items == kWave)  // e.g. head_dim 64 in 16-row tiles (GPT-2)
+      launch_interp_read<TO, 1>(a, grid, st);
     else
-      KVECC_LAUNCH((shim_read_h84_interp_kernel<TO, false>), dim3(grid), dim3(kBytesReadWaves * kWave), 0, st, a);
+      launch_interp_read<TO, 0>(a, grid, st);
   } else if (codec == KVECC_CODEC_H84) {
     launch_bytes_plain<TO, KVECC_CODEC_H84>(a, st);
   } else if (codec == KVECC_CODEC_H74) {
