@@ -366,7 +366,7 @@ struct TileItems {
 // t.rows, a missing block, a row's last group running into the next row)
 // loads return 0, which decodes to 0 with no error count; the overrun
 // codeword is masked out of the statistics and never reaches the output.
-template <bool PACKED>
+template <bool PACKED, int NG = 0>
 __device__ __forceinline__ void tile_issue(const ShimTileArgs &a, const ShimTile &t, uint32_t lane,
                                            const TileItems &it, u32x4 (&w)[kTileGroups], float &scale) {
   const bool live = t.row0 >= 0;
@@ -382,8 +382,8 @@ __device__ __forceinline__ void tile_issue(const ShimTileArgs &a, const ShimTile
   scale = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * lane, 0, 0));
   const uint32_t groups = a.tr * a.gpr;
 #pragma unroll
-  for (int i = 0; i < kTileGroups; ++i) {
-    if (i * kWave >= (int)groups) break;  // uniform
+  for (int i = 0; i < (NG ? NG : kTileGroups); ++i) {
+    if (!NG && i * kWave >= (int)groups) break;  // uniform (NG: the fixed count)
     const uint32_t off = it.r1[i] * a.rowb + (PACKED ? 12u : 16u) * it.q1[i];
     if (PACKED) {  // 4 three-byte codewords in 3 dwords
       const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, kTileAux);
@@ -428,7 +428,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_out(const ShimTileArgs &a
   return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)uni(t.rows * a.d * (uint32_t)sizeof(TO)), 0x00020000);
 }
 
-template <typename TO, bool STATS, bool PACKED>
+template <typename TO, bool STATS, bool PACKED, int NG = 0, int NCF = 0>
 __global__ __launch_bounds__(kGolayTileBlock) void shim_read_golay_tiles_kernel(ShimTileArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t tab[8192];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kGolayTileWaves][kTileStage];
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kGolayTileBlock) void shim_read_golay_tiles_kernel(
   ShimTile cur = shim_tile(a, u);
   u32x4 w[kTileGroups];
   float scale;
-  tile_issue<PACKED>(a, cur, lane, it, w, scale);
+  tile_issue<PACKED, NG>(a, cur, lane, it, w, scale);
   uint8_t *stage = stage_all[wave];
   const char *tb = reinterpret_cast<const char *>(tab);
   for (;;) {
@@ -497,8 +497,8 @@ __global__ __launch_bounds__(kGolayTileBlock) void shim_read_golay_tiles_kernel(
     // 3), summed over the lane's <= 16 codewords of the tile: no carry
     uint32_t cnt = 0;
 #pragma unroll
-    for (int i = 0; i < kTileGroups; ++i) {
-      if (i * kWave >= (int)groups) break;  // uniform
+    for (int i = 0; i < (NG ? NG : kTileGroups); ++i) {
+      if (!NG && i * kWave >= (int)groups) break;  // uniform
       const uint32_t q = it.q1[i];
       uint32_t sp[4];
 #pragma unroll
@@ -531,15 +531,15 @@ __global__ __launch_bounds__(kGolayTileBlock) void shim_read_golay_tiles_kernel(
     const bool more = u < a.units;
     if (more) {
       cur = shim_tile(a, u);
-      tile_issue<PACKED>(a, cur, lane, it, w, scale);
+      tile_issue<PACKED, NG>(a, cur, lane, it, w, scale);
     }
     // ---- phase 2: dequantize VPL values per lane, one 16-byte store each -------
     // (stores of rows past the tile fall outside its output descriptor: dropped)
     const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
     const bool dead = t.row0 < 0;
 #pragma unroll
-    for (int i = 0; i < NC; ++i) {
-      if (i * kWave >= (int)chunks) break;  // uniform
+    for (int i = 0; i < (NCF ? NCF : NC); ++i) {
+      if (!NCF && i * kWave >= (int)chunks) break;  // uniform (NCF: the fixed count)
       uint32_t r, l, o;
       if (kItemsInRegs) {
         r = it.r2[i];

@@ -143,3 +143,21 @@ def test_bench_strong_headline_two_ranks(gpu):
     slowest = max(p["elapsed_s"] for p in two["config"]["per_rank"])
     assert two["value"] == pytest.approx(total * 4 / slowest, rel=1e-6)
     assert two["decode_stats"] == one["decode_stats"]
+
+
+@pytest.mark.gpu
+def test_bench_under_torchrun_takes_the_launchers_world(gpu):
+    """The driver's form: torchrun starts the ranks; --gpus may be omitted (it
+    then comes from WORLD_SIZE) and nothing is spawned a second time."""
+    from kvecc import launch
+    port = launch.free_port()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--backend", "gloo", "--steps", "3", "--warmup", "1", "--roofline-samples", "1",
+                        "--sections", "montecarlo"],
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 2 and line["config"]["launcher"] == "external (torchrun)"
+    assert line["config"]["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert line["montecarlo"]["world"] == 2 and len(line["montecarlo"]["per_rank"]) == 2

@@ -516,3 +516,51 @@ __attribute__((visibility("default"))) int kvecc_exp_gread(int v, const void *k_
 }
 
 }  // extern "C"
+
+// the product's fused Golay read (persistent grid, its launch shape) with fixed
+// phase-1 / phase-2 item counts (ng, nc rounds per lane): no per-item exit test
+extern "C" __attribute__((visibility("default"))) int kvecc_exp_gread_fixed(
+    int ng, int nc, const void *k_cache, const void *v_cache, const float *k_scales, const float *v_scales,
+    const int32_t *table, int64_t tstride, int64_t batch, int64_t ctx, int64_t hkv, int64_t d, int64_t block_size,
+    int packed, void *k_out, void *v_out, uint64_t *stats, void *stream) {
+  using namespace kvecc;
+  ShimTileArgs a{};
+  a.cache[0] = k_cache;
+  a.cache[1] = v_cache;
+  a.scales[0] = k_scales;
+  a.scales[1] = v_scales;
+  a.out[0] = k_out;
+  a.out[1] = v_out;
+  a.table = table;
+  a.atab = golay_attn_table_dev();
+  a.stats = stats;
+  const int64_t g = (d + 2) / 3, gpr = cdiv(g, 4), lr = 12 * gpr;
+  a.tstride = (uint32_t)tstride;
+  a.hkv = (uint32_t)hkv;
+  a.d = (uint32_t)d;
+  a.g = (uint32_t)g;
+  a.layers = 1;
+  a.bs = (uint32_t)block_size;
+  a.layer = 0;
+  a.ctx = (uint32_t)ctx;
+  a.gpr = (uint32_t)gpr;
+  a.lr = (uint32_t)lr;
+  a.tr = (uint32_t)std::min<int64_t>({block_size, kTileStage / lr, (int64_t)kWave * kTileGroups / gpr,
+                                      (int64_t)kWave, (int64_t)kWave * kTileChunks / (d / 8)});
+  a.tpb = (uint32_t)cdiv(block_size, a.tr);
+  a.nlb = (uint32_t)cdiv(ctx, block_size);
+  a.units = (uint32_t)(2 * batch * hkv * a.nlb * a.tpb);
+  a.rowb = (uint32_t)(packed ? KVECC_GOLAY_PACKED_ROW(g) : 4 * g);
+  a.dyn = shim_dyn_slot(stream);
+  if ((int64_t)cdiv(a.tr * a.gpr, kWave) != ng || (int64_t)a.tr * (d / 8) != (int64_t)nc * kWave)
+    return set_error(KVECC_EINVAL, "fixed counts %d / %d do not match the tile", ng, nc);
+  const unsigned grid = tile_grid(a.units);
+  hipStream_t st = as_stream(stream);
+  if (ng == 3 && nc == 4 && !packed)
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<__half, true, false, 3, 4>), dim3(grid), dim3(kGolayTileBlock), 0, st, a);
+  else if (ng == 3 && nc == 4 && packed)
+    KVECC_LAUNCH((shim_read_golay_tiles_kernel<__half, true, true, 3, 4>), dim3(grid), dim3(kGolayTileBlock), 0, st, a);
+  else
+    return set_error(KVECC_EINVAL, "no instance for %d / %d", ng, nc);
+  return check_launch("exp_gread_fixed");
+}

@@ -61,6 +61,7 @@ def main():
     vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
     lib.kvecc_exp_gread.argtypes = [ci, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, ci, vp, vp, vp, ci, ci, vp]
     lib.kvecc_exp_gread.restype = ci
+    lib.kvecc_exp_gread_fixed.argtypes = [ci, ci, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, ci, vp, vp, vp, vp]
     prod = lib.kvecc_shim_read_batch
     prod.argtypes = _lib.SIGNATURES["kvecc_shim_read_batch"]
     prod.restype = ci
@@ -90,7 +91,12 @@ def main():
         def call(r, ev=None):
             if ev is not None:
                 tn(ev[0].cuda_event, ev[1].cuda_event)
-            if r == "product":
+            if r in ("fixed", "pk_fixed"):  # the product kernel, fixed item counts (3 / 4)
+                rc = lib.kvecc_exp_gread_fixed(3, 4, caches[0].data_ptr(), caches[1].data_ptr(), scales[0].data_ptr(),
+                                               scales[1].data_ptr(), table.data_ptr(), table.shape[1], B, L, H, D, bs,
+                                               int(packed), out[0].data_ptr(), out[1].data_ptr(),
+                                               stats[r].data_ptr(), stream)
+            elif r == "product":
                 rc = prod(caches[0].data_ptr(), caches[1].data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(),
                           table.data_ptr(), table.shape[1], B, L, H, D, 1, bs, 0, cid, 0,
                           out[0].data_ptr(), out[1].data_ptr(), ops._DT[torch.float16], stats[r].data_ptr(), stream)
