@@ -607,3 +607,92 @@ def test_count_ne_vs_torch(gpu, n, offset):
     st = ops.new_stats(gpu)
     ops.count_ne_into(a, b, st)
     assert ops.read_stats(st, 1)[0] == int((a != b).sum())
+
+
+# ---------------------------------------------------------------------------
+# Full BASELINE sizes anchored to the C oracle itself (not only to the host
+# backend, which shares codec_math.h with the kernels): the oracle is pinned to
+# the reference-generated golden vectors (tests/test_oracle.py).  The oracle is
+# single-threaded; the flat tensor is cut into shards that carry the full
+# tensor's global_n / offset0, run on 16 host threads (ctypes drops the GIL).
+# ---------------------------------------------------------------------------
+
+def _oracle_sharded(fn, arrays, n, parts=64, threads=16):
+    """fn(lo, hi) -> tuple of numpy outputs for elements [lo, hi); concatenated."""
+    from concurrent.futures import ThreadPoolExecutor
+    bounds = [(n * k // parts, n * (k + 1) // parts) for k in range(parts)]
+    with ThreadPoolExecutor(threads) as pool:
+        res = list(pool.map(lambda b: fn(*b), bounds))
+    return res
+
+
+def test_config2_full_size_vs_oracle(gpu, oracle):
+    """Config 2 at [8,4096,32,128]: H(8,4) encode -> inject(BER 1e-3, 8 bits, the
+    flat tensor's Philox stream) -> decode, HIP against the C oracle bit for bit."""
+    import numpy as np
+
+    import kvecc
+    g = torch.Generator().manual_seed(21)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), dtype=torch.uint8, generator=g)
+    n = x.numel()
+    xn = x.numpy().reshape(-1)
+    cw = kvecc.hamming84_encode(x.to(gpu))
+    noisy, st = kvecc.inject_bit_errors_triton(cw, 1e-3, 8, seed=42, return_stats=True)
+    dec, et, dst = kvecc.hamming84_decode(noisy, return_error_types=True)
+
+    def shard(lo, hi):
+        c = oracle.hamming84_encode(xn[lo:hi])
+        nz, _, s = oracle.inject(c, 1e-3, 8, 42, global_n=n, offset0=lo)
+        d, e, ds = oracle.hamming84_decode(nz)
+        return c, nz, s, d, e, ds
+
+    res = _oracle_sharded(shard, None, n)
+    cat = lambda k: np.concatenate([r[k] for r in res])  # noqa: E731
+    assert np.array_equal(cw.cpu().numpy().reshape(-1), cat(0))
+    assert np.array_equal(noisy.cpu().numpy().reshape(-1), cat(1))
+    assert st == tuple(sum(r[2][k] for r in res) for k in range(2))
+    assert np.array_equal(dec.cpu().numpy().reshape(-1), cat(3))
+    assert np.array_equal(et.cpu().numpy().reshape(-1), cat(4))
+    assert dst == tuple(sum(r[5][k] for r in res) for k in range(2)) and dst[0] > 0 and dst[1] > 0
+
+
+def test_config3_full_size_vs_oracle(gpu, oracle):
+    """Config 3 at [8,4096,32,128]: per-head padded Golay triplets (43 codewords
+    per head, M_h = 45,088,768) -> inject(BER 1e-2, 24 bits) -> decode, HIP
+    (the headline's kernels) against the C oracle bit for bit."""
+    import numpy as np
+
+    from kvecc import ops
+    g = torch.Generator().manual_seed(31)
+    x = torch.randint(0, 16, (8, 4096, 32, 128), dtype=torch.uint8, generator=g)
+    trip = torch.zeros(8, 4096, 32, 129, dtype=torch.uint8)
+    trip[..., :128] = x
+    trip = trip.view(-1, 3)
+    m = trip.shape[0]
+    tn = trip.numpy()
+    d_trip = trip.to(gpu)
+    cw = torch.empty(m, dtype=torch.int32, device=gpu)
+    ops.golay_encode_into(d_trip.view(-1), cw, m)
+    noisy = torch.empty_like(cw)
+    ist = ops.new_stats(gpu)
+    ops.inject_into(cw, noisy, 1e-2, 24, seed=42, stats=ist)
+    out = torch.empty(m * 3, dtype=torch.uint8, device=gpu)
+    cnt = torch.empty(m, dtype=torch.uint8, device=gpu)
+    dst = ops.new_stats(gpu)
+    ops.golay_decode_into(noisy, out, cnt, dst)
+
+    def shard(lo, hi):
+        c = oracle.golay_encode(tn[lo:hi])
+        nz, _, s = oracle.inject(c, 1e-2, 24, 42, global_n=m, offset0=lo)
+        t, k, ds = oracle.golay_decode(nz)
+        return c, nz, s, t, k, ds
+
+    res = _oracle_sharded(shard, None, m)
+    cat = lambda k: np.concatenate([r[k] for r in res])  # noqa: E731
+    assert np.array_equal(cw.cpu().numpy(), cat(0))
+    assert np.array_equal(noisy.cpu().numpy(), cat(1))
+    assert ops.read_stats(ist) == [sum(r[2][k] for r in res) for k in range(2)]
+    assert np.array_equal(out.cpu().numpy().reshape(-1, 3), cat(3))
+    assert np.array_equal(cnt.cpu().numpy(), cat(4))
+    exp = [sum(r[5][k] for r in res) for k in range(2)]
+    assert ops.read_stats(dst) == exp and exp[0] > 0 and exp[1] > 0
