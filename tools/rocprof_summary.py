@@ -28,15 +28,15 @@ import sys
 SECTIONS = {
     "roofline": ("golay_decode_kernel<true, true>", ("roofline", "bytes_per_launch"), ("kernel_ms", "decode")),
     "encode": ("golay_encode_kernel(", None, ("kernel_ms", "encode")),
-    "fused_golay_decode": ("shim_read_golay_tiles_kernel<__half, true, false>", ("fused_golay_decode", "bytes_per_launch"),
+    "fused_golay_decode": ("shim_read_golay_tiles_kernel<__half, true, false, 0, 0>", ("fused_golay_decode", "bytes_per_launch"),
                            ("fused_golay_decode", "kernel_ms")),
-    "fused_golay_decode.packed": ("shim_read_golay_tiles_kernel<__half, true, true>",
+    "fused_golay_decode.packed": ("shim_read_golay_tiles_kernel<__half, true, true, 0, 0>",
                                   ("fused_golay_decode", "packed", "bytes_per_launch"),
                                   ("fused_golay_decode", "packed", "kernel_ms")),
     "fused_h84.plain": ("shim_read_bytes_tiles_kernel<__half, 2, true>",
                         ("fused_golay_decode", "hamming84", "plain", "bytes_per_launch"),
                         ("fused_golay_decode", "hamming84", "plain", "kernel_ms")),
-    "fused_h84.interp": ("shim_read_h84_interp_kernel<__half, true>",
+    "fused_h84.interp": ("shim_read_h84_interp_kernel<__half, true, 2>",
                          ("fused_golay_decode", "hamming84", "interp", "bytes_per_launch"),
                          ("fused_golay_decode", "hamming84", "interp", "kernel_ms")),
     "golay_rows.decode": ("golay_decode_rows_reg_kernel<true", ("golay_rows", "bytes_per_launch"),
