@@ -12,6 +12,7 @@
 #   prof      rocprofv3 kernel trace + stats of bench.py (the roofline's kernel times)
 #   pmc       FETCH_SIZE / WRITE_SIZE passes of bench.py (traffic.json)
 #   injpmc    VALU counter passes of the injection + the VALU microbenchmark
+#   attnpmc   SQ counter pass (VALU, LDS, bank conflicts, waits) of MHA paged attention per codec
 #   valu      tools/exp/run_valu_rate2.py (issue cost vs chains / waves)
 #   configs   tools/bench_configs.py (every BASELINE config's kernels)
 #   shim      tools/bench_shim.py: config 4 eager, HIP graph, inductor; host backend
@@ -76,6 +77,11 @@ for s in $STEPS; do
                "$ROOT/tools/inject_pmc.py"
              QUICK=1 pmc valu_pmc3 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU SQ_BUSY_CYCLES -- \
                "$ROOT/tools/exp/run_valu_rate2.py" ;;
+    attnpmc) for c in golay golay_packed hamming84; do
+               pmc attnpmc_$c SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS \
+                 SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES -- "$ROOT/tools/bench_attention.py" --codec $c \
+                 --iters 20 --passes 1 --warmup 20 --warmup-s 0.1
+             done ;;
     valu)    run valu_rate2 300 python tools/exp/run_valu_rate2.py "$OUT/valu_rate2.json" ;;
     configs) run configs 900 python tools/bench_configs.py ;;
     shim)    run shim_compiled 900 python tools/bench_shim.py --bers 0 1e-3 1e-2 --graph --compile inductor
