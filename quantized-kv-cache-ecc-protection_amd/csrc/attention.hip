@@ -205,6 +205,14 @@ struct Chunk {
   // values before the row scale, (q - 8): H(8,4) through `lut` (LDS, byte ->
   // data(byte) - 8; double errors keep their data, :144-148), Golay through the
   // correction tables (uncorrectable words keep their data, as golay_decode)
+  // SP (Golay; instantiated only by tools/exp/attn_exp.hip): the parity half of
+  // the spread table as two 64-entry tables, p(lo) = T0[lo & 63] ^ T1[lo >> 6]
+  // (the entries are linear in lo), after the 4096-entry correction half: 16.5
+  // KiB of LDS instead of 32, conflict-free parity gathers, 2 more VALU per
+  // codeword.  Slower at every split and rows-in-flight count tried (MHA
+  // int32 75.0 vs 73.2 us, packed 65.2 vs 59.9; profiles/r06/attn/
+  // golay_split_parity_ab.txt): the kernel is bound by its VALU work
+  template <bool SP = false>
   __device__ __forceinline__ void decode(const h84_lut_t *lut, const uint32_t *gtab, float *v) const {
     if constexpr (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
@@ -220,9 +228,15 @@ struct Chunk {
         // holds the received parity -- so the syndrome's byte offset into the
         // correction half is ((w ^ P) & 0x3FFC000) >> 12: one v_bitop3
         // (0x28 = (S0 ^ S1) & S2) and a shift
-        const uint32_t p = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab) + (w[k] & 0x3FFCu));
+        const char *tb = reinterpret_cast<const char *>(gtab);
+        uint32_t p;
+        if (SP)
+          p = *reinterpret_cast<const uint32_t *>(tb + 16384 + (w[k] & 0xFCu)) ^
+              *reinterpret_cast<const uint32_t *>(tb + 16384 + 256 + ((w[k] >> 6) & 0xFCu));
+        else
+          p = *reinterpret_cast<const uint32_t *>(tb + (w[k] & 0x3FFCu));
         const uint32_t off = __builtin_amdgcn_bitop3_b32(w[k], p, 0x03FFC000u, 0x28) >> 12;
-        const uint32_t e = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gtab + 4096) + off);
+        const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + (SP ? 0 : 16384) + off);
         // corrected nibbles: (p ^ e) & 0xF0000F0F; the conversions are written
         // out because the compiler otherwise re-extracts each nibble with a
         // shift and a mask.  The third value comes out as 16 n (byte 3 = n << 4):
@@ -445,7 +459,7 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
 // loaded and decoded once and used G times (a dot product, an online softmax
 // state and an accumulator per head), where one workgroup per query head read
 // and decoded every cache row H/Hkv times.
-template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1, int UR = 0>
+template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1, int UR = 0, bool SP = false>
 __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
@@ -464,7 +478,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   // tables the block-table slice (before the copy) and the merge buffer (after
   // the loop) live in the same LDS, which keeps 4 workgroups per CU.
   constexpr bool kSpread = is_golay(CODEC);
-  constexpr int kTabWords = !is_golay(CODEC) ? 4 : kSpread ? 8192 : 4096;
+  constexpr int kTabWords = !is_golay(CODEC) ? 4 : SP ? 4096 + 128 : kSpread ? 8192 : 4096;
   static_assert(!kSpread || (TP * W * E <= kTabWords && kMaxSplit + 1 <= kTabWords), "LDS aliasing");
   __shared__ __attribute__((aligned(16))) uint32_t gtab[kTabWords];
   __shared__ float red_own[kSpread ? 1 : TP * W * E];  // per-group acc
@@ -526,7 +540,16 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       rows[i] = row;
     }
   }
-  if (kSpread) {
+  if (kSpread && SP) {
+    __syncthreads();  // blks (aliased) fully read
+    // the correction half, then T0[k] = P(k) and T1[k] = P(k << 6)
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab_x + 4096);
+    u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
+#pragma unroll
+    for (int i = threadIdx.x; i < 1024; i += kBlock) dst[i] = src[i];
+    if (threadIdx.x < 128)
+      gtab[4096 + threadIdx.x] = a.atab_x[threadIdx.x < 64 ? threadIdx.x : (threadIdx.x - 64) << 6];
+  } else if (kSpread) {
     __syncthreads();  // blks (aliased) fully read
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab_x);
     u32x4 *dst = reinterpret_cast<u32x4 *>(gtab);
@@ -632,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       for (int j = 0; j < G; ++j) part[j] = 0.0f;
       if (live) {
         float kv[E];
-        kc[u].decode(lut, gtab, kv);
+        kc[u].template decode<SP>(lut, gtab, kv);
 #pragma unroll
         for (int j = 0; j < G; ++j) {
           part[j] = dot<E>(qv[j], kv);
@@ -677,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         float vv[E];
-        vc[u].decode(lut, gtab, vv);
+        vc[u].template decode<SP>(lut, gtab, vv);
 #pragma unroll
         for (int j = 0; j < G; ++j) axpy<E>(acc[j], ps[j][u], vv);
       }

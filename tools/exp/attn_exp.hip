@@ -30,6 +30,17 @@ static void launch_mfma_g(int codec, const AttnArgs &a, int64_t batch, hipStream
 }  // namespace exp
 }  // namespace kvecc
 
+// Golay MHA split kernel (fp16 queries, G = 1, fused combine) with the parity
+// half as two 64-entry tables (sp = 1: 16.5 KiB of LDS instead of 32), u rows
+// in flight (0: the product's), per_cu workgroups per CU in the split choice
+template <int CODEC, int U, bool SP>
+static void launch_gsp(const kvecc::AttnArgs &a, dim3 grid, hipStream_t st) {
+  using namespace kvecc;
+  constexpr int VEC = CODEC == KVECC_CODEC_GOLAY ? kGolayVec : kGolayPackedVec;
+  KVECC_LAUNCH((paged_attn_split_kernel<__half, CODEC, VEC, 16, true, 1, U, SP>), grid, dim3(kBlock), 0, st, a);
+}
+
+
 extern "C" {
 
 // kvecc_paged_attention (fp16 queries, caches < 4 GiB) with the matrix-core
@@ -138,6 +149,58 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_packed(
     KVECC_LAUNCH((paged_attn_split_kernel<__half, KVECC_CODEC_GOLAY_PACKED, 4, 16, true, 1>), grid, dim3(kBlock), 0,
                  st, a);
   return check_launch("exp_paged_attention_packed");
+}
+
+
+__attribute__((visibility("default"))) int kvecc_exp_paged_attention_gsp(
+    int packed, int sp, int u, int per_cu, const void *query, const void *k_cache, const void *v_cache,
+    const int32_t *block_table, const int32_t *context_lens, const float *k_scales, const float *v_scales, void *out,
+    int64_t batch, int64_t heads, int64_t kv_heads, int64_t head_dim, int64_t num_blocks, int64_t block_size,
+    int64_t max_blocks, int64_t max_context_len, float sm_scale, float *workspace, void *stream) {
+  using namespace kvecc;
+  AttnArgs a;
+  a.q = query;
+  a.k_cache = k_cache;
+  a.v_cache = v_cache;
+  a.table = block_table;
+  a.ctx_lens = context_lens;
+  a.k_scales = k_scales;
+  a.v_scales = v_scales;
+  a.ws = workspace;
+  a.out = out;
+  a.heads = heads;
+  a.kv_heads = kv_heads;
+  a.d = head_dim;
+  a.g = (head_dim + 2) / 3;
+  a.rowb = (uint32_t)KVECC_GOLAY_PACKED_ROW(a.g);
+  a.layers = 1;
+  a.layer = 0;
+  a.bs = block_size;
+  a.max_blocks = max_blocks;
+  a.sm_scale = sm_scale;
+  a.empty_value = 0.0f;
+  const int64_t rows_total = num_blocks * kv_heads * block_size;
+  a.cache_bytes = (uint32_t)(rows_total * (packed ? (int64_t)a.rowb : 4 * a.g));
+  a.scale_bytes = (uint32_t)(rows_total * 4);
+  a.split = choose_split(batch * heads, max_context_len, per_cu);
+  a.nsplit = cdiv(max_context_len, a.split);
+  if (a.nsplit > kMaxSplits) return set_error(KVECC_EINVAL, "too many splits");
+  a.ctr = attn_counter_slot(stream);
+  a.par = golay_parity_table_dev();
+  a.cor = golay_correct_table_dev();
+  a.atab = golay_attn_table_dev();
+  a.atab_x = golay_attn_x_table_dev();
+  const dim3 grid((unsigned)a.nsplit, (unsigned)(batch * heads));
+  hipStream_t st = as_stream(stream);
+#define GSP(PK, UU, S)                                                                             \
+  if (packed == PK && u == UU && sp == S) {                                                        \
+    launch_gsp<PK ? KVECC_CODEC_GOLAY_PACKED : KVECC_CODEC_GOLAY, UU, S>(a, grid, st);            \
+    return check_launch("exp_paged_attention_gsp");                                                \
+  }
+  GSP(0, 0, false) GSP(0, 0, true) GSP(0, 3, true) GSP(0, 4, true) GSP(0, 3, false)
+  GSP(1, 0, false) GSP(1, 0, true) GSP(1, 2, true) GSP(1, 3, true)
+#undef GSP
+  return set_error(KVECC_EINVAL, "no gsp instance");
 }
 
 }  // extern "C"

@@ -40,6 +40,10 @@ def main():
     pk.argtypes = [ci, ci] + [vp] * 8 + [i64] * 8 + [f32, vp, vp]
     if sys.argv[1:] == ["packed_vec"]:
         return packed_vec(dev, pk)
+    if sys.argv[1:2] == ["gsp"]:
+        gsp = lib.kvecc_exp_paged_attention_gsp
+        gsp.argtypes = [ci, ci, ci, ci] + [vp] * 8 + [i64] * 8 + [f32, vp, vp]
+        return golay_split_parity(dev, gsp, sys.argv[2:] or ["golay", "golay_packed"])
     for codec in (sys.argv[1:] or ["hamming84", "golay_packed", "golay"]):
         for heads, kvh, variants in ((32, 32, VARIANTS), (32, 8, GQA_VARIANTS)):
             g = torch.Generator(device=dev).manual_seed(0)
@@ -97,6 +101,73 @@ def main():
                 print(f"{codec:13s} {heads}q/{kvh}kv {lab:20s} {res[lab]:7.2f} us/call  maxdiff {diff:.3g}",
                       flush=True)
             del kc, vc, ws
+
+
+def golay_split_parity(dev, gsp, codecs):
+    """Golay MHA split kernel: spread parity table (sp 0, the product) vs two
+    64-entry tables (sp 1), rows in flight (u, 0 = the product's), workgroups
+    per CU of the split choice; random cache words; bit-equal outputs expected
+    (same arithmetic)."""
+    heads = kvh = 32
+    for codec in codecs:
+        packed = codec == "golay_packed"
+        g = torch.Generator(device=dev).manual_seed(0)
+        nb = CTX // BS
+        blocks = B * nb
+        per = (D + 2) // 3
+        if packed:
+            per = (3 * per + 3) // 4 * 4
+        kc, vc = kv_cache_pair((blocks, 1, kvh, BS * per), torch.uint8 if packed else torch.int32, dev)
+        kc.random_(0, 256 if packed else 1 << 24, generator=g)
+        vc.copy_(kc.roll(1, 0))
+        ks = torch.rand(blocks, 1, kvh, BS, device=dev, generator=g)
+        vs = torch.rand_like(ks)
+        table = torch.randperm(blocks, device=dev, generator=g).to(torch.int32).view(B, nb)
+        lens = torch.full((B,), CTX, dtype=torch.int32, device=dev)
+        q = torch.randn(B, heads, D, device=dev, generator=g).half()
+        ws = torch.empty(B * heads * 64 * (D + 2), dtype=torch.float32, device=dev)
+        ref = torch.empty_like(q)
+        out = torch.empty_like(q)
+        s = torch.cuda.current_stream().cuda_stream
+        sm = 1 / math.sqrt(D)
+
+        def prod():
+            ops.paged_attention_into(q, kc, vc, table, lens, ks, vs, ref, 0, BS, sm, codec, CTX)
+
+        def var(sp, u, per_cu):
+            def run():
+                rc = gsp(int(packed), sp, u, per_cu, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), table.data_ptr(),
+                         lens.data_ptr(), ks.data_ptr(), vs.data_ptr(), out.data_ptr(), B, heads, kvh, D, blocks, BS,
+                         nb, CTX, sm, ws.data_ptr(), s)
+                assert rc == 0, rc
+            return run
+
+        cfgs = ([(0, 0, 4), (1, 0, 4), (1, 0, 8), (1, 3, 4), (1, 3, 8), (1, 4, 4), (1, 4, 8), (0, 3, 4)] if not packed
+                else [(0, 0, 4), (1, 0, 4), (1, 0, 8), (1, 2, 8), (1, 3, 4), (1, 3, 8)])
+        runs = [("product", prod)] + [(f"sp{a}_u{b}_cu{c}", var(a, b, c)) for a, b, c in cfgs]
+        res = {lab: [] for lab, _ in runs}
+        for _ in range(3):
+            for lab, run in runs:
+                for _ in range(100):
+                    run()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(ITERS):
+                    run()
+                e1.record()
+                torch.cuda.synchronize()
+                res[lab].append(e0.elapsed_time(e1) * 1e3 / ITERS)
+        prod()
+        torch.cuda.synchronize()
+        for lab, run in runs:
+            diff = 0.0
+            if lab != "product":
+                run()
+                torch.cuda.synchronize()
+                diff = float((out.float() - ref.float()).abs().max())
+            print(f"{codec:13s} {lab:16s} {min(res[lab]):7.2f} us/call (passes {', '.join(f'{x:.2f}' for x in res[lab])})"
+                  f"  maxdiff {diff:.3g}", flush=True)
+        del kc, vc, ws
 
 
 def packed_vec(dev, pk):
