@@ -33,11 +33,12 @@ static void launch_mfma_g(int codec, const AttnArgs &a, int64_t batch, hipStream
 // Golay MHA split kernel (fp16 queries, G = 1, fused combine) with the parity
 // half as two 64-entry tables (sp = 1: 16.5 KiB of LDS instead of 32), u rows
 // in flight (0: the product's), per_cu workgroups per CU in the split choice
-template <int CODEC, int U, bool SP>
+template <int CODEC, int U, bool SP, int VEC0 = 0>
 static void launch_gsp(const kvecc::AttnArgs &a, dim3 grid, hipStream_t st) {
   using namespace kvecc;
-  constexpr int VEC = CODEC == KVECC_CODEC_GOLAY ? kGolayVec : kGolayPackedVec;
-  KVECC_LAUNCH((paged_attn_split_kernel<__half, CODEC, VEC, 16, true, 1, U, SP>), grid, dim3(kBlock), 0, st, a);
+  constexpr int VEC = VEC0 ? VEC0 : CODEC == KVECC_CODEC_GOLAY ? kGolayVec : kGolayPackedVec;
+  constexpr int W = VEC == 6 ? 8 : 16;  // lanes per token row: 43 codewords / VEC, rounded up to a power of two
+  KVECC_LAUNCH((paged_attn_split_kernel<__half, CODEC, VEC, W, true, 1, U, SP>), grid, dim3(kBlock), 0, st, a);
 }
 
 
@@ -198,6 +199,13 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_gsp(
     return check_launch("exp_paged_attention_gsp");                                                \
   }
   GSP(0, 0, false) GSP(0, 0, true) GSP(0, 3, true) GSP(0, 4, true) GSP(0, 3, false)
+  // sp 2: 6 codewords per lane, 8 lanes per token row (int32), u rows in flight
+  if (packed == 0 && sp == 2) {
+    if (u == 1) launch_gsp<KVECC_CODEC_GOLAY, 1, false, 6>(a, grid, st);
+    else if (u == 2) launch_gsp<KVECC_CODEC_GOLAY, 2, false, 6>(a, grid, st);
+    else launch_gsp<KVECC_CODEC_GOLAY, 3, false, 6>(a, grid, st);
+    return check_launch("exp_paged_attention_gsp");
+  }
   GSP(1, 0, false) GSP(1, 0, true) GSP(1, 2, true) GSP(1, 3, true)
 #undef GSP
   return set_error(KVECC_EINVAL, "no gsp instance");

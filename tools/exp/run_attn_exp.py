@@ -142,8 +142,12 @@ def golay_split_parity(dev, gsp, codecs):
                 assert rc == 0, rc
             return run
 
-        cfgs = ([(0, 0, 4), (1, 0, 4), (1, 0, 8), (1, 3, 4), (1, 3, 8), (1, 4, 4), (1, 4, 8), (0, 3, 4)] if not packed
-                else [(0, 0, 4), (1, 0, 4), (1, 0, 8), (1, 2, 8), (1, 3, 4), (1, 3, 8)])
+        cfgs = os.environ.get("GSP_CFGS")  # "sp:u:cu,..." (sp 2: 6 codewords per lane, int32)
+        if cfgs:
+            cfgs = [tuple(int(x) for x in c.split(":")) for c in cfgs.split(",")]
+        else:
+            cfgs = ([(0, 0, 4), (1, 0, 4), (1, 0, 8), (1, 3, 4), (1, 3, 8), (1, 4, 4), (1, 4, 8), (0, 3, 4)]
+                    if not packed else [(0, 0, 4), (1, 0, 4), (1, 0, 8), (1, 2, 8), (1, 3, 4), (1, 3, 8)])
         runs = [("product", prod)] + [(f"sp{a}_u{b}_cu{c}", var(a, b, c)) for a, b, c in cfgs]
         res = {lab: [] for lab, _ in runs}
         for _ in range(3):
