@@ -15,10 +15,14 @@
 //   GATHER 0: the real table lookups; 1: lookups at lane-private, conflict-free
 //          addresses (same instruction count, WRONG values: attributes the LDS
 //          bank conflicts); 2: no lookups (WRONG values: the memory ceiling)
+//          3: split parity in LDS, the correction entry from the global table;
+//          4: uint16 tables (8.25 KiB); 5: the byte-class tables (5.1 KiB, below)
 //   SPLITP the parity half as two 64-entry tables (16.5 KiB of tables)
 //   PAD    extra bytes per staged row in the phase-2 tile
 //   BLOCK  threads per workgroup
 #include "../../quantized-kv-cache-ecc-protection_amd/csrc/shim.hip"
+
+#include <vector>
 
 namespace kvecc {
 namespace exp {
@@ -49,6 +53,54 @@ __device__ __forceinline__ ShimTile tile_at(const ShimTileArgs &a, uint32_t u) {
   return t;
 }
 
+// Byte-class Golay decoder (GATHER 5).  With the systematic generator [I | B]
+// (B symmetric, B B = I) an error (de, pe) of weight <= 3 has syndrome
+// s = B de ^ pe, and q = B s = de ^ B pe.  Either wt(pe) <= 1 and de = B (s ^ m)
+// with m = pe's data-side image (0 or one unit vector e_i, since B e_i is row
+// i of B and B (s ^ e_i) = q ^ B_i), or wt(de) <= 1 and de = m = 0 or e_i.  So
+// one byte per syndrome -- idx (bits 0-3; 15: none), flag (bit 4: de = B (s ^
+// e_idx), else de = e_idx) and the count n (bits 5-7: 0-3, 4 = uncorrectable,
+// which keeps the data) -- plus linear pieces: spread(B (s ^ e_i)) =
+// spread(B s) ^ spread(B_i) and spread(B s) from two 64-entry tables.
+// Words: [0, 64) T0[i] = spread(i) | par(i) << 20, [64, 128) T1 for i << 6,
+// [128, 192) U0[i] = spread(par(i)), [192, 256) U1 for i << 6, [256, 288)
+// K[flag << 4 | idx] = spread(flag ? B_idx : e_idx) (0 past idx 11), then the
+// 4096 class bytes.
+constexpr int kBcBytes = 288;  // word offset of the class bytes
+constexpr int kBcWords = kBcBytes + 1024;
+constexpr int kBcAlloc = 1536;  // 6 KiB: whole 1 KiB LDS-DMA chunks (STAGE 2)
+
+static void bc_tables(uint32_t *t) {
+  auto sp = [](uint32_t d) { return golay_spread(d & 0xFFFu); };
+  for (uint32_t i = 0; i < 64; ++i) {
+    t[i] = sp(i) | golay_parity12(i) << 20;
+    t[64 + i] = sp(i << 6) | golay_parity12(i << 6) << 20;
+    t[128 + i] = sp(golay_parity12(i));
+    t[192 + i] = sp(golay_parity12(i << 6));
+  }
+  for (uint32_t k = 0; k < 32; ++k) {
+    const uint32_t idx = k & 15u, flag = k >> 4;
+    t[256 + k] = idx < 12 ? sp(flag ? golay_parity12(1u << idx) : 1u << idx) : 0u;
+  }
+  uint8_t *c = reinterpret_cast<uint8_t *>(t + kBcBytes);
+  for (int s = 0; s < 4096; ++s) c[s] = 0x80 | 0x0F;  // uncorrectable: n = 4, de = 0
+  // coset leaders of weight <= 3 (unique: minimum distance 8)
+  for (uint32_t e = 0; e < (1u << 24); ++e) {
+    const int w = __builtin_popcount(e);
+    if (w > 3) continue;
+    const uint32_t de = e & 0xFFFu, pe = e >> 12;
+    const uint32_t s = golay_parity12(de) ^ pe;
+    uint32_t code = 0xFFu;
+    for (uint32_t flag = 0; flag < 2 && code == 0xFFu; ++flag)
+      for (uint32_t idx = 0; idx < 16 && code == 0xFFu; ++idx) {
+        if (idx >= 12 && idx < 15) continue;
+        const uint32_t m = idx < 12 ? 1u << idx : 0u;
+        if ((flag ? golay_parity12(s ^ m) : m) == de) code = idx | flag << 4 | (uint32_t)w << 5;
+      }
+    c[s] = (uint8_t)code;
+  }
+}
+
 template <int SCHED, int CHUNK, int STAGE, int GATHER, int SPLITP, int PAD, int BLOCK, bool PACKED, int PCT = 65,
           int ORDER = 0>
 __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, const uint16_t *par16,
@@ -59,7 +111,8 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
   // from the global table (16 KiB, cache-resident; ~79 % of lanes read entry 0)
   // GATHER 4: uint16 tables, 8.25 KiB: split parity (12 bits) and the correction
   // (data error | count << 12); the nibbles are spread by VALU
-  constexpr int kTab = GATHER == 3 ? 128 : GATHER == 4 ? (128 + 4096) / 2 : SPLITP ? 128 + 4096 : 8192;
+  // GATHER 5: the byte-class decoder (bc_tables below), 5.1 KiB
+  constexpr int kTab = GATHER == 5 ? kBcAlloc : GATHER == 3 ? 128 : GATHER == 4 ? (128 + 4096) / 2 : SPLITP ? 128 + 4096 : 8192;
   __shared__ __attribute__((aligned(16))) uint32_t tab[kTab];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[kW][kTileStage];
   __shared__ float scale_all[kW][kWave];
@@ -97,8 +150,15 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
   auto stage_tables = [&]() {
     if (STAGE == 2) {
       // LDS-DMA: each wave-instruction writes 1 KiB (lane l at base + 16 l)
-      const char *src = reinterpret_cast<const char *>(a.atab);
-      if (SPLITP) {
+      const char *src = reinterpret_cast<const char *>(GATHER == 5 ? reinterpret_cast<const void *>(par16) : a.atab);
+      if (GATHER == 5) {
+        for (int c = wave; c < kBcAlloc / 256; c += kW)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 1024 * c + 16 * lane),
+                                           reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                               reinterpret_cast<uintptr_t>(tab) + 1024 * c),
+                                           16, 0, 0);
+        return;
+      } else if (SPLITP) {
         // parity pieces are gathers (entries i and i << 6): plain copy below
       } else {
         for (int c = wave; c < 32; c += kW)
@@ -109,7 +169,11 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
         return;
       }
     }
-    if (GATHER == 4) {
+    if (GATHER == 5) {
+      const u32x4 *s4 = reinterpret_cast<const u32x4 *>(par16);
+      u32x4 *d4 = reinterpret_cast<u32x4 *>(tab);
+      for (int i = threadIdx.x; i < kBcWords / 4; i += BLOCK) d4[i] = s4[i];
+    } else if (GATHER == 4) {
       uint16_t *t16 = reinterpret_cast<uint16_t *>(tab);
       for (int i = threadIdx.x; i < 128; i += BLOCK) t16[i] = par16[i < 64 ? i : (i - 64) << 6];
       const u32x4 *s4 = reinterpret_cast<const u32x4 *>(cor16);
@@ -154,7 +218,7 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.atab + 4096), 0, 16384, 0x00020000);
   for (;;) {
     scale_all[wave][lane] = scale;
-    uint32_t cnt = 0;
+    uint32_t cnt = 0, bc_tot = 0, bc_unc = 0;
 #pragma unroll
     for (int i = 0; i < kTileGroups; ++i) {
       if (i * kWave >= (int)groups) break;
@@ -167,7 +231,21 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
         if (c > 0) cw = 4 * q + c < a.g ? cw : 0u;
         const char *tb = reinterpret_cast<const char *>(tab);
         uint32_t p, e;
-        if (GATHER == 4) {
+        if (GATHER == 5) {
+          // p: spread(lo) | parity(lo) << 20; s: syndrome; us: spread(B s);
+          // b: the syndrome's class byte; de = flag ? B (s ^ m) : m, spread
+          const uint8_t *c8 = reinterpret_cast<const uint8_t *>(tab + kBcBytes);
+          const uint32_t p = tab[cw & 63u] ^ tab[64 + ((cw >> 6) & 63u)];
+          const uint32_t s = ((cw >> 12) ^ (p >> 20)) & 0xFFFu;
+          const uint32_t us = tab[128 + (s & 63u)] ^ tab[192 + (s >> 6)];
+          const uint32_t b = c8[s];
+          const uint32_t k = tab[256 + (b & 31u)];
+          const uint32_t mask = (uint32_t)__builtin_amdgcn_sbfe((int)b, 4, 1);
+          sp[c4] = __builtin_amdgcn_bitop3_b32(p, (mask & us) ^ k, 0x000F0F0Fu, 0x28);
+          bc_tot += b >> 5;  // n: 0-3 bits corrected, 4 uncorrectable
+          bc_unc += b >> 7;
+          continue;
+        } else if (GATHER == 4) {
           const uint16_t *t16 = reinterpret_cast<const uint16_t *>(tab);
           const uint32_t par = (uint32_t)t16[cw & 63u] ^ (uint32_t)t16[64 + ((cw >> 6) & 63u)];
           const uint32_t c = t16[128 + (((cw >> 12) ^ par) & 0xFFFu)];  // error | count << 12
@@ -205,8 +283,8 @@ __global__ __launch_bounds__(BLOCK) void golay_read_exp_kernel(ShimTileArgs a, c
         dst[2] = sp[2] >> 16 | sp[3] << 8;
       }
     }
-    bits += cnt & 63u;
-    unc += cnt >> 6;
+    bits += (cnt & 63u) + bc_tot - 4u * bc_unc;
+    unc += (cnt >> 6) + bc_unc;
     wave_lds_sync();
     const ShimTile t = cur;
     u = SCHED == 0 ? sched.next(u, lane) : u + 1;
@@ -366,6 +444,7 @@ struct Variant {
   const char *name;
   void (*kern)(ShimTileArgs, const uint16_t *, const uint16_t *);
   int sched, chunk, block;
+  int bc;  // passes the byte-class tables (GATHER 5)
 };
 
 #define GV(NAME, S, C, ST, G, SP, PD, B, PK) \
@@ -447,6 +526,20 @@ static const Variant kVariants[] = {
     {"full1_u16_hm", golay_read_exp_kernel<1, 1, 0, 4, 0, 0, 512, false, 65, 1>, 1, 1, 512},
     {"full2_u16_hm", golay_read_exp_kernel<1, 2, 0, 4, 0, 0, 512, false, 65, 1>, 1, 2, 512},
     {"pk_pers_hm", golay_read_exp_kernel<0, 1, 0, 0, 0, 0, 512, true, 65, 1>, 0, 1, 512},
+    // byte-class decoder (5.1 KiB of tables): full grids and the product's persistent shape
+    {"full1_bc", golay_read_exp_kernel<1, 1, 0, 5, 0, 0, 512, false>, 1, 1, 512, 1},
+    {"full2_bc", golay_read_exp_kernel<1, 2, 0, 5, 0, 0, 512, false>, 1, 2, 512, 1},
+    {"full1_bc_b256", golay_read_exp_kernel<1, 1, 0, 5, 0, 0, 256, false>, 1, 1, 256, 1},
+    {"full2_bc_b256", golay_read_exp_kernel<1, 2, 0, 5, 0, 0, 256, false>, 1, 2, 256, 1},
+    {"full1_bc_s1", golay_read_exp_kernel<1, 1, 1, 5, 0, 0, 512, false>, 1, 1, 512, 1},
+    {"full1_bc_glds", golay_read_exp_kernel<1, 1, 2, 5, 0, 0, 512, false>, 1, 1, 512, 1},
+    {"full2_bc_glds", golay_read_exp_kernel<1, 2, 2, 5, 0, 0, 512, false>, 1, 2, 512, 1},
+    {"full1_bc_b1024", golay_read_exp_kernel<1, 1, 0, 5, 0, 0, 1024, false>, 1, 1, 1024, 1},
+    {"full1_bc_glds_b1024", golay_read_exp_kernel<1, 1, 2, 5, 0, 0, 1024, false>, 1, 1, 1024, 1},
+    {"pers_bc_b256_p30", golay_read_exp_kernel<0, 1, 0, 5, 0, 0, 256, false, 30>, 0, 1, 256, 1},
+    {"pk_full1_bc", golay_read_exp_kernel<1, 1, 0, 5, 0, 0, 512, true>, 1, 1, 512, 1},
+    {"pk_full2_bc", golay_read_exp_kernel<1, 2, 0, 5, 0, 0, 512, true>, 1, 2, 512, 1},
+    {"pk_pers_bc_b256_p30", golay_read_exp_kernel<0, 1, 0, 5, 0, 0, 256, true, 30>, 0, 1, 256, 1},
     {"pf2", golay_read_pf2_kernel<512, false, 65>, 0, 1, 512},
     {"pf2_b256", golay_read_pf2_kernel<256, false, 65>, 0, 1, 256},
     {"pf2_p50", golay_read_pf2_kernel<512, false, 50>, 0, 1, 512},
@@ -510,8 +603,20 @@ __attribute__((visibility("default"))) int kvecc_exp_gread(int v, const void *k_
     grid = (unsigned)std::min<int64_t>(cdiv(a.units, kw), (int64_t)cu_count() * per_cu);
   else
     grid = (unsigned)cdiv(cdiv(a.units, var.chunk), kw);
-  KVECC_LAUNCH(var.kern, dim3(grid), dim3(var.block), (unsigned)lds_pad, as_stream(stream), a,
-               golay_parity_table_dev(), golay_correct_table_dev());
+  const uint16_t *t0 = golay_parity_table_dev();
+  if (var.bc) {
+    static uint32_t *bc_dev = nullptr;
+    if (!bc_dev) {
+      std::vector<uint32_t> h(exp::kBcAlloc, 0u);
+      exp::bc_tables(h.data());
+      if (hipMalloc(&bc_dev, sizeof(uint32_t) * h.size()) != hipSuccess ||
+          hipMemcpy(bc_dev, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return set_error(KVECC_EHIP, "exp_gread: byte-class tables");
+    }
+    t0 = reinterpret_cast<const uint16_t *>(bc_dev);
+  }
+  KVECC_LAUNCH(var.kern, dim3(grid), dim3(var.block), (unsigned)lds_pad, as_stream(stream), a, t0,
+               golay_correct_table_dev());
   return check_launch("exp_gread");
 }
 
