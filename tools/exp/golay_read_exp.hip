@@ -24,6 +24,8 @@
 
 #include <vector>
 
+#include "golay_bc.h"
+
 namespace kvecc {
 namespace exp {
 
@@ -51,54 +53,6 @@ __device__ __forceinline__ ShimTile tile_at(const ShimTileArgs &a, uint32_t u) {
   const int32_t blk = ld_scalar(a.table + (int64_t)b * a.tstride + lb);
   t.row0 = blk < 0 ? -1 : (((int64_t)blk * a.layers + a.layer) * a.hkv + h) * a.bs + ch * a.tr;
   return t;
-}
-
-// Byte-class Golay decoder (GATHER 5).  With the systematic generator [I | B]
-// (B symmetric, B B = I) an error (de, pe) of weight <= 3 has syndrome
-// s = B de ^ pe, and q = B s = de ^ B pe.  Either wt(pe) <= 1 and de = B (s ^ m)
-// with m = pe's data-side image (0 or one unit vector e_i, since B e_i is row
-// i of B and B (s ^ e_i) = q ^ B_i), or wt(de) <= 1 and de = m = 0 or e_i.  So
-// one byte per syndrome -- idx (bits 0-3; 15: none), flag (bit 4: de = B (s ^
-// e_idx), else de = e_idx) and the count n (bits 5-7: 0-3, 4 = uncorrectable,
-// which keeps the data) -- plus linear pieces: spread(B (s ^ e_i)) =
-// spread(B s) ^ spread(B_i) and spread(B s) from two 64-entry tables.
-// Words: [0, 64) T0[i] = spread(i) | par(i) << 20, [64, 128) T1 for i << 6,
-// [128, 192) U0[i] = spread(par(i)), [192, 256) U1 for i << 6, [256, 288)
-// K[flag << 4 | idx] = spread(flag ? B_idx : e_idx) (0 past idx 11), then the
-// 4096 class bytes.
-constexpr int kBcBytes = 288;  // word offset of the class bytes
-constexpr int kBcWords = kBcBytes + 1024;
-constexpr int kBcAlloc = 1536;  // 6 KiB: whole 1 KiB LDS-DMA chunks (STAGE 2)
-
-static void bc_tables(uint32_t *t) {
-  auto sp = [](uint32_t d) { return golay_spread(d & 0xFFFu); };
-  for (uint32_t i = 0; i < 64; ++i) {
-    t[i] = sp(i) | golay_parity12(i) << 20;
-    t[64 + i] = sp(i << 6) | golay_parity12(i << 6) << 20;
-    t[128 + i] = sp(golay_parity12(i));
-    t[192 + i] = sp(golay_parity12(i << 6));
-  }
-  for (uint32_t k = 0; k < 32; ++k) {
-    const uint32_t idx = k & 15u, flag = k >> 4;
-    t[256 + k] = idx < 12 ? sp(flag ? golay_parity12(1u << idx) : 1u << idx) : 0u;
-  }
-  uint8_t *c = reinterpret_cast<uint8_t *>(t + kBcBytes);
-  for (int s = 0; s < 4096; ++s) c[s] = 0x80 | 0x0F;  // uncorrectable: n = 4, de = 0
-  // coset leaders of weight <= 3 (unique: minimum distance 8)
-  for (uint32_t e = 0; e < (1u << 24); ++e) {
-    const int w = __builtin_popcount(e);
-    if (w > 3) continue;
-    const uint32_t de = e & 0xFFFu, pe = e >> 12;
-    const uint32_t s = golay_parity12(de) ^ pe;
-    uint32_t code = 0xFFu;
-    for (uint32_t flag = 0; flag < 2 && code == 0xFFu; ++flag)
-      for (uint32_t idx = 0; idx < 16 && code == 0xFFu; ++idx) {
-        if (idx >= 12 && idx < 15) continue;
-        const uint32_t m = idx < 12 ? 1u << idx : 0u;
-        if ((flag ? golay_parity12(s ^ m) : m) == de) code = idx | flag << 4 | (uint32_t)w << 5;
-      }
-    c[s] = (uint8_t)code;
-  }
 }
 
 template <int SCHED, int CHUNK, int STAGE, int GATHER, int SPLITP, int PAD, int BLOCK, bool PACKED, int PCT = 65,
@@ -605,15 +559,8 @@ __attribute__((visibility("default"))) int kvecc_exp_gread(int v, const void *k_
     grid = (unsigned)cdiv(cdiv(a.units, var.chunk), kw);
   const uint16_t *t0 = golay_parity_table_dev();
   if (var.bc) {
-    static uint32_t *bc_dev = nullptr;
-    if (!bc_dev) {
-      std::vector<uint32_t> h(exp::kBcAlloc, 0u);
-      exp::bc_tables(h.data());
-      if (hipMalloc(&bc_dev, sizeof(uint32_t) * h.size()) != hipSuccess ||
-          hipMemcpy(bc_dev, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice) != hipSuccess)
-        return set_error(KVECC_EHIP, "exp_gread: byte-class tables");
-    }
-    t0 = reinterpret_cast<const uint16_t *>(bc_dev);
+    t0 = reinterpret_cast<const uint16_t *>(exp::bc_tables_dev());
+    if (!t0) return set_error(KVECC_EHIP, "exp_gread: byte-class tables");
   }
   KVECC_LAUNCH(var.kern, dim3(grid), dim3(var.block), (unsigned)lds_pad, as_stream(stream), a, t0,
                golay_correct_table_dev());
