@@ -57,12 +57,25 @@ __device__ __forceinline__ void load_tables(uint16_t *lds, const uint16_t *__res
 // triplet packing / unpacking and the table decode: codec_math.h
 // ---- encode -------------------------------------------------------------------
 
+// Codewords past the last whole tile (m - ntiles * tile < tile of them) are
+// encoded / decoded one per thread by the first workgroups, before their
+// tiles: no tail launch (flat M_f = 44,739,243 codewords leaves 2,731; the
+// separate tail kernel cost ~2 us of launch per call)
 __global__ __launch_bounds__(kEncBlock) void golay_encode_kernel(const uint32_t *__restrict__ trip,
                                                                  u32x4 *__restrict__ cw,
-                                                                 int64_t ntiles,
+                                                                 int64_t ntiles, int64_t m,
                                                                  const uint16_t *__restrict__ par) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[4096];
   load_tables<kEncBlock>(lds, par, nullptr, false);
+  {
+    const uint8_t *t8 = reinterpret_cast<const uint8_t *>(trip);
+    int32_t *c32 = reinterpret_cast<int32_t *>(cw);
+    for (int64_t i = ntiles * kEncTile + (int64_t)blockIdx.x * kEncBlock + threadIdx.x; i < m;
+         i += (int64_t)gridDim.x * kEncBlock) {
+      const uint32_t d = golay_pack(t8[3 * i], t8[3 * i + 1], t8[3 * i + 2]);
+      c32[i] = (int32_t)(d | (uint32_t)lds[d] << 12);
+    }
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -114,7 +127,7 @@ template <bool WITH_COUNTS, bool WITH_STATS>
 __global__ __launch_bounds__(kDecBlock) void golay_decode_kernel(const u32x4 *__restrict__ cw,
                                                                  uint32_t *__restrict__ trip,
                                                                  uint32_t *__restrict__ counts,
-                                                                 int64_t ntiles,
+                                                                 int64_t ntiles, int64_t m,
                                                                  const uint16_t *__restrict__ par,
                                                                  const uint16_t *__restrict__ cor,
                                                                  uint64_t *__restrict__ stats) {
@@ -123,6 +136,24 @@ __global__ __launch_bounds__(kDecBlock) void golay_decode_kernel(const u32x4 *__
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   uint32_t bits = 0, unc = 0;
+  {  // the tail (see golay_encode_kernel)
+    const int32_t *c32 = reinterpret_cast<const int32_t *>(cw);
+    uint8_t *t8 = reinterpret_cast<uint8_t *>(trip);
+    uint8_t *n8 = reinterpret_cast<uint8_t *>(counts);
+    for (int64_t i = ntiles * kDecTile + (int64_t)blockIdx.x * kDecBlock + threadIdx.x; i < m;
+         i += (int64_t)gridDim.x * kDecBlock) {
+      uint32_t c;
+      const uint32_t d = decode_one((uint32_t)c32[i], lds, c);
+      t8[3 * i] = (uint8_t)(d & 0xFu);
+      t8[3 * i + 1] = (uint8_t)(d >> 4 & 0xFu);
+      t8[3 * i + 2] = (uint8_t)(d >> 8);
+      if (WITH_COUNTS) n8[i] = (uint8_t)c;
+      if (WITH_STATS) {
+        bits += c & 3u;
+        unc += c >> 2;
+      }
+    }
+  }
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t base = t * kDecTile + wave * kWaveCw + lane * 4;
     u32x4 v[kGroups];
@@ -714,13 +745,13 @@ KVECC_API int kvecc_golay_encode(const uint8_t *triplets, int32_t *codewords, in
   int64_t done = 0;
   if (aligned(triplets, 4) && aligned(codewords, 16)) {
     int64_t ntiles = m / kEncTile;
-    if (ntiles > 0) {
+    if (ntiles > 0) {  // the tile kernel also takes the tail
       unsigned g = grid_for(ntiles, 1, kEncPerCu);  // grid-strided
       KVECC_LAUNCH(golay_encode_kernel, dim3(g), dim3(kEncBlock), 0, st,
                          reinterpret_cast<const uint32_t *>(triplets),
-                         reinterpret_cast<u32x4 *>(codewords), ntiles, par);
+                         reinterpret_cast<u32x4 *>(codewords), ntiles, m, par);
+      done = m;
     }
-    done = ntiles * kEncTile;
   }
   if (done < m) {
     unsigned g = grid_for(m - done, kBlock);
@@ -749,15 +780,15 @@ KVECC_API int kvecc_golay_decode(const int32_t *codewords, uint8_t *triplets, ui
       auto n = reinterpret_cast<uint32_t *>(counts);
       const dim3 b(kDecBlock);
       if (counts && stats)
-        KVECC_LAUNCH((golay_decode_kernel<true, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<true, true>), dim3(g), b, 0, st, c, t, n, ntiles, m, par, cor, stats);
       else if (counts)
-        KVECC_LAUNCH((golay_decode_kernel<true, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<true, false>), dim3(g), b, 0, st, c, t, n, ntiles, m, par, cor, stats);
       else if (stats)
-        KVECC_LAUNCH((golay_decode_kernel<false, true>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<false, true>), dim3(g), b, 0, st, c, t, n, ntiles, m, par, cor, stats);
       else
-        KVECC_LAUNCH((golay_decode_kernel<false, false>), dim3(g), b, 0, st, c, t, n, ntiles, par, cor, stats);
+        KVECC_LAUNCH((golay_decode_kernel<false, false>), dim3(g), b, 0, st, c, t, n, ntiles, m, par, cor, stats);
+      done = m;  // the tile kernel also takes the tail
     }
-    done = ntiles * kDecTile;
   }
   if (done < m) {
     unsigned g = grid_for(m - done, kBlock);
