@@ -116,6 +116,36 @@ def test_golay_random_vs_oracle(gpu, oracle, m, offset):
     assert st == ost
 
 
+@pytest.mark.parametrize("m", [4096 * 3 + 1, 8192 * 2 + 4095, 44_739_243 // 64])
+@pytest.mark.parametrize("with_counts", [False, True])
+@pytest.mark.parametrize("with_stats", [False, True])
+def test_golay_tile_kernels_take_the_tail(gpu, oracle, m, with_counts, with_stats):
+    """The tile kernels decode / encode the last m % tile codewords themselves
+    (golay.hip), in every counts / statistics instance; lengths past whole
+    decode (4096) and encode (8192) tiles, and 1/64 of config 3's flat M_f."""
+    from kvecc import ops
+    rng = np.random.default_rng(m + 2 * with_counts + with_stats)
+    trip = rng.integers(0, 16, size=(m, 3), dtype=np.int64).astype(np.uint8)
+    cw = torch.empty(m, dtype=torch.int32, device=gpu)
+    ops.golay_encode_into(_t(trip, gpu).view(-1), cw, m)
+    ocw = oracle.golay_encode(trip)
+    assert np.array_equal(_np(cw), ocw)
+    noisy = ocw.astype(np.int64) ^ (rng.random(m) < 0.3) * (1 << rng.integers(0, 24, size=m))
+    noisy[::13] ^= 0x3 << 20  # a second (and third) error on some words
+    noisy[::101] = rng.integers(0, 1 << 24, size=noisy[::101].size)
+    noisy = noisy.astype(np.int32)
+    out = torch.full((m * 3,), 0xEE, dtype=torch.uint8, device=gpu)
+    counts = torch.full((m,), 0xEE, dtype=torch.uint8, device=gpu) if with_counts else None
+    stats = ops.new_stats(gpu) if with_stats else None
+    ops.golay_decode_into(_t(noisy, gpu), out, counts, stats)
+    od, oc, ost = oracle.golay_decode(noisy)
+    assert np.array_equal(_np(out).reshape(-1, 3), od)
+    if with_counts:
+        assert np.array_equal(_np(counts), oc)
+    if with_stats:
+        assert tuple(ops.read_stats(stats)) == tuple(ost)
+
+
 def test_golay_full_config_roundtrip(gpu, oracle):
     """BASELINE config 3 shape with per-head packing: rows of 128 -> 43 codewords."""
     import kvecc
