@@ -394,6 +394,203 @@ __global__ __launch_bounds__(BLOCK) void golay_read_pf2_kernel(ShimTileArgs a, c
   }
 }
 
+// DIRECT: no LDS tile.  Lane l of a wave takes output chunk j = l & 15 (values
+// 8j..8j+7 of a row: one 16-byte store) of row 4i + (l >> 4), i = 0..3, of the
+// wave's 16-row tile: it loads the 4 codewords c0 = 8j/3 .. c0 + 3 of its row
+// (16 bytes at a 4-byte aligned offset; the last lane's 4th is past the row and
+// unused), decodes them, and selects its 8 nibbles with two v_perm.  Each
+// codeword is decoded by up to two lanes; the statistics count it at the lane
+// holding its first nibble.  d = 128 (43 codewords per row), fp16 out, int32 caches.
+// SCHED 0: the product's persistent schedule (PCT static); 1: a full grid.
+// TABK 0: the 32 KiB spread tables; 1: the byte-class tables (golay_bc.h).
+// STG 1 (full grid): the tables come by LDS-DMA, issued first; then the
+// wave's tile loads; a counted vmcnt retires only the DMA before a raw
+// s_barrier, so the tile's HBM loads are in flight while the tables land.
+template <int SCHED, int TABK, int BLOCK, int PCT = 30, int STG = 0>
+__global__ __launch_bounds__(BLOCK) void golay_read_direct_kernel(ShimTileArgs a, const uint16_t *bc16,
+                                                                  const uint16_t *) {
+  using TO = __half;
+  constexpr int kW = BLOCK / kWave;
+  constexpr int kTab = TABK ? (STG ? kBcAlloc : kBcWords) : 8192;
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTab];
+  const uint32_t *tsrc = TABK ? reinterpret_cast<const uint32_t *>(bc16) : a.atab;
+  if (STG == 0) {
+    const u32x4 *s4 = reinterpret_cast<const u32x4 *>(tsrc);
+    u32x4 *d4 = reinterpret_cast<u32x4 *>(tab);
+    for (int i = threadIdx.x; i < kTab / 4; i += BLOCK) d4[i] = s4[i];
+    __syncthreads();
+  }
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  const uint32_t rg = lane >> 4, j = lane & 15;
+  const uint32_t c0 = (8 * j) / 3, f = (8 * j) % 3;
+  const uint32_t selA = f == 0 ? 0x04020100u : f == 1 ? 0x05040201u : 0x06050402u;
+  const uint32_t selB = f == 0 ? 0x05040201u : f == 1 ? 0x06050402u : 0x04020100u;
+  const bool f2 = f == 2;
+  uint32_t own = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (3 * (c0 + k) >= 8 * j && 3 * (c0 + k) <= 8 * j + 7) own |= 1u << k;
+  const uint32_t gw = blockIdx.x * kW + wave, nwaves = gridDim.x * kW;
+  uint32_t u = gw;
+  if (STG == 0 && u >= a.units) return;
+  TileSchedule sched;
+  if (STG == 0 && SCHED == 0) sched.init(a.units, a.dyn, gw, nwaves, lane, PCT);
+  auto issue = [&](const ShimTile &t, u32x4 (&w)[4], float (&sc)[4]) {
+    const bool live = t.row0 >= 0;
+    const int64_t row0 = live ? t.row0 : 0;
+    const uint32_t side = uni(t.side);
+    const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + row0 * (int64_t)a.rowb);
+    const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + row0));
+    const uint32_t nrows = uni(live ? t.rows : 0u);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.rowb), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ss =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = 4 * i + rg;
+      w[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.rowb + 4 * c0, 0, kTileAux));
+      sc[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * r, 0, 0));
+    }
+  };
+  ShimTile cur;
+  u32x4 w[4];
+  float sc[4];
+  if (STG == 1) {
+    static_assert(STG == 0 || SCHED == 1, "LDS-DMA staging: full grid only");
+    const char *src = reinterpret_cast<const char *>(tsrc);
+    for (int c = wave; c < kTab / 256; c += kW)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 1024 * c + 16 * lane),
+                                       reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                           reinterpret_cast<uintptr_t>(tab) + 1024 * c),
+                                       16, 0, 0);
+    const bool active = u < a.units;
+    if (active) {
+      cur = shim_tile(a, u);
+      issue(cur, w, sc);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the DMA (issued first) has landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    if (!active) return;
+  } else {
+    cur = shim_tile(a, u);
+    issue(cur, w, sc);
+  }
+  uint32_t bits = 0, unc = 0;
+  const char *tb = reinterpret_cast<const char *>(tab);
+  for (;;) {
+    const ShimTile t = cur;
+    u32x4 wc[4];
+    float scc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      wc[i] = w[i];
+      scc[i] = sc[i];
+    }
+    bool more = false;
+    if (SCHED == 0) {
+      u = sched.next(u, lane);
+      more = u < a.units;
+      if (more) {
+        cur = shim_tile(a, u);
+        issue(cur, w, sc);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t os = tile_out<TO>(a, t);
+    const bool dead = t.row0 < 0;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t sp[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t cw = wc[i][k];
+        uint32_t n;
+        if (TABK) {
+          sp[k] = bc_decode(tab, cw, n);
+          n = (n & 3u) | (n >> 2) << 6;
+        } else {
+          const uint32_t p = *reinterpret_cast<const uint32_t *>(tb + ((cw << 2) & 0x3FFCu));
+          const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + 16384 + (((cw >> 10) ^ (p >> 18)) & 0x3FFCu));
+          sp[k] = __builtin_amdgcn_bitop3_b32(p, e, 0x000F0F0Fu, 0x28);
+          n = e >> 24;
+        }
+        cnt += (own >> k) & 1u ? n : 0u;
+      }
+      const uint32_t nb[2] = {__builtin_amdgcn_perm(sp[1], sp[0], selA),
+                              __builtin_amdgcn_perm(f2 ? sp[3] : sp[2], f2 ? sp[2] : sp[1], selB)};
+      const uint32_t r = 4 * i + rg;
+      tile_store(os, (r * 128u + 8u * j) * 2u, dq16<TO>(nb, scc[i], dead));
+    }
+    bits += cnt & 63u;
+    unc += cnt >> 6;
+    if (!more) break;
+  }
+  bits = wave_sum(bits);
+  unc = wave_sum(unc);
+  if (lane == 0) {
+    uint64_t *slot = a.stats + (gw % KVECC_STATS_SLOTS) * KVECC_STATS_STRIDE;
+    if (bits) atomicAdd(reinterpret_cast<unsigned long long *>(slot), (unsigned long long)bits);
+    if (unc) atomicAdd(reinterpret_cast<unsigned long long *>(slot + 1), (unsigned long long)unc);
+  }
+}
+
+// PROBE (no decode, WRONG values): the fused read's bytes moved with a given
+// load pattern, to price the pattern itself.  Full grid, one tile per wave,
+// the tile's 16 row scales loaded, 4 KiB stored per tile as the product does.
+//   MODE 0: the tile's 2752 bytes as 16-byte loads at 16-byte aligned offsets
+//           (1 KiB contiguous per wave-instruction; tile bases are 64-byte aligned)
+//   MODE 1: the product's pattern (row r, 4-codeword group q at r * 172 + 16 q)
+//   MODE 2: the direct kernel's (4 codewords from 8j/3 of row 4i + l/16)
+template <int MODE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void golay_read_probe_kernel(ShimTileArgs a, const uint16_t *, const uint16_t *) {
+  constexpr int kW = BLOCK / kWave;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint32_t lane = threadIdx.x % kWave;
+  const uint32_t u = blockIdx.x * kW + wave;
+  if (u >= a.units) return;
+  const ShimTile t = shim_tile(a, u);
+  const bool live = t.row0 >= 0;
+  const int64_t row0 = live ? t.row0 : 0;
+  const uint32_t side = uni(t.side);
+  const char *base = uni(reinterpret_cast<const char *>(a.cache[side]) + row0 * (int64_t)a.rowb);
+  const char *sbase = uni(reinterpret_cast<const char *>(a.scales[side] + row0));
+  const uint32_t nrows = uni(live ? t.rows : 0u);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)(nrows * a.rowb), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ss =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(sbase), 0, (int)(4 * nrows), 0x00020000);
+  u32x4 acc = {lane, 0u, 0u, 0u};
+  auto mix = [&](const u32x4 &v) { acc = u32x4{acc.x ^ v.x, acc.y ^ v.y, acc.z ^ v.z, acc.w ^ v.w}; };
+  if (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      mix(__builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 * i + 16 * lane, 0, kTileAux)));
+  } else if (MODE == 1) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const uint32_t f = lane + 64 * i, r = f / 11, q = f - 11 * r;
+      if (f < 176)
+        mix(__builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.rowb + 16 * q, 0, kTileAux)));
+    }
+  } else {
+    const uint32_t j = lane & 15, c0 = (8 * j) / 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = 4 * i + (lane >> 4);
+      mix(__builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.rowb + 4 * c0, 0, kTileAux)));
+    }
+  }
+  const uint32_t sc = __builtin_amdgcn_raw_buffer_load_b32(ss, 4 * (lane & 15), 0, 0);
+  const __amdgpu_buffer_rsrc_t os = tile_out<__half>(a, t);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    tile_store(os, 1024 * i + 16 * lane, u32x4{acc.x ^ sc, acc.y ^ (uint32_t)i, acc.z, acc.w});
+}
+
 struct Variant {
   const char *name;
   void (*kern)(ShimTileArgs, const uint16_t *, const uint16_t *);
@@ -494,6 +691,24 @@ static const Variant kVariants[] = {
     {"pk_full1_bc", golay_read_exp_kernel<1, 1, 0, 5, 0, 0, 512, true>, 1, 1, 512, 1},
     {"pk_full2_bc", golay_read_exp_kernel<1, 2, 0, 5, 0, 0, 512, true>, 1, 2, 512, 1},
     {"pk_pers_bc_b256_p30", golay_read_exp_kernel<0, 1, 0, 5, 0, 0, 256, true, 30>, 0, 1, 256, 1},
+    // no LDS tile (golay_read_direct_kernel)
+    {"direct_pers_b256_p30", golay_read_direct_kernel<0, 0, 256, 30>, 0, 1, 256, 0},
+    {"direct_pers_b512_p30", golay_read_direct_kernel<0, 0, 512, 30>, 0, 1, 512, 0},
+    {"direct_full_b512", golay_read_direct_kernel<1, 0, 512>, 1, 1, 512, 0},
+    {"direct_full_bc_b512", golay_read_direct_kernel<1, 1, 512>, 1, 1, 512, 1},
+    {"direct_full_bc_b256", golay_read_direct_kernel<1, 1, 256>, 1, 1, 256, 1},
+    {"direct_pers_bc_b256_p30", golay_read_direct_kernel<0, 1, 256, 30>, 0, 1, 256, 1},
+    {"direct_full_bc_dma_b512", golay_read_direct_kernel<1, 1, 512, 30, 1>, 1, 1, 512, 1},
+    {"direct_full_bc_dma_b256", golay_read_direct_kernel<1, 1, 256, 30, 1>, 1, 1, 256, 1},
+    {"direct_full_bc_dma_b1024", golay_read_direct_kernel<1, 1, 1024, 30, 1>, 1, 1, 1024, 1},
+    {"direct_full_dma_b512", golay_read_direct_kernel<1, 0, 512, 30, 1>, 1, 1, 512, 0},
+    // load-pattern probes (no decode)
+    {"probe_aligned_b256", golay_read_probe_kernel<0, 256>, 1, 1, 256},
+    {"probe_rows_b256", golay_read_probe_kernel<1, 256>, 1, 1, 256},
+    {"probe_direct_b256", golay_read_probe_kernel<2, 256>, 1, 1, 256},
+    {"probe_aligned_b512", golay_read_probe_kernel<0, 512>, 1, 1, 512},
+    {"probe_rows_b512", golay_read_probe_kernel<1, 512>, 1, 1, 512},
+    {"probe_direct_b512", golay_read_probe_kernel<2, 512>, 1, 1, 512},
     {"pf2", golay_read_pf2_kernel<512, false, 65>, 0, 1, 512},
     {"pf2_b256", golay_read_pf2_kernel<256, false, 65>, 0, 1, 256},
     {"pf2_p50", golay_read_pf2_kernel<512, false, 50>, 0, 1, 512},
