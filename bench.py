@@ -484,12 +484,12 @@ def fused_decode_bench(dev, steps, warmup, packed=False):
             "bytes_per_launch": rows * bytes_per_row,
             "bytes_per_token_row": bytes_per_row, "hbm_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
             "write_share": 2 * D / bytes_per_row,
-            "ceiling_note": "this byte mix (59 % writes) through a random block table runs at best 147 us "
-                            "(0.77) in a no-decode probe (profiles/r03/fused/store_perm.log); the persistent "
-                            "grid the 32 KiB tables need: 159 us with no table lookups (0.71, "
-                            "profiles/r04/fused/read_exp_ab_a.log); a full grid with the tables made "
-                            "algebraic: 155 us with no error path, 160-182 us with one "
-                            "(profiles/r05/golay_tf_ab2.log)",
+            "ceiling_note": "moving exactly these bytes (the same tiles through the same block table, the "
+                            "row scales, 4 KiB stores per tile) with no decode at all takes 153.6-157.3 us "
+                            "(0.73-0.74) in the same process as the kernel's 159.0 "
+                            "(profiles/r06/golay_read_direct_probe.txt); 128-byte aligned 2816-byte units with "
+                            "no scales ran 147 us (profiles/r03/fused/store_perm.log); every decode structure "
+                            "tried lands at 157-162 us (profiles/r06/golay_read_byteclass.txt)",
             "timing": f"HIP events carried by the dispatch, mean of {steps} launches after >= {warmup} warm-up calls and >= 0.25 s"}
 
 
