@@ -709,6 +709,8 @@ static const Variant kVariants[] = {
     {"probe_aligned_b512", golay_read_probe_kernel<0, 512>, 1, 1, 512},
     {"probe_rows_b512", golay_read_probe_kernel<1, 512>, 1, 1, 512},
     {"probe_direct_b512", golay_read_probe_kernel<2, 512>, 1, 1, 512},
+    {"pk_probe_aligned_b256", golay_read_probe_kernel<0, 256>, 1, 1, 256},
+    {"pk_probe_aligned_b512", golay_read_probe_kernel<0, 512>, 1, 1, 512},
     {"pf2", golay_read_pf2_kernel<512, false, 65>, 0, 1, 512},
     {"pf2_b256", golay_read_pf2_kernel<256, false, 65>, 0, 1, 256},
     {"pf2_p50", golay_read_pf2_kernel<512, false, 50>, 0, 1, 512},
