@@ -211,9 +211,13 @@ struct Chunk {
   // KiB of LDS instead of 32, conflict-free parity gathers, 2 more VALU per
   // codeword.  Slower at every split and rows-in-flight count tried (MHA
   // int32 75.0 vs 73.2 us, packed 65.2 vs 59.9; profiles/r06/attn/
-  // golay_split_parity_ab.txt): the kernel is bound by its VALU work
-  template <bool SP = false>
+  // golay_split_parity_ab.txt): the kernel is bound by its VALU work.
+  // DEC: 0 the product's decode, 1 split parity (SP above), 2 a probe that
+  // keeps the decode's VALU but skips its two LDS gathers (WRONG values; only
+  // tools/exp/attn_exp.hip instantiates 1 and 2)
+  template <int DEC = 0>
   __device__ __forceinline__ void decode(const h84_lut_t *lut, const uint32_t *gtab, float *v) const {
+    constexpr bool SP = DEC == 1;
     if constexpr (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
@@ -230,13 +234,15 @@ struct Chunk {
         // (0x28 = (S0 ^ S1) & S2) and a shift
         const char *tb = reinterpret_cast<const char *>(gtab);
         uint32_t p;
-        if (SP)
+        if (DEC == 2)
+          p = w[k] & 0x3FFCu;
+        else if (SP)
           p = *reinterpret_cast<const uint32_t *>(tb + 16384 + (w[k] & 0xFCu)) ^
               *reinterpret_cast<const uint32_t *>(tb + 16384 + 256 + ((w[k] >> 6) & 0xFCu));
         else
           p = *reinterpret_cast<const uint32_t *>(tb + (w[k] & 0x3FFCu));
         const uint32_t off = __builtin_amdgcn_bitop3_b32(w[k], p, 0x03FFC000u, 0x28) >> 12;
-        const uint32_t e = *reinterpret_cast<const uint32_t *>(tb + (SP ? 0 : 16384) + off);
+        const uint32_t e = DEC == 2 ? off : *reinterpret_cast<const uint32_t *>(tb + (SP ? 0 : 16384) + off);
         // corrected nibbles: (p ^ e) & 0xF0000F0F; the conversions are written
         // out because the compiler otherwise re-extracts each nibble with a
         // shift and a mask.  The third value comes out as 16 n (byte 3 = n << 4):
@@ -459,8 +465,9 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
 // loaded and decoded once and used G times (a dot product, an online softmax
 // state and an accumulator per head), where one workgroup per query head read
 // and decoded every cache row H/Hkv times.
-template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1, int UR = 0, bool SP = false>
+template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1, int UR = 0, int DEC = 0>
 __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
+  constexpr bool SP = DEC == 1;  // Chunk::decode's DEC (experiment forks only)
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
@@ -655,7 +662,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       for (int j = 0; j < G; ++j) part[j] = 0.0f;
       if (live) {
         float kv[E];
-        kc[u].template decode<SP>(lut, gtab, kv);
+        kc[u].template decode<DEC>(lut, gtab, kv);
 #pragma unroll
         for (int j = 0; j < G; ++j) {
           part[j] = dot<E>(qv[j], kv);
@@ -700,7 +707,7 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         float vv[E];
-        vc[u].template decode<SP>(lut, gtab, vv);
+        vc[u].template decode<DEC>(lut, gtab, vv);
 #pragma unroll
         for (int j = 0; j < G; ++j) axpy<E>(acc[j], ps[j][u], vv);
       }

@@ -31,14 +31,15 @@ static void launch_mfma_g(int codec, const AttnArgs &a, int64_t batch, hipStream
 }  // namespace kvecc
 
 // Golay MHA split kernel (fp16 queries, G = 1, fused combine) with the parity
-// half as two 64-entry tables (sp = 1: 16.5 KiB of LDS instead of 32), u rows
+// half as two 64-entry tables (sp = 1: 16.5 KiB of LDS instead of 32; sp = 3:
+// no table gathers at all, a probe), u rows
 // in flight (0: the product's), per_cu workgroups per CU in the split choice
-template <int CODEC, int U, bool SP, int VEC0 = 0>
+template <int CODEC, int U, int DEC, int VEC0 = 0>
 static void launch_gsp(const kvecc::AttnArgs &a, dim3 grid, hipStream_t st) {
   using namespace kvecc;
   constexpr int VEC = VEC0 ? VEC0 : CODEC == KVECC_CODEC_GOLAY ? kGolayVec : kGolayPackedVec;
   constexpr int W = VEC == 6 ? 8 : 16;  // lanes per token row: 43 codewords / VEC, rounded up to a power of two
-  KVECC_LAUNCH((paged_attn_split_kernel<__half, CODEC, VEC, W, true, 1, U, SP>), grid, dim3(kBlock), 0, st, a);
+  KVECC_LAUNCH((paged_attn_split_kernel<__half, CODEC, VEC, W, true, 1, U, DEC>), grid, dim3(kBlock), 0, st, a);
 }
 
 
@@ -195,7 +196,7 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_gsp(
   hipStream_t st = as_stream(stream);
 #define GSP(PK, UU, S)                                                                             \
   if (packed == PK && u == UU && sp == S) {                                                        \
-    launch_gsp<PK ? KVECC_CODEC_GOLAY_PACKED : KVECC_CODEC_GOLAY, UU, S>(a, grid, st);            \
+    launch_gsp<PK ? KVECC_CODEC_GOLAY_PACKED : KVECC_CODEC_GOLAY, UU, (int)S>(a, grid, st);       \
     return check_launch("exp_paged_attention_gsp");                                                \
   }
   GSP(0, 0, false) GSP(0, 0, true) GSP(0, 3, true) GSP(0, 4, true) GSP(0, 3, false)
@@ -207,6 +208,12 @@ __attribute__((visibility("default"))) int kvecc_exp_paged_attention_gsp(
     return check_launch("exp_paged_attention_gsp");
   }
   GSP(1, 0, false) GSP(1, 0, true) GSP(1, 2, true) GSP(1, 3, true)
+  // sp 3: the product's kernel with its decode's two LDS gathers skipped (WRONG values: prices them)
+  if (sp == 3 && u == 0) {
+    if (packed) launch_gsp<KVECC_CODEC_GOLAY_PACKED, 0, 2>(a, grid, st);
+    else launch_gsp<KVECC_CODEC_GOLAY, 0, 2>(a, grid, st);
+    return check_launch("exp_paged_attention_gsp");
+  }
 #undef GSP
   return set_error(KVECC_EINVAL, "no gsp instance");
 }
