@@ -428,7 +428,12 @@ __device__ __forceinline__ uint32_t type_pack4(uint32_t t) {
 
 constexpr int kHpBlock = 256;
 
-// a lane owns 16 values: one 16-byte codeword access, 8 bytes of nibbles
+// a lane owns 16 values: one 16-byte codeword access, 8 bytes of nibbles.
+// Grid-stride at 64 workgroups per CU (kHpEncPerCu): 32.4-33.1 us against
+// 33.6-33.8 at 32, and at or within noise of full grids with 1, 2 or 4 chunks
+// per lane (34.3 / 32.6 / 34.7) at config 2's 134 M values
+// (profiles/r06/h84_packed_encode_grid.txt, tools/exp/h84_pk_enc_exp.hip)
+constexpr int kHpEncPerCu = 64;
 __global__ __launch_bounds__(kHpBlock) void h84_encode_packed_kernel(const u32x2 *__restrict__ nib,
                                                                      u32x4 *__restrict__ cw,
                                                                      int64_t n16) {
@@ -640,7 +645,7 @@ KVECC_API int kvecc_hamming84_encode_packed(const uint8_t *nibbles, uint8_t *cod
   if (aligned(nibbles, 8) && aligned(codewords, 16)) {
     const int64_t n16 = n / 16;
     if (n16 > 0)
-      KVECC_LAUNCH(h84_encode_packed_kernel, dim3(grid_for(n16, kHpBlock, 32)), dim3(kHpBlock),
+      KVECC_LAUNCH(h84_encode_packed_kernel, dim3(grid_for(n16, kHpBlock, kHpEncPerCu)), dim3(kHpBlock),
                          0, st, reinterpret_cast<const u32x2 *>(nibbles),
                          reinterpret_cast<u32x4 *>(codewords), n16);
     done = n16 * 16;
