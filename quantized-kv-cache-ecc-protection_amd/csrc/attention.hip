@@ -150,8 +150,16 @@ struct Chunk {
       }
     } else {
       const uint32_t off = ((uint32_t)row * (uint32_t)a.g + VEC * c) * 4u;
+      if constexpr (VEC == 3) {  // one 12-byte load: 71.9 vs 72.6 us per MHA call against
+                                 // three dword loads (profiles/r06/attn/golay_no_gather_probe.txt)
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+        w[0] = v[0] << 2;
+        w[1] = v[1] << 2;
+        w[2] = v[2] << 2;
+      } else {
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0) << 2;
+        for (int k = 0; k < VEC; ++k) w[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * k, 0, 0) << 2;
+      }
     }
   }
   __device__ __forceinline__ void load(const AttnArgs &a, const void *cache, int64_t row, int c) {
@@ -212,12 +220,12 @@ struct Chunk {
   // codeword.  Slower at every split and rows-in-flight count tried (MHA
   // int32 75.0 vs 73.2 us, packed 65.2 vs 59.9; profiles/r06/attn/
   // golay_split_parity_ab.txt): the kernel is bound by its VALU work.
-  // DEC: 0 the product's decode, 1 split parity (SP above), 2 a probe that
-  // keeps the decode's VALU but skips its two LDS gathers (WRONG values; only
-  // tools/exp/attn_exp.hip instantiates 1 and 2)
+  // DEC bits (0: the product; only tools/exp/attn_exp.hip sets any): 1 split
+  // parity (SP above), 2 a probe that keeps the decode's VALU but skips its two
+  // LDS gathers and the tables' staging and LDS (WRONG values)
   template <int DEC = 0>
   __device__ __forceinline__ void decode(const h84_lut_t *lut, const uint32_t *gtab, float *v) const {
-    constexpr bool SP = DEC == 1;
+    constexpr bool SP = (DEC & 1) != 0;
     if constexpr (CODEC == KVECC_CODEC_H84) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
@@ -234,7 +242,7 @@ struct Chunk {
         // (0x28 = (S0 ^ S1) & S2) and a shift
         const char *tb = reinterpret_cast<const char *>(gtab);
         uint32_t p;
-        if (DEC == 2)
+        if (DEC & 2)
           p = w[k] & 0x3FFCu;
         else if (SP)
           p = *reinterpret_cast<const uint32_t *>(tb + 16384 + (w[k] & 0xFCu)) ^
@@ -242,7 +250,7 @@ struct Chunk {
         else
           p = *reinterpret_cast<const uint32_t *>(tb + (w[k] & 0x3FFCu));
         const uint32_t off = __builtin_amdgcn_bitop3_b32(w[k], p, 0x03FFC000u, 0x28) >> 12;
-        const uint32_t e = DEC == 2 ? off : *reinterpret_cast<const uint32_t *>(tb + (SP ? 0 : 16384) + off);
+        const uint32_t e = (DEC & 2) ? off : *reinterpret_cast<const uint32_t *>(tb + (SP ? 0 : 16384) + off);
         // corrected nibbles: (p ^ e) & 0xF0000F0F; the conversions are written
         // out because the compiler otherwise re-extracts each nibble with a
         // shift and a mask.  The third value comes out as 16 n (byte 3 = n << 4):
@@ -467,7 +475,7 @@ __device__ void combine_if_last(const AttnArgs &a, int64_t bh0, float *wt) {
 // and decoded every cache row H/Hkv times.
 template <typename T, int CODEC, int VEC, int W, bool BUF, int G = 1, int UR = 0, int DEC = 0>
 __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
-  constexpr bool SP = DEC == 1;  // Chunk::decode's DEC (experiment forks only)
+  constexpr bool SP = (DEC & 1) != 0;  // Chunk::decode's DEC bits (experiment forks only)
   using C = Chunk<CODEC, VEC>;
   constexpr int E = C::E;
   constexpr int TP = kBlock / W;  // token rows per pass (one per lane group)
@@ -485,7 +493,9 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
   // tables the block-table slice (before the copy) and the merge buffer (after
   // the loop) live in the same LDS, which keeps 4 workgroups per CU.
   constexpr bool kSpread = is_golay(CODEC);
-  constexpr int kTabWords = !is_golay(CODEC) ? 4 : SP ? 4096 + 128 : kSpread ? 8192 : 4096;
+  // (DEC 2, the no-lookup probe: no tables, only the aliased block-table slice and merge buffer)
+  constexpr int kProbeWords = TP * W * E > kMaxSplit + 1 ? TP * W * E : kMaxSplit + 1;
+  constexpr int kTabWords = !is_golay(CODEC) ? 4 : (DEC & 2) ? kProbeWords : SP ? 4096 + 128 : kSpread ? 8192 : 4096;
   static_assert(!kSpread || (TP * W * E <= kTabWords && kMaxSplit + 1 <= kTabWords), "LDS aliasing");
   __shared__ __attribute__((aligned(16))) uint32_t gtab[kTabWords];
   __shared__ float red_own[kSpread ? 1 : TP * W * E];  // per-group acc
@@ -547,7 +557,9 @@ __global__ __launch_bounds__(kBlock) void paged_attn_split_kernel(AttnArgs a) {
       rows[i] = row;
     }
   }
-  if (kSpread && SP) {
+  if (kSpread && (DEC & 2)) {
+    __syncthreads();  // blks (aliased) fully read; the probe stages no tables
+  } else if (kSpread && SP) {
     __syncthreads();  // blks (aliased) fully read
     // the correction half, then T0[k] = P(k) and T1[k] = P(k << 6)
     const u32x4 *src = reinterpret_cast<const u32x4 *>(a.atab_x + 4096);
