@@ -45,7 +45,11 @@ def main():
         gsp.argtypes = [ci, ci, ci, ci] + [vp] * 8 + [i64] * 8 + [f32, vp, vp]
         return golay_split_parity(dev, gsp, sys.argv[2:] or ["golay", "golay_packed"])
     for codec in (sys.argv[1:] or ["hamming84", "golay_packed", "golay"]):
-        for heads, kvh, variants in ((32, 32, VARIANTS), (32, 8, GQA_VARIANTS)):
+        sets = ((32, 32, VARIANTS), (32, 8, GQA_VARIANTS))
+        if os.environ.get("GQA_SET"):  # "label:G:per_cu:fused,...": GQA 32q/8kv only
+            sets = ((32, 8, [(c.split(":")[0], *(int(x) for x in c.split(":")[1:]))
+                             for c in os.environ["GQA_SET"].split(",")]),)
+        for heads, kvh, variants in sets:
             g = torch.Generator(device=dev).manual_seed(0)
             nb = CTX // BS
             blocks = B * nb
