@@ -46,9 +46,12 @@ def main():
         return golay_split_parity(dev, gsp, sys.argv[2:] or ["golay", "golay_packed"])
     for codec in (sys.argv[1:] or ["hamming84", "golay_packed", "golay"]):
         sets = ((32, 32, VARIANTS), (32, 8, GQA_VARIANTS))
-        if os.environ.get("GQA_SET"):  # "label:G:per_cu:fused,...": GQA 32q/8kv only
-            sets = ((32, 8, [(c.split(":")[0], *(int(x) for x in c.split(":")[1:]))
-                             for c in os.environ["GQA_SET"].split(",")]),)
+        def parse_set(env):  # "label:G:per_cu:fused,..."
+            return [(c.split(":")[0], *(int(x) for x in c.split(":")[1:])) for c in os.environ[env].split(",")]
+        if os.environ.get("GQA_SET") or os.environ.get("MHA_SET"):  # only the sets given
+            sets = tuple(x for x in ((32, 32, parse_set("MHA_SET") if os.environ.get("MHA_SET") else None),
+                                     (32, 8, parse_set("GQA_SET") if os.environ.get("GQA_SET") else None))
+                         if x[2])
         for heads, kvh, variants in sets:
             g = torch.Generator(device=dev).manual_seed(0)
             nb = CTX // BS
